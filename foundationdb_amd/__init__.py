@@ -1,0 +1,22 @@
+"""MI355X-native batched CRC-32C for FoundationDB's crc32c_append() call sites.
+
+The product is the C-ABI shared library ``foundationdb_amd/lib/libfdb_crc32c.so``
+(header ``include/fdb_crc32c.h``).  This package is the Python host mirror of
+that boundary: ``crc32c_append`` with the reference's signature semantics and
+batched device entry points over torch-allocated HBM buffers.
+"""
+from .crc32c import (  # noqa: F401
+    CRC32CError,
+    LIB_PATH,
+    batch_fixed,
+    batch_varlen,
+    crc32c_append,
+    crc32c_append_zeros,
+    crc32c_combine,
+    crc32c_shift,
+    fill_splitmix64,
+    gpu_init,
+    lib,
+)
+
+__version__ = "0.1.0"

@@ -1,0 +1,115 @@
+// Host-side scalar CRC-32C: the link-compatible crc32c_append symbol plus the
+// GF(2) shift/combine helpers the batched API needs to merge partial results.
+//
+// crc32c_append has the semantics of contrib/crc32/crc32c.cpp:346-356 (seed
+// pre-inversion :197, post-inversion :310, any alignment, length 0 returns the
+// seed).  It exists so a FoundationDB build can link this library in place of
+// contrib/crc32 for its single-buffer call sites; the batched GPU entry points
+// never route through it.
+//
+// Implementation: SSE4.2 crc32q over three independent streams of kBlock
+// bytes each, merged with byte-indexed tables of x^(8*kBlock) (own generator,
+// crc32c_math.h); a sliced-table fallback when the CPU lacks SSE4.2.
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <nmmintrin.h>
+#endif
+
+#include "crc32c_math.h"
+
+namespace fdbcrc {
+namespace {
+
+constexpr size_t kBlock = 1024;  // bytes per stream per interleaved round
+
+struct HostTables {
+	uint32_t slice[8][256];     // slice[k][b]: byte b followed by k zero bytes
+	uint32_t merge[4][256];     // x^(8*kBlock) as byte tables
+	bool sse42 = false;
+	HostTables() {
+		for (uint32_t b = 0; b < 256; ++b) slice[0][b] = byte_step(b);
+		for (int k = 1; k < 8; ++k)
+			for (uint32_t b = 0; b < 256; ++b) slice[k][b] = (slice[k - 1][b] >> 8) ^ slice[0][slice[k - 1][b] & 0xffu];
+		mul_tables_byte(xpow8(kBlock), merge);
+#if defined(__x86_64__)
+		unsigned a, b, c, d;
+		if (__get_cpuid(1, &a, &b, &c, &d)) sse42 = (c & bit_SSE4_2) != 0;
+#endif
+	}
+};
+
+const HostTables& tables() {
+	static const HostTables t;
+	return t;
+}
+
+inline uint32_t apply_merge(const HostTables& t, uint32_t r) {
+	return t.merge[0][r & 0xff] ^ t.merge[1][(r >> 8) & 0xff] ^ t.merge[2][(r >> 16) & 0xff] ^ t.merge[3][r >> 24];
+}
+
+inline uint64_t load64(const uint8_t* p) {
+	uint64_t v;
+	memcpy(&v, p, 8);
+	return v;
+}
+
+uint32_t raw_sliced(const HostTables& t, uint32_t s, const uint8_t* p, size_t n) {
+	for (; n >= 8; n -= 8, p += 8) {
+		const uint64_t v = load64(p) ^ s;
+		s = t.slice[7][v & 0xff] ^ t.slice[6][(v >> 8) & 0xff] ^ t.slice[5][(v >> 16) & 0xff] ^
+		    t.slice[4][(v >> 24) & 0xff] ^ t.slice[3][(v >> 32) & 0xff] ^ t.slice[2][(v >> 40) & 0xff] ^
+		    t.slice[1][(v >> 48) & 0xff] ^ t.slice[0][v >> 56];
+	}
+	for (; n; --n) s = (s >> 8) ^ t.slice[0][(s ^ *p++) & 0xff];
+	return s;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("sse4.2"))) uint32_t raw_sse42(const HostTables& t, uint32_t s, const uint8_t* p, size_t n) {
+	while (n && (reinterpret_cast<uintptr_t>(p) & 7)) {
+		s = _mm_crc32_u8(s, *p++);
+		--n;
+	}
+	uint64_t s0 = s;
+	while (n >= 3 * kBlock) {
+		uint64_t s1 = 0, s2 = 0;
+		const uint8_t* q = p;
+		for (const uint8_t* end = p + kBlock; q < end; q += 8) {
+			s0 = _mm_crc32_u64(s0, load64(q));
+			s1 = _mm_crc32_u64(s1, load64(q + kBlock));
+			s2 = _mm_crc32_u64(s2, load64(q + 2 * kBlock));
+		}
+		s0 = apply_merge(t, apply_merge(t, (uint32_t)s0) ^ (uint32_t)s1) ^ (uint32_t)s2;
+		p += 3 * kBlock;
+		n -= 3 * kBlock;
+	}
+	for (; n >= 8; n -= 8, p += 8) s0 = _mm_crc32_u64(s0, load64(p));
+	uint32_t r = (uint32_t)s0;
+	for (; n; --n) r = _mm_crc32_u8(r, *p++);
+	return r;
+}
+#endif
+
+}  // namespace
+}  // namespace fdbcrc
+
+extern "C" {
+
+uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length) {
+	const fdbcrc::HostTables& t = fdbcrc::tables();
+#if defined(__x86_64__)
+	if (t.sse42) return ~fdbcrc::raw_sse42(t, ~crc, input, length);
+#endif
+	return ~fdbcrc::raw_sliced(t, ~crc, input, length);
+}
+
+uint32_t crc32c_shift(uint32_t reg, uint64_t nbytes) { return fdbcrc::gf2_mul(reg, fdbcrc::xpow8(nbytes)); }
+
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) { return crc_b ^ crc32c_shift(crc_a, len_b); }
+
+uint32_t crc32c_append_zeros(uint32_t crc, uint64_t nzeros) { return ~crc32c_shift(~crc, nzeros); }
+
+}  // extern "C"

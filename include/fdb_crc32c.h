@@ -1,0 +1,95 @@
+/*
+ * fdb_crc32c.h -- C ABI of the MI355X batched CRC-32C engine.
+ *
+ * Drop-in boundary for FoundationDB's CRC-32C path.  The reference exposes a
+ * single C-linkage function,
+ *     extern "C" uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length);
+ * declared at contrib/crc32/include/crc32/crc32c.h:36-39 and implemented at
+ * contrib/crc32/crc32c.cpp:346-356, from the static library `crc32`
+ * (contrib/crc32/CMakeLists.txt:1) that flow links PUBLIC
+ * (flow/CMakeLists.txt:125).  Every caller loops it one buffer at a time:
+ *   - SQLite page codec, 4088 B, seed 0xfdbeefdb  (fdbserver/kvstore/KeyValueStoreSQLite.cpp:118-129)
+ *   - AsyncFileWriteChecker, 4096 B pages, seed 0xab12fd93 (fdbrpc/AsyncFileWriteChecker.h:283-331)
+ *   - DiskQueue V1 pages, 4092 B, seed 0xfdbeefdb  (fdbserver/kvstore/DiskQueue.cpp:1083-1085)
+ *   - FileTransfer chained 8 KiB reads, seed 0      (fdbrpc/FileTransfer.cpp:29-37)
+ *
+ * This library exports that symbol unchanged (host, synchronous) and adds the
+ * batched entry points the reference lacks.  All checksums are bit-identical
+ * to crc32c_append for every (seed, bytes, length), including length 0
+ * (returns the seed) and any alignment.
+ *
+ * Conventions: plain pointers and sizes only.  `d_` pointers are device
+ * (HBM) pointers of the current HIP device; `h_` pointers are host pointers.
+ * `stream` is a hipStream_t passed as void* (NULL = the legacy default
+ * stream).  Device calls are asynchronous on `stream` and return an int
+ * status: 0 on success, a negative FDB_CRC32C_E* code on failure (never a
+ * silent fallback -- there is no CPU path behind the device entry points).
+ */
+#ifndef FDB_CRC32C_H
+#define FDB_CRC32C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDB_CRC32C_OK 0
+#define FDB_CRC32C_EINVAL (-1)  /* bad argument (null pointer with count>0, misaligned workspace, ...) */
+#define FDB_CRC32C_ENODEV (-2)  /* no HIP device / gfx950 code object not loadable */
+#define FDB_CRC32C_EHIP (-3)    /* a HIP runtime call failed; see crc32c_gpu_last_error() */
+#define FDB_CRC32C_ENOMEM (-4)  /* device or pinned host allocation failed */
+
+/* ---- Scalar, host: the reference symbol -------------------------------- */
+
+/* Replaces contrib/crc32/include/crc32/crc32c.h:36-39 (impl crc32c.cpp:346-356).
+ * Same name, arguments, return value and total behaviour. */
+uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length);
+
+/* ---- GF(2) helpers, host ----------------------------------------------- */
+
+/* Raw register times x^(8*nbytes) mod P: the zeros operator that the
+ * reference applies by table in shift_crc (contrib/crc32/crc32c.cpp:175-178). */
+uint32_t crc32c_shift(uint32_t reg, uint64_t nbytes);
+
+/* crc32c_append(s, A||B) from crc_a = crc32c_append(s, A) and
+ * crc_b = crc32c_append(0, B).  Lets independently checksummed chunks
+ * reproduce the reference's chained form (fdbrpc/FileTransfer.cpp:29-37). */
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* crc32c_append(crc, <nzeros zero bytes>) in O(log nzeros). */
+uint32_t crc32c_append_zeros(uint32_t crc, uint64_t nzeros);
+
+/* ---- Batched, device-resident ------------------------------------------ */
+
+/* Prepare the current device (upload operator tables).  Optional: every
+ * device entry point does it on first use, but calling it up front keeps the
+ * one synchronous upload out of a stream capture.  Thread-safe. */
+int crc32c_gpu_init(void);
+
+/* Buffer i (0 <= i < count) is the `length` bytes at d_base + i*stride.
+ * Seed of buffer i: d_seeds ? d_seeds[i] : seed.  Writes d_out[i].
+ * Replaces `for i: out[i] = crc32c_append(seed, base + i*stride, length)`,
+ * the loop of AsyncFileWriteChecker::updateChecksumHistory
+ * (fdbrpc/AsyncFileWriteChecker.h:283-331) and of a whole-file page scan
+ * (SQLiteDB::checkAllPageChecksums, KeyValueStoreSQLite.cpp:1378-1470). */
+int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
+                           const uint32_t* d_seeds, uint32_t* d_out, void* stream);
+
+/* Buffer i is the d_lengths[i] bytes at d_base + d_offsets[i] (any alignment,
+ * any order, overlaps allowed).  Seed as above.  Writes d_out[i]. */
+int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                            uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
+
+/* Text of the last error recorded on the calling thread ("" if none). */
+const char* crc32c_gpu_last_error(void);
+
+/* Library build identification, e.g. "fdb_crc32c 0.1 gfx950". */
+const char* crc32c_gpu_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FDB_CRC32C_H */

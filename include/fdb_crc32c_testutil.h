@@ -1,0 +1,16 @@
+/* fdb_crc32c_testutil.h -- synthetic data generation for tests and bench.py.
+ * Not part of the checksum path. */
+#ifndef FDB_CRC32C_TESTUTIL_H
+#define FDB_CRC32C_TESTUTIL_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* d_dst[k] = splitmix64 word k of the stream seeded with `state`
+ * (BASELINE.md generator: z = state + (k+1)*0x9E3779B97F4A7C15, then the
+ * standard splitmix64 finaliser).  Asynchronous on `stream` (hipStream_t). */
+int crc32c_testutil_fill_splitmix64(void* d_dst, uint64_t nwords, uint64_t state, void* stream);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,143 @@
+"""ctypes bindings for the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Two libraries, both built by oracle/Makefile:
+  * liboracle_crc32c.so: our C restatement of contrib/crc32 (crc32c_oracle.c).
+  * _ref/libcrc32c_ref.so: the reference's crc32c.cpp compiled unmodified
+    (present wherever `make -C oracle` ran with /root/reference mounted; the
+    .so travels to the GPU box with the repo snapshot).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(_HERE, "liboracle_crc32c.so")
+REF_SO = os.path.join(_HERE, "_ref", "libcrc32c_ref.so")
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _ptr(a, t):
+    if a is None:
+        return None
+    return a.ctypes.data_as(t)
+
+
+class _Lib:
+    def __init__(self, path, symbol):
+        self.path = path
+        self.lib = ctypes.CDLL(path)
+        self.fn = getattr(self.lib, symbol)
+        self.fn.restype = ctypes.c_uint32
+        self.fn.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+
+    def append(self, crc, data):
+        if isinstance(data, np.ndarray):
+            data = np.ascontiguousarray(data, dtype=np.uint8)
+            return self.fn(crc & 0xFFFFFFFF, data.ctypes.data, data.nbytes)
+        b = bytes(data)
+        return self.fn(crc & 0xFFFFFFFF, b, len(b))
+
+
+_oracle = None
+_ref = None
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        _oracle = _Lib(ORACLE_SO, "oracle_crc32c_append")
+        L = _oracle.lib
+        L.oracle_crc32c_bitwise.restype = ctypes.c_uint32
+        L.oracle_crc32c_bitwise.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_crc32c_shift.restype = ctypes.c_uint32
+        L.oracle_crc32c_shift.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+        L.oracle_crc32c_combine.restype = ctypes.c_uint32
+        L.oracle_crc32c_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        L.oracle_crc32c_batch_fixed.restype = None
+        L.oracle_crc32c_batch_fixed.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_crc32c_batch_varlen.restype = None
+        L.oracle_crc32c_batch_varlen.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_splitmix64_fill.restype = None
+        L.oracle_splitmix64_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
+    return _oracle
+
+
+def reference_available():
+    return os.path.exists(REF_SO)
+
+
+def reference():
+    """The reference's own crc32c_append (contrib/crc32/crc32c.cpp:346-356)."""
+    global _ref
+    if _ref is None:
+        if not os.path.exists(REF_SO):
+            raise FileNotFoundError(REF_SO + " (run `make -C oracle` where /root/reference exists)")
+        _ref = _Lib(REF_SO, "crc32c_append")
+    return _ref
+
+
+def crc32c(crc, data):
+    return oracle().append(crc, data)
+
+
+def crc32c_bitwise(crc, data):
+    b = bytes(data)
+    return oracle().lib.oracle_crc32c_bitwise(crc & 0xFFFFFFFF, b, len(b))
+
+
+def shift(raw, nbytes):
+    return oracle().lib.oracle_crc32c_shift(raw & 0xFFFFFFFF, nbytes)
+
+
+def combine(crc_a, crc_b, len_b):
+    return oracle().lib.oracle_crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
+
+
+def batch_fixed(buf, stride, length, count, seed=0, seeds=None, threads=None):
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    if count:
+        assert (count - 1) * stride + length <= buf.nbytes
+    out = np.zeros(count, dtype=np.uint32)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    threads = threads or min(16, os.cpu_count() or 1)
+    oracle().lib.oracle_crc32c_batch_fixed(buf.ctypes.data, stride, length, count, seed & 0xFFFFFFFF,
+                                           None if sd is None else sd.ctypes.data, out.ctypes.data, threads)
+    return out
+
+
+def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, threads=None):
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+    n = offsets.size
+    assert lengths.size == n
+    if n:
+        assert int((offsets + lengths).max()) <= buf.nbytes
+    out = np.zeros(n, dtype=np.uint32)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    threads = threads or min(16, os.cpu_count() or 1)
+    oracle().lib.oracle_crc32c_batch_varlen(buf.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, n,
+                                            seed & 0xFFFFFFFF, None if sd is None else sd.ctypes.data,
+                                            out.ctypes.data, threads)
+    return out
+
+
+def splitmix64(nwords, state):
+    out = np.empty(nwords, dtype=np.uint64)
+    oracle().lib.oracle_splitmix64_fill(out.ctypes.data, nwords, state)
+    return out
