@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident batched CRC-32C on MI355X.
+
+Default workload = BASELINE.json configs[1]: 1 Mi x 4 KiB pages resident in
+HBM, one checksum per page, bit-exact with contrib/crc32.  A "step" is one
+pass of the engine over the whole batch (one kernel launch).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload pages4k|pages8k|zipf|chunks]
+
+N > 1 is launched by torch.distributed.run, one rank per GPU.  Pages shard
+trivially: every rank checksums its own batch of the same shape (weak
+scaling, no data-path collective); RCCL is used only to take the max elapsed
+time over ranks and to gather the per-rank byte counts.
+
+Rank 0 prints ONE JSON line.  `value` is GiB/s of buffer bytes read, whole
+job, from the host clock around the K timed steps.  `roofline.achieved` is the
+dominant kernel's algorithmic bytes per launch (buffer bytes + 4 B checksum
+per buffer [+ per-buffer metadata]) / its average launch duration measured
+with HIP events on the launch stream.  `cpu_baseline` times the reference's
+own crc32c.cpp (oracle/_ref) single-threaded on a bounded sample of the same
+workload on this host.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import foundationdb_amd as F  # noqa: E402
+import bench_workloads as W  # noqa: E402
+
+METRIC = "device-resident CRC32C GiB/s on 4 KiB page batches; % of HBM-read peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--workload", default="pages4k", choices=sorted(W.WORKLOADS))
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
+    p.add_argument("--no-verify", action="store_true")
+    return p.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(wl, seconds):
+    """Reference crc32c_append (oracle/_ref), 1 thread pinned to one core."""
+    from oracle import oracle as O
+    sample = wl.cpu_sample()
+    kind = "reference" if O.reference_available() else "port"
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    os.sched_setaffinity(0, {core})
+    try:
+        def once():
+            t = time.perf_counter()
+            if kind == "reference":
+                sample.run_reference(O)
+            else:
+                sample.run_port(O)
+            return time.perf_counter() - t
+        once()  # warm
+        best, total, reps = 1e30, 0.0, 0
+        while total < seconds or reps < 3:
+            dt = once()
+            best = min(best, dt)
+            total += dt
+            reps += 1
+    finally:
+        os.sched_setaffinity(0, old)
+    return {"value": round(sample.nbytes / best / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{sample.desc}; best of {reps} passes ({total:.1f} s of CPU work), 1 thread pinned to "
+                      f"core {core} of {len(old)} allowed; host CPU: {cpu_model()}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    F.gpu_init()
+
+    wl = W.WORKLOADS[args.workload](dev, rank)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        wl.step(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        wl.step(stream)
+        ends[i].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    ok = True
+    if not args.no_verify:
+        ok = wl.verify()
+
+    stats = torch.tensor([elapsed, float(wl.bytes_per_step), 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = stats[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        bytes_all = stats[1:2].clone()
+        dist.all_reduce(bytes_all, op=dist.ReduceOp.SUM)
+        bad = stats[2:3].clone()
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+        elapsed = float(t_max.item())
+        total_bytes = float(bytes_all.item()) * args.steps
+        ok = bad.item() == 0
+    else:
+        total_bytes = float(wl.bytes_per_step) * args.steps
+
+    if rank == 0:
+        value = total_bytes / elapsed / GIB
+        achieved = wl.algorithmic_bytes_per_step / (kernel_ms * 1e-3) / 1e9
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": wl.data_desc,
+            "config": dict(wl.config, parallelism=f"{world} GPU(s), independent shards per rank; RCCL only "
+                                                  "for max-time / byte-count reduction"),
+            "pct_of_hbm_read_peak": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS, 2),
+            "parity_ok": bool(ok),
+            "roofline": {
+                "bound": "hbm",
+                "kernel": wl.kernel_name,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "avg_launch_ms": round(kernel_ms, 4),
+                "algorithmic_bytes_per_launch": wl.algorithmic_bytes_per_step,
+                "traffic": W.pmc_traffic(args.workload),
+            },
+        }
+        if args.cpu_seconds > 0:
+            rec["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+"""Workloads for bench.py (BASELINE.json configs), each a synthetic input of
+the named shape generated directly in HBM (or pinned host memory), plus the
+CPU-baseline sample and a parity check of the last device result.
+
+configs[0]  CPU contrib/crc32 on 65536 x 4 KiB pages        -> cpu_baseline of pages4k
+configs[1]  1 Mi x 4 KiB pages, 1 GPU                        -> "pages4k" (default)
+configs[2]  Zipf 64 B - 16 KiB packets, 1 GPU                -> "zipf"
+configs[3]  8 KiB sqlite pages, sharded per GPU              -> "pages8k"
+configs[4]  4 KiB - 1 MiB chunks; device-only rate           -> "chunks"
+            (the host-to-host pipelined rate: "chunks-host")
+"""
+import json
+import os
+
+import numpy as np
+import torch
+
+import foundationdb_amd as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "crc32c_golden.json")
+STATE = 0x5EED
+
+
+def _golden():
+    with open(GOLDEN) as fh:
+        return json.load(fh)
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    return d.get("hbm_bytes_per_launch")
+
+
+class CpuSample:
+    def __init__(self, desc, nbytes, buf, stride=None, length=None, count=None, offsets=None, lengths=None, seed=0):
+        self.desc, self.nbytes, self.buf = desc, nbytes, buf
+        self.stride, self.length, self.count = stride, length, count
+        self.offsets, self.lengths, self.seed = offsets, lengths, seed
+
+    def run_reference(self, O):
+        if self.offsets is None:
+            return O.reference_batch_fixed(self.buf, self.stride, self.length, self.count, seed=self.seed)
+        L = O.reference().lib
+        import ctypes
+        f = L.ref_batch_varlen
+        f.restype = None
+        f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+        out = np.zeros(self.offsets.size, np.uint32)
+        f(self.buf.ctypes.data, self.offsets.ctypes.data, self.lengths.ctypes.data, self.offsets.size, self.seed,
+          out.ctypes.data)
+        return out
+
+    def run_port(self, O):
+        if self.offsets is None:
+            return O.batch_fixed(self.buf, self.stride, self.length, self.count, seed=self.seed, threads=1)
+        return O.batch_varlen(self.buf, self.offsets, self.lengths, seed=self.seed, threads=1)
+
+
+class Pages:
+    kernel_name = "fdbcrc::k_pages"
+
+    def __init__(self, dev, rank, page_bytes=4096, count=1 << 20, seed=0):
+        self.dev, self.page_bytes, self.count, self.seed = dev, page_bytes, count, seed
+        self.buf = torch.empty(count * page_bytes, dtype=torch.uint8, device=dev)
+        F.fill_splitmix64(self.buf, STATE)
+        self.out = torch.empty(count, dtype=torch.uint32, device=dev)
+        self.bytes_per_step = count * page_bytes
+        self.algorithmic_bytes_per_step = count * (page_bytes + 4)
+        self.data_desc = (f"synthetic: splitmix64 stream (state 0x{STATE:X}) generated in HBM, "
+                          f"{count} pages x {page_bytes} B, seed 0x{seed:08x}")
+        self.config = {"workload": f"{count} x {page_bytes} B pages, device-resident, fixed stride",
+                       "pages": count, "page_bytes": page_bytes, "seed": seed, "stride": page_bytes}
+
+    def step(self, stream):
+        F.batch_fixed(self.buf, self.page_bytes, self.page_bytes, self.count, seed=self.seed, out=self.out,
+                      stream=stream)
+
+    def verify(self):
+        g = _golden()
+        got = self.out.cpu().numpy()
+        if self.page_bytes == 4096 and self.count == 1 << 20:
+            d = [d for d in g["pages_full"]["digests"] if d["seed"] == self.seed][0]
+            return int(np.bitwise_xor.reduce(got)) == d["xor"] and int(got.astype(np.uint64).sum()) == d["sum"]
+        if self.page_bytes == 8192 and self.count == 1 << 19 and self.seed == 0xFDBEEFDB:
+            d = g["pages_full"]["digest_8k_fdbeefdb"]
+            return int(np.bitwise_xor.reduce(got)) == d["xor"] and int(got.astype(np.uint64).sum()) == d["sum"]
+        return _spot_check(self.buf, np.arange(self.count, dtype=np.uint64) * self.page_bytes,
+                           np.full(self.count, self.page_bytes, np.uint64), self.seed, got)
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        n = 65536 if self.page_bytes == 4096 else 32768
+        buf = O.splitmix64(n * self.page_bytes // 8, STATE).view(np.uint8)
+        return CpuSample(f"{n} x {self.page_bytes} B pages (configs[0] sample of the same stream)",
+                         n * self.page_bytes, buf, stride=self.page_bytes, length=self.page_bytes, count=n,
+                         seed=self.seed)
+
+
+def _spot_check(buf, offsets, lengths, seed, got, n=512):
+    """Recheck n random buffers with the library's independent host path."""
+    rng = np.random.default_rng(0)
+    idx = rng.choice(offsets.size, size=min(n, offsets.size), replace=False)
+    for i in idx:
+        o, l = int(offsets[i]), int(lengths[i])
+        data = buf[o:o + l].cpu().numpy()
+        if F.crc32c_append(seed, data) != int(got[i]):
+            return False
+    return True
+
+
+class VarLen:
+    kernel_name = "fdbcrc::k_general"
+
+    def __init__(self, dev, rank, lengths, align, desc, seed=0):
+        self.dev, self.seed = dev, seed
+        lengths = np.asarray(lengths, dtype=np.uint64)
+        padded = (lengths + (align - 1)) // align * align
+        offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.uint64)
+        total = int(offsets[-1] + padded[-1])
+        self.h_offsets, self.h_lengths = offsets, lengths
+        self.buf = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=dev)
+        F.fill_splitmix64(self.buf, STATE)
+        self.offsets = torch.from_numpy(offsets.astype(np.int64)).to(dev)
+        self.lengths = torch.from_numpy(lengths.astype(np.int64)).to(dev)
+        self.out = torch.empty(lengths.size, dtype=torch.uint32, device=dev)
+        n = lengths.size
+        self.bytes_per_step = int(lengths.sum())
+        # data + u64 offset + u64 length + u32 checksum per buffer
+        self.algorithmic_bytes_per_step = self.bytes_per_step + 20 * n
+        self.data_desc = f"synthetic: splitmix64 stream (state 0x{STATE:X}) in HBM; {desc}"
+        self.config = {"workload": desc, "buffers": int(n), "total_bytes": self.bytes_per_step,
+                       "mean_len": round(self.bytes_per_step / n, 1), "align": align, "seed": seed}
+
+    def step(self, stream):
+        F.batch_varlen(self.buf, self.offsets, self.lengths, seed=self.seed, out=self.out, stream=stream)
+
+    def verify(self):
+        return _spot_check(self.buf, self.h_offsets, self.h_lengths, self.seed, self.out.cpu().numpy())
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        # a prefix of the same buffer list of about 256 MiB
+        csum = np.cumsum(self.h_lengths)
+        k = int(np.searchsorted(csum, 256 << 20)) + 1
+        k = min(k, self.h_lengths.size)
+        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        buf = O.splitmix64((end + 7) // 8, STATE).view(np.uint8)
+        return CpuSample(f"first {k} buffers ({int(csum[k - 1]) >> 20} MiB) of the same list", int(csum[k - 1]), buf,
+                         offsets=self.h_offsets[:k].copy(), lengths=self.h_lengths[:k].copy(), seed=self.seed)
+
+
+def zipf_lengths(total_bytes=1 << 30, seed=1):
+    """Packet sizes: bucket k in 1..256 with P(k) ~ 1/k (Zipf, exponent 1.0),
+    length = clip(64*k - u, 64, 16384) with u uniform in [0, 63]."""
+    rng = np.random.default_rng(seed)
+    k = np.arange(1, 257)
+    p = (1.0 / k) / (1.0 / k).sum()
+    mean = float((p * (64 * k - 31.5)).sum())
+    n = int(total_bytes / mean)
+    ks = rng.choice(k, size=n, p=p)
+    u = rng.integers(0, 64, n)
+    return np.clip(64 * ks - u, 64, 16384).astype(np.uint64)
+
+
+def chunk_lengths(total_bytes=1 << 30, seed=5):
+    """Backup-sized chunks, log-uniform on [4 KiB, 1 MiB]."""
+    rng = np.random.default_rng(seed)
+    out, tot = [], 0
+    while tot < total_bytes:
+        L = int(np.exp(rng.uniform(np.log(4096), np.log(1 << 20))))
+        out.append(L)
+        tot += L
+    return np.array(out, dtype=np.uint64)
+
+
+WORKLOADS = {
+    "pages4k": lambda dev, rank: Pages(dev, rank, 4096, 1 << 20, 0),
+    "pages8k": lambda dev, rank: Pages(dev, rank, 8192, 1 << 19, 0xFDBEEFDB),
+    "zipf": lambda dev, rank: VarLen(dev, rank, zipf_lengths(), 256,
+                                     "Zipf(1.0) packet sizes 64 B - 16 KiB, ~1 GiB per batch, 256 B-aligned offsets"),
+    "chunks": lambda dev, rank: VarLen(dev, rank, chunk_lengths(), 4096,
+                                       "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch"),
+}

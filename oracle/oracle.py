@@ -91,6 +91,22 @@ def reference():
     return _ref
 
 
+def reference_batch_fixed(buf, stride, length, count, seed=0, out=None):
+    """Single-threaded loop over the reference crc32c_append (bench cpu_baseline)."""
+    L = reference().lib
+    f = L.ref_batch_fixed
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                  ctypes.c_void_p]
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    if count:
+        assert (count - 1) * stride + length <= buf.nbytes
+    if out is None:
+        out = np.zeros(count, dtype=np.uint32)
+    f(buf.ctypes.data, stride, length, count, seed & 0xFFFFFFFF, out.ctypes.data)
+    return out
+
+
 def crc32c(crc, data):
     return oracle().append(crc, data)
 

@@ -1,0 +1,118 @@
+"""The CPU oracle (our restatement of contrib/crc32) against the reference's own outputs."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def sm_bytes(nbytes, state):
+    return O.splitmix64((nbytes + 7) // 8, state).view(np.uint8)[:nbytes].copy()
+
+
+def test_kats(golden, oracle_mod):
+    for k in golden["kat"]:
+        data = bytes.fromhex(k["hex"])
+        assert O.crc32c(k["seed"], data) == k["crc"], k["name"]
+        assert O.crc32c_bitwise(k["seed"], data) == k["crc"], k["name"]
+    names = {k["name"]: k["crc"] for k in golden["kat"]}
+    # published check values (RFC 3720 B.4 and the CRC-32C catalogue check value)
+    assert names["check-123456789"] == 0xE3069283
+    assert names["rfc3720-zeros32"] == 0x8A9136AA
+    assert names["rfc3720-ones32"] == 0x62A8AB43
+    assert names["rfc3720-incr32"] == 0x46DD794E
+    assert names["rfc3720-decr32"] == 0x113FDB5C
+
+
+def _pattern(p, n):
+    if p == "zero":
+        return bytes(n)
+    if p == "i&255":
+        return bytes(i & 255 for i in range(n))
+    if p == "i*37+11":
+        return bytes(((i * 37 + 11) & 0xFF) for i in range(n))
+    raise ValueError(p)
+
+
+def test_patterns(golden, oracle_mod):
+    for e in golden["pattern"]:
+        assert O.crc32c(e["seed"], _pattern(e["pattern"], e["length"])) == e["crc"], e["name"]
+    legacy = [e for e in golden["pattern"] if e["name"] == "sqlite-legacy-test-page"][0]
+    assert legacy["crc"] == 0x23E52E01
+
+
+def test_edge_grid(golden, oracle_mod):
+    e = golden["edge"]
+    data = sm_bytes(e["nbytes"], e["state"])
+    for si, s in enumerate(e["seeds"]):
+        for off in range(e["offsets"]):
+            for n in range(e["max_len"] + 1):
+                assert O.crc32c(s, data[off:off + n]) == e["crc"][si][off][n], (s, off, n)
+
+
+def test_edge_grid_bitwise_subset(golden, oracle_mod):
+    e = golden["edge"]
+    data = sm_bytes(e["nbytes"], e["state"])
+    for si, s in enumerate(e["seeds"]):
+        for off in (0, 5, 15):
+            for n in range(0, e["max_len"] + 1, 7):
+                assert O.crc32c_bitwise(s, data[off:off + n]) == e["crc"][si][off][n]
+
+
+def test_thresholds(golden, oracle_mod):
+    t = golden["threshold"]
+    data = sm_bytes(t["nbytes"], t["state"])
+    for off, n, s, want in t["cases"]:
+        assert O.crc32c(s, data[off:off + n]) == want, (off, n, s)
+
+
+def test_page_batch_digests(golden, oracle_mod):
+    pb = golden["pages"]
+    pages = O.splitmix64(512 * pb["count"], pb["state"]).view(np.uint8)
+    for d in pb["digests"]:
+        c = O.batch_fixed(pages, 4096, 4096, pb["count"], seed=d["seed"])
+        assert int(np.bitwise_xor.reduce(c)) == d["xor"]
+        assert int(c.astype(np.uint64).sum()) == d["sum"]
+        assert [int(x) for x in c[:64]] == d["first64"]
+    # SURVEY §8c / BASELINE.md published digest of this batch at seed 0
+    d0 = [d for d in pb["digests"] if d["seed"] == 0][0]
+    assert d0["xor"] == 0xC18E0D85 and d0["sum"] == 0x0000807AFF89425D
+    assert d0["first64"][0] == 0x076DE509 and d0["first64"][1] == 0x808DD38F
+    c8 = O.batch_fixed(pages, 8192, 8192, pb["count"] // 2, seed=0xFDBEEFDB)
+    assert int(np.bitwise_xor.reduce(c8)) == pb["digest_8k_fdbeefdb"]["xor"]
+    c4088 = O.batch_fixed(pages, 4096, 4088, pb["count"], seed=0xFDBEEFDB)
+    assert int(c4088.astype(np.uint64).sum()) == pb["digest_4088_fdbeefdb"]["sum"]
+    c4092 = O.batch_fixed(pages[4:], 4096, 4092, pb["count"], seed=0xFDBEEFDB)
+    assert int(c4092.astype(np.uint64).sum()) == pb["digest_4092_at4_fdbeefdb"]["sum"]
+
+
+def test_chained_equals_oneshot(golden, oracle_mod):
+    c = golden["chained"]
+    data = sm_bytes(c["nbytes"] + 64, c["state"])[:c["nbytes"]]
+    crc = 0
+    for i in range(0, c["nbytes"], c["read"]):
+        crc = O.crc32c(crc, data[i:i + c["read"]])
+    assert crc == c["crc"] == c["oneshot"] == O.crc32c(0, data)
+
+
+def test_combine_and_shift_identities(oracle_mod):
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        a = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        s = int(rng.integers(0, 2**32))
+        assert O.combine(O.crc32c(s, a), O.crc32c(0, b), len(b)) == O.crc32c(s, a + b)
+        # seed linearity: crc(s,M) ^ crc(0,M) depends only on (s, |M|)
+        assert O.crc32c(s, b) ^ O.crc32c(0, b) == O.crc32c(s, bytes(len(b))) ^ O.crc32c(0, bytes(len(b)))
+
+
+@pytest.mark.skipif(not O.reference_available(), reason="oracle/_ref not built (no /root/reference)")
+def test_oracle_matches_compiled_reference_random():
+    ref = O.reference()
+    rng = np.random.default_rng(11)
+    buf = rng.integers(0, 256, 300_000, dtype=np.uint8)
+    for _ in range(3000):
+        off = int(rng.integers(0, 64))
+        n = int(rng.integers(0, 70_000)) if rng.random() < 0.9 else int(rng.integers(0, 299_000))
+        n = min(n, buf.size - off)
+        s = int(rng.integers(0, 2**32))
+        assert O.crc32c(s, buf[off:off + n]) == ref.append(s, buf[off:off + n])
