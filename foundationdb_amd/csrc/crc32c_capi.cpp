@@ -90,11 +90,11 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
 	if (int rc = device_state(&st)) return rc;
 	hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 	const uint8_t* base = static_cast<const uint8_t*>(d_base);
-	const uint64_t rows = length / 1024;
-	const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && (stride % 16 == 0) && length % 1024 == 0 &&
-	                     (rows == 1 || rows == 2 || rows == 4 || rows == 8);
+	const uint64_t blocks = length / 4096;
+	const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && (stride % 16 == 0) && length % 4096 == 0 &&
+	                     (blocks == 1 || blocks == 2);
 	if (aligned) {
-		launch_pages((int)rows, base, stride, count, seed, d_seeds, d_out, st->tables, st->num_cus, s);
+		launch_pages((int)blocks, base, stride, count, seed, d_seeds, d_out, st->tables, st->num_cus, s);
 	} else {
 		launch_general(base, stride, length, nullptr, nullptr, count, seed, d_seeds, d_out, st->tables, st->num_cus,
 		               s);

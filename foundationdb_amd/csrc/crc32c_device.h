@@ -8,14 +8,15 @@ namespace fdbcrc {
 
 struct DevTables {
 	uint32_t slice[2][256];     // [0] byte + one zero byte (T1), [1] single byte (T0)
-	uint32_t horner[8][16];     // nibble tables of x^(8*1008): row-to-row lane shift
-	uint32_t lane[64][8][16];   // nibble tables of x^(128*(63-l)): lane l to end of row
+	uint32_t block[8][16];      // nibble tables of x^(8*4096): block-to-block shift
+	uint32_t lane[64][8][16];   // nibble tables of x^(8*64*(63-l)): lane l to end of block
+	uint32_t slice4[4][256];    // [k]: byte followed by 3-k zero bytes (4-byte slicing T3..T0)
 };
 
 // Build the tables on the host (crc32c_tables.cpp).
 void build_dev_tables(DevTables* t);
 
-int launch_pages(int rows, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
+int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream);
 int launch_general(const uint8_t* base, uint64_t stride, uint64_t length, const uint64_t* offsets,
                    const uint64_t* lengths, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,

@@ -13,12 +13,15 @@ void build_dev_tables(DevTables* t) {
 		t->slice[1][b] = t0;                                  // T0: one byte
 		t->slice[0][b] = (t0 >> 8) ^ byte_step(t0 & 0xffu);   // T1: byte then one zero byte
 	}
-	// Row-to-row shift: a lane's next chunk sits 1024 bytes after its previous
-	// one; feeding 16 bytes already multiplies by x^128, so pre-multiply by
-	// x^(8*1008).
-	mul_tables_nibble(xpow8(1008), t->horner);
-	// Lane l's chunk is followed by 16*(63-l) bytes of the same row.
-	for (int l = 0; l < 64; ++l) mul_tables_nibble(xpow8(16u * (63 - l)), t->lane[l]);
+	// 4-byte slicing: slice4[3] = T0 (one byte), slice4[k] = slice4[k+1] followed by one zero byte.
+	for (uint32_t b = 0; b < 256; ++b) t->slice4[3][b] = byte_step(b);
+	for (int k = 2; k >= 0; --k)
+		for (uint32_t b = 0; b < 256; ++b)
+			t->slice4[k][b] = (t->slice4[k + 1][b] >> 8) ^ byte_step(t->slice4[k + 1][b] & 0xffu);
+	// Block-to-block shift: consecutive 4 KiB blocks of one buffer.
+	mul_tables_nibble(xpow8(4096), t->block);
+	// Lane l holds bytes [64l, 64l+64) of a block: 64*(63-l) bytes follow it.
+	for (int l = 0; l < 64; ++l) mul_tables_nibble(xpow8(64u * (63 - l)), t->lane[l]);
 }
 
 }  // namespace fdbcrc
