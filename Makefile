@@ -37,8 +37,16 @@ $(LIB): $(HIP_OBJS) $(CPP_OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# bounds-checked build for kernel debugging (foundationdb_amd/lib/libfdb_crc32c_debug.so)
+DBG_LIB := foundationdb_amd/lib/libfdb_crc32c_debug.so
+debug: $(HIP_SRCS) $(CPP_SRCS) $(HDRS)
+	@mkdir -p build/dbg
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) -DFDBCRC_DEBUG -c $$f -o build/dbg/$$(basename $$f).o || exit 1; done
+	for f in $(CPP_SRCS); do $(CXX) $(CXXFLAGS) -DFDBCRC_DEBUG -c $$f -o build/dbg/$$(basename $$f).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(DBG_LIB) build/dbg/*.o
+
 clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean debug

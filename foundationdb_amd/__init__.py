@@ -17,6 +17,7 @@ from .crc32c import (  # noqa: F401
     fill_splitmix64,
     gpu_init,
     lib,
+    varlen_workspace_bytes,
 )
 
 __version__ = "0.1.0"

@@ -16,7 +16,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfdb_crc32c.so")
+LIB_PATH = os.environ.get("FDBCRC_LIB") or os.path.join(_HERE, "lib", "libfdb_crc32c.so")
 
 
 class CRC32CError(RuntimeError):
@@ -48,6 +48,10 @@ def lib():
         L.crc32c_gpu_batch_fixed.argtypes = [vp, u64, u64, u64, u32, vp, vp, vp]
         L.crc32c_gpu_batch_varlen.restype = ctypes.c_int
         L.crc32c_gpu_batch_varlen.argtypes = [vp, vp, vp, u64, u32, vp, vp, vp]
+        L.crc32c_gpu_varlen_workspace_bytes.restype = u64
+        L.crc32c_gpu_varlen_workspace_bytes.argtypes = [u64]
+        L.crc32c_gpu_batch_varlen_ws.restype = ctypes.c_int
+        L.crc32c_gpu_batch_varlen_ws.argtypes = [vp, vp, vp, u64, u32, vp, vp, vp, u64, vp]
         L.crc32c_gpu_last_error.restype = ctypes.c_char_p
         L.crc32c_gpu_last_error.argtypes = []
         L.crc32c_gpu_version.restype = ctypes.c_char_p
@@ -130,8 +134,16 @@ def batch_fixed(buf, stride, length, count, seed=0, seeds=None, out=None, stream
     return out
 
 
-def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=None):
-    """CRC of buffer i = bytes [offsets[i], offsets[i]+lengths[i]) of device tensor `buf`."""
+def varlen_workspace_bytes(count):
+    return int(lib().crc32c_gpu_varlen_workspace_bytes(int(count)))
+
+
+def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=None, workspace=None):
+    """CRC of buffer i = bytes [offsets[i], offsets[i]+lengths[i]) of device tensor `buf`.
+
+    `workspace`: optional uint8 device tensor of at least varlen_workspace_bytes(count)
+    bytes (caller-owned planning workspace; otherwise the library's per-stream one).
+    """
     _require_device(buf, "buf")
     _require_device(offsets, "offsets")
     _require_device(lengths, "lengths")
@@ -147,9 +159,17 @@ def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=Non
         _require_device(seeds, "seeds")
         sp = ctypes.c_void_p(seeds.data_ptr())
     with torch.cuda.device(buf.device):
-        rc = lib().crc32c_gpu_batch_varlen(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
-                                           ctypes.c_void_p(lengths.data_ptr()), count, seed & 0xFFFFFFFF, sp,
-                                           ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+        if workspace is None:
+            rc = lib().crc32c_gpu_batch_varlen(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+                                               ctypes.c_void_p(lengths.data_ptr()), count, seed & 0xFFFFFFFF, sp,
+                                               ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+        else:
+            _require_device(workspace, "workspace")
+            rc = lib().crc32c_gpu_batch_varlen_ws(
+                ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+                ctypes.c_void_p(lengths.data_ptr()), count, seed & 0xFFFFFFFF, sp, ctypes.c_void_p(out.data_ptr()),
+                ctypes.c_void_p(workspace.data_ptr()), workspace.numel() * workspace.element_size(),
+                _stream_handle(stream))
     _check(rc, "crc32c_gpu_batch_varlen")
     return out
 

@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -18,6 +19,7 @@ struct DeviceState {
 	DevTables* tables = nullptr;  // device copy
 	int num_cus = 0;
 	bool ready = false;
+	std::map<hipStream_t, std::pair<void*, uint64_t>> ws;  // varlen planning workspace per stream
 };
 
 std::mutex g_mu;
@@ -64,6 +66,30 @@ int device_state(DeviceState** st) {
 	return 0;
 }
 
+// Planning workspace owned by the library for the convenience entry point,
+// one per (device, stream) so concurrent streams never share it.  Growing it
+// synchronises the stream once (the old buffer may still be in use).
+int stream_workspace(DeviceState* st, hipStream_t s, uint64_t need, void** ws, uint64_t* have) {
+	std::lock_guard<std::mutex> lock(g_mu);
+	auto& slot = st->ws[s];
+	if (slot.second < need) {
+		if (slot.first) {
+			hipError_t e = hipStreamSynchronize(s);
+			if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "hipStreamSynchronize(workspace)", e);
+			(void)hipFree(slot.first);
+			slot = {nullptr, 0};
+		}
+		uint64_t sz = need < (1u << 20) ? (1u << 20) : need * 2;
+		void* p = nullptr;
+		hipError_t e = hipMalloc(&p, sz);
+		if (e != hipSuccess) return fail(FDB_CRC32C_ENOMEM, "hipMalloc(workspace)", e);
+		slot = {p, sz};
+	}
+	*ws = slot.first;
+	*have = slot.second;
+	return 0;
+}
+
 int check_launch(const char* what) {
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, what, e);
@@ -74,6 +100,46 @@ int check_launch(const char* what) {
 }  // namespace fdbcrc
 
 using namespace fdbcrc;
+
+#ifdef FDBCRC_DEBUG
+// Debug builds: every varlen/general launch first sets the allowed data window
+// (computed on the host from the batch description) and afterwards reports
+// bounds violations instead of faulting.
+extern "C" int crc32c_debug_bounds(uint64_t lo, uint64_t hi);
+extern "C" int crc32c_debug_read(uint64_t* d_out8);
+namespace {
+void debug_report(const char* what) {
+	uint64_t* d = nullptr;
+	uint64_t h[8] = {0};
+	if (hipMalloc(&d, 64) != hipSuccess) return;
+	crc32c_debug_read(d);
+	(void)hipMemcpy(h, d, 64, hipMemcpyDeviceToHost);
+	(void)hipFree(d);
+	if (h[2]) fprintf(stderr, "[fdbcrc debug] %s: %llu violations, first bad 0x%llx at site %llu (window 0x%llx..0x%llx)\n",
+	                  what, (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4],
+	                  (unsigned long long)h[0], (unsigned long long)h[1]);
+}
+void debug_window_varlen(const void* base, const uint64_t* d_off, const uint64_t* d_len, uint64_t n) {
+	uint64_t lo = ~0ull, hi = 0;
+	uint64_t* ho = (uint64_t*)malloc(8 * n);
+	uint64_t* hl = (uint64_t*)malloc(8 * n);
+	(void)hipDeviceSynchronize();
+	(void)hipMemcpy(ho, d_off, 8 * n, hipMemcpyDeviceToHost);
+	(void)hipMemcpy(hl, d_len, 8 * n, hipMemcpyDeviceToHost);
+	for (uint64_t i = 0; i < n; ++i) {
+		if (!hl[i]) continue;
+		const uint64_t a = (uint64_t)base + ho[i];
+		if (a < lo) lo = a;
+		if (a + hl[i] > hi) hi = a + hl[i];
+	}
+	free(ho);
+	free(hl);
+	if (hi == 0) lo = hi = 1;
+	crc32c_debug_bounds(lo, hi);
+}
+}  // namespace
+#endif
+
 
 extern "C" {
 
@@ -93,13 +159,52 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
 	const uint64_t blocks = length / 4096;
 	const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && (stride % 16 == 0) && length % 4096 == 0 &&
 	                     (blocks == 1 || blocks == 2);
-	if (aligned) {
-		launch_pages((int)blocks, base, stride, count, seed, d_seeds, d_out, st->tables, st->num_cus, s);
-	} else {
-		launch_general(base, stride, length, nullptr, nullptr, count, seed, d_seeds, d_out, st->tables, st->num_cus,
-		               s);
+	int rc;
+	if (length == 0)
+		rc = launch_fill_seeds(count, seed, d_seeds, d_out, s);
+	else if (aligned)
+		rc = launch_pages((int)blocks, base, stride, count, seed, d_seeds, d_out, st->tables, st->num_cus, s);
+	else {
+#ifdef FDBCRC_DEBUG
+		crc32c_debug_bounds((uint64_t)base, (uint64_t)base + (count - 1) * stride + length);
+#endif
+		rc = launch_fixed_general(base, stride, length, count, seed, d_seeds, d_out, st->tables, st->num_cus, s);
+#ifdef FDBCRC_DEBUG
+		(void)hipDeviceSynchronize();
+		debug_report("batch_fixed(general)");
+#endif
 	}
+	if (rc) return fail(FDB_CRC32C_EHIP, "crc32c_gpu_batch_fixed: launch setup failed");
 	return check_launch("crc32c_gpu_batch_fixed launch");
+}
+
+uint64_t crc32c_gpu_varlen_workspace_bytes(uint64_t count) {
+	DeviceState* st;
+	if (device_state(&st)) return 0;
+	return varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16);
+}
+
+int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                               uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
+                               uint64_t workspace_bytes, void* stream) {
+	if (count == 0) return 0;
+	if (!d_out || !d_offsets || !d_lengths || !d_base)
+		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	const uint64_t need = varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16);
+	if (!d_workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: workspace too small or misaligned");
+#ifdef FDBCRC_DEBUG
+	debug_window_varlen(d_base, d_offsets, d_lengths, count);
+#endif
+	launch_varlen(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, seed, d_seeds, d_out, st->tables,
+	              st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream));
+#ifdef FDBCRC_DEBUG
+	(void)hipDeviceSynchronize();
+	debug_report("batch_varlen");
+#endif
+	return check_launch("crc32c_gpu_batch_varlen launch");
 }
 
 int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
@@ -109,13 +214,18 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
 	DeviceState* st;
 	if (int rc = device_state(&st)) return rc;
-	launch_general(static_cast<const uint8_t*>(d_base), 0, 0, d_offsets, d_lengths, count, seed, d_seeds, d_out,
-	               st->tables, st->num_cus, reinterpret_cast<hipStream_t>(stream));
-	return check_launch("crc32c_gpu_batch_varlen launch");
+	void* ws = nullptr;
+	uint64_t have = 0;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
+	                              varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have))
+		return rc;
+	return crc32c_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
 }
 
 const char* crc32c_gpu_last_error(void) { return t_err.c_str(); }
 
 const char* crc32c_gpu_version(void) { return "fdb_crc32c 0.1 gfx950"; }
+
+
 
 }  // extern "C"

@@ -1,0 +1,307 @@
+// Device-side building blocks shared by the page and variable-length kernels:
+// LDS images of the operator tables, the 2-/4-byte sliced register update,
+// nibble-table constant multiplies, the wave XOR reduction and the 4 KiB
+// block load + permlane swizzle.  See crc32c_kernels.hip for the geometry.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_device.h"
+
+namespace fdbcrc {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// LDS image (byte offsets).  Lane l always reads bank column l%32.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSliceOff = 0x00000;  // [256 idx][2 tab][32 col]         64 KiB
+constexpr uint32_t kBlockOff = 0x10000;  // [8 nib][16 v][32 col]            16 KiB  x^(8*4096)
+constexpr uint32_t kLaneOff = 0x14000;   // [2 half][8 nib][16 v][32 col]    32 KiB  x^(8*64*(63-l))
+constexpr uint32_t kLdsBytes = 0x1C000;  // 112 KiB -> one 1024-thread workgroup per CU
+constexpr uint32_t kTabT1 = 0;           // slice table: byte followed by one zero byte
+constexpr uint32_t kTabT0 = 128;         // slice table: single byte
+
+// Layout B (4 KiB page kernel only): 4-byte slicing, 160 KiB = all of LDS.
+//   region 0 [idx][T3,T2][col], region 1 [idx][T1,T0][col], then lane tables.
+constexpr uint32_t kS4Off = 0x00000;     // 2 x 64 KiB
+constexpr uint32_t kS4LaneOff = 0x20000; // [2 half][8 nib][16 v][32 col]    32 KiB  x^(8*64*(63-l))
+constexpr uint32_t kLdsBytesB = 0x28000; // 160 KiB
+
+__device__ __forceinline__ uint32_t lds_rd(const uint32_t* lds, uint32_t byte_addr) {
+	return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Expand the compact tables into the bank-replicated LDS image.  Each thread
+// first issues all of its (independent) global loads, then writes: slice and
+// block-shift values go to all 32 bank columns, lane-combine values to the
+// one column (lane%32) of the lane they belong to.
+__device__ inline void fill_lds(uint32_t* lds, const DevTables* __restrict__ t) {
+	constexpr uint32_t kSlice = 512, kBlock = 128, kLane = 64 * 128;
+	constexpr uint32_t kCompact = kSlice + kBlock + kLane;  // 8832 words
+	constexpr uint32_t kPer = (kCompact + 1023) / 1024;
+	const uint32_t* src = reinterpret_cast<const uint32_t*>(t);
+	uint32_t v[kPer];
+#pragma unroll
+	for (uint32_t i = 0; i < kPer; ++i) {
+		const uint32_t q = threadIdx.x + i * blockDim.x;
+		v[i] = q < kCompact ? src[q] : 0u;
+	}
+#pragma unroll
+	for (uint32_t i = 0; i < kPer; ++i) {
+		const uint32_t q = threadIdx.x + i * blockDim.x;
+		if (q < kSlice) {  // slice[tab][idx] -> [idx][tab][col]
+			const uint32_t tab = q >> 8, idx = q & 255;
+			uint32_t* d = lds + (kSliceOff / 4) + (idx * 2 + tab) * 32;
+#pragma unroll
+			for (int c = 0; c < 32; ++c) d[c] = v[i];
+		} else if (q < kSlice + kBlock) {  // block[nib][v] -> [nib][v][col]
+			uint32_t* d = lds + (kBlockOff / 4) + (q - kSlice) * 32;
+#pragma unroll
+			for (int c = 0; c < 32; ++c) d[c] = v[i];
+		} else if (q < kCompact) {  // lane[l][nib][v] -> [l/32][nib][v][l%32]
+			const uint32_t r = q - kSlice - kBlock;
+			const uint32_t l = r >> 7, nv = r & 127;
+			lds[(kLaneOff / 4) + (l >> 5) * 4096 + nv * 32 + (l & 31)] = v[i];
+		}
+	}
+	__syncthreads();
+}
+
+// Layout B fill: slice4 (1024 words) to all 32 columns, lane tables to their column.
+__device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t) {
+	constexpr uint32_t kSlice = 1024, kLane = 64 * 128;
+	constexpr uint32_t kCompact = kSlice + kLane;  // 9216 words
+	constexpr uint32_t kPer = (kCompact + 1023) / 1024;
+	const uint32_t* s4 = &t->slice4[0][0];
+	const uint32_t* ln = &t->lane[0][0][0];
+	uint32_t v[kPer];
+#pragma unroll
+	for (uint32_t i = 0; i < kPer; ++i) {
+		const uint32_t q = threadIdx.x + i * blockDim.x;
+		v[i] = q < kSlice ? s4[q] : (q < kCompact ? ln[q - kSlice] : 0u);
+	}
+#pragma unroll
+	for (uint32_t i = 0; i < kPer; ++i) {
+		const uint32_t q = threadIdx.x + i * blockDim.x;
+		if (q < kSlice) {  // slice4[k][idx], k = 0..3 -> T3,T2 | T1,T0 regions
+			const uint32_t k = q >> 8, idx = q & 255;
+			uint32_t* d = lds + (kS4Off / 4) + (k >> 1) * 16384 + (idx * 2 + (k & 1)) * 32;
+#pragma unroll
+			for (int c = 0; c < 32; ++c) d[c] = v[i];
+		} else if (q < kCompact) {
+			const uint32_t r = q - kSlice;
+			const uint32_t l = r >> 7, nv = r & 127;
+			lds[(kS4LaneOff / 4) + (l >> 5) * 4096 + nv * 32 + (l & 31)] = v[i];
+		}
+	}
+	__syncthreads();
+}
+
+struct LaneCtx {
+	uint32_t c_slice;  // col*4
+	uint32_t c_block;  // kBlockOff | col*4
+	uint32_t c_lane;   // kLaneOff + half*16 KiB | col*4
+	uint32_t ld_off;   // byte offset of this lane's first 16 B load inside a block
+	int lane;
+};
+
+__device__ __forceinline__ LaneCtx make_ctx() {
+	LaneCtx c;
+	c.lane = threadIdx.x & 63;
+	const uint32_t col4 = (c.lane & 31) * 4;
+	c.c_slice = kSliceOff | col4;
+	c.c_block = kBlockOff | col4;
+	c.c_lane = (kLaneOff + (c.lane >> 5) * 0x4000) | col4;
+	// lane m = 32h + 16q + r loads, for load k = 2kb + ka, the 16 bytes at
+	//   2048*ka + 1024*kb + 64r + 32q + 16h
+	// which after the swap network (unswizzle) puts block bytes
+	// [64l, 64l+64) into lane l as registers r[0..3].
+	const uint32_t h = c.lane >> 5, q = (c.lane >> 4) & 1, r = c.lane & 15;
+	c.ld_off = 64 * r + 32 * q + 16 * h;
+	return c;
+}
+
+// Two bytes of register update: x already holds (register ^ data).
+//   x' = (x >> 16) ^ T1[x.b0] ^ T0[x.b1]
+__device__ __forceinline__ uint32_t half_step(const uint32_t* lds, uint32_t x, uint32_t c_slice) {
+	const uint32_t a0 = __builtin_amdgcn_perm(x, c_slice, 0x0c0c0400u);  // (x.b0 << 8) | col*4
+	const uint32_t a1 = __builtin_amdgcn_perm(x, c_slice, 0x0c0c0500u);  // (x.b1 << 8) | col*4
+	return xor3(x >> 16, lds_rd(lds, a0 + kTabT1), lds_rd(lds, a1 + kTabT0));
+}
+
+// Feed 16 bytes into register s.
+__device__ __forceinline__ uint32_t feed16(const uint32_t* lds, uint32_t s, u32x4 w, uint32_t c_slice) {
+	s = half_step(lds, half_step(lds, s ^ w.x, c_slice), c_slice);
+	s = half_step(lds, half_step(lds, s ^ w.y, c_slice), c_slice);
+	s = half_step(lds, half_step(lds, s ^ w.z, c_slice), c_slice);
+	s = half_step(lds, half_step(lds, s ^ w.w, c_slice), c_slice);
+	return s;
+}
+
+// Layout B: four bytes per step, s' = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3]
+// with x = s ^ word.  c4 = col*4 | 0x10000 (byte 2 selects region 1).
+__device__ __forceinline__ uint32_t word_step4(const uint32_t* lds, uint32_t x, uint32_t c4) {
+	const uint32_t a3 = __builtin_amdgcn_perm(x, c4, 0x0c0c0400u);  // (x.b0 << 8) | col*4
+	const uint32_t a2 = __builtin_amdgcn_perm(x, c4, 0x0c0c0500u);  // (x.b1 << 8) | col*4
+	const uint32_t a1 = __builtin_amdgcn_perm(x, c4, 0x0c020600u);  // 0x10000 | (x.b2 << 8) | col*4
+	const uint32_t a0 = __builtin_amdgcn_perm(x, c4, 0x0c020700u);  // 0x10000 | (x.b3 << 8) | col*4
+	return xor3(lds_rd(lds, a3), lds_rd(lds, a2 + 128), lds_rd(lds, a1)) ^ lds_rd(lds, a0 + 128);
+}
+
+__device__ __forceinline__ uint32_t feed16_b(const uint32_t* lds, uint32_t s, u32x4 w, uint32_t c4) {
+	s = word_step4(lds, s ^ w.x, c4);
+	s = word_step4(lds, s ^ w.y, c4);
+	s = word_step4(lds, s ^ w.z, c4);
+	s = word_step4(lds, s ^ w.w, c4);
+	return s;
+}
+
+// Multiply a register by the constant whose nibble tables start at `base`
+// (base already carries the lane's column).
+__device__ __forceinline__ uint32_t mul_nibbles(const uint32_t* lds, uint32_t s, uint32_t base) {
+	uint32_t r[8];
+#pragma unroll
+	for (int n = 0; n < 8; ++n) {
+		const uint32_t v = (s >> (4 * n)) & 15u;
+		r[n] = lds_rd(lds, ((v << 7) | base) + n * 2048);
+	}
+	return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
+
+// Cross-lane reads with unsigned results.  The builtins return `int`: widening
+// that to 64 bits sign-extends, so every 64-bit value is rebuilt from
+// explicitly unsigned halves.
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int k) {
+	return (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+}
+__device__ __forceinline__ uint32_t rdfirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int k) {
+	return ((uint64_t)rdlane((uint32_t)(v >> 32), k) << 32) | (uint64_t)rdlane((uint32_t)v, k);
+}
+__device__ __forceinline__ uint64_t rdfirst64(uint64_t v) {
+	return ((uint64_t)rdfirst((uint32_t)(v >> 32)) << 32) | (uint64_t)rdfirst((uint32_t)v);
+}
+
+// XOR of v over each 16-lane row; every lane of the row gets its row's value.
+__device__ __forceinline__ uint32_t row_xor(uint32_t v) {
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+	return v;
+}
+
+// XOR of v over all 64 lanes, returned wave-uniform.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+	return rdlane(v, 0) ^ rdlane(v, 16) ^ rdlane(v, 32) ^ rdlane(v, 48);
+}
+
+#ifdef FDBCRC_DEBUG
+// Debug builds (make debug): every data load is bounds-checked against the
+// window set by crc32c_debug_bounds(); violations are counted and skipped
+// instead of faulting.  [0] lo, [1] hi, [2] violations, [3] first bad address
+static __device__ unsigned long long g_dbg[8];
+__device__ __forceinline__ bool dbg_ok(const void* p, uint64_t n, int site) {
+	const uint64_t a = reinterpret_cast<uint64_t>(p);
+	// aligned 16-byte chunks may extend past the data to the next 16-byte
+	// boundary (same page, cannot fault): allow the 16-byte-rounded window
+	if (g_dbg[1] == 0 || (a >= (g_dbg[0] & ~15ull) && a + n <= ((g_dbg[1] + 15) & ~15ull))) return true;
+	if (atomicAdd(&g_dbg[2], 1ull) == 0) {
+		g_dbg[3] = a;
+		g_dbg[4] = (unsigned long long)site;
+	}
+	return false;
+}
+#define DBG_OK(p, n, site) dbg_ok((p), (n), (site))
+#else
+#define DBG_OK(p, n, site) true
+#endif
+
+// Every data load goes through the global address space (global_load_*,
+// in-order vmcnt), never a FLAT load: addresses computed from integers would
+// otherwise lose their address space.
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+	if (!DBG_OK(p, 16, 1)) return u32x4{0u, 0u, 0u, 0u};
+	return __builtin_nontemporal_load((g_u32x4*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+__device__ __forceinline__ uint32_t ld1(const uint8_t* p) {
+	if (!DBG_OK(p, 1, 2)) return 0u;
+	return *((g_u8*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+// ---------------------------------------------------------------------------
+// 4 KiB blocks
+// ---------------------------------------------------------------------------
+struct Block {
+	u32x4 r[4];
+};
+
+__device__ __forceinline__ void load_block(Block& b, const uint8_t* block, uint32_t ld_off) {
+	const uint8_t* p = block + ld_off;
+	b.r[0] = ld16(p);
+	b.r[1] = ld16(p + 2048);
+	b.r[2] = ld16(p + 1024);
+	b.r[3] = ld16(p + 3072);
+}
+
+__device__ __forceinline__ void swap32(u32x4& x, u32x4& y) {
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		const auto t = __builtin_amdgcn_permlane32_swap(x[i], y[i], false, false);
+		x[i] = t[0];
+		y[i] = t[1];
+	}
+}
+
+__device__ __forceinline__ void swap16(u32x4& x, u32x4& y) {
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		const auto t = __builtin_amdgcn_permlane16_swap(x[i], y[i], false, false);
+		x[i] = t[0];
+		y[i] = t[1];
+	}
+}
+
+// After this, lane l holds block bytes [64l, 64l+64) in r[0..3].
+__device__ __forceinline__ void unswizzle(Block& b) {
+	swap32(b.r[0], b.r[1]);
+	swap32(b.r[2], b.r[3]);
+	swap16(b.r[0], b.r[2]);
+	swap16(b.r[1], b.r[3]);
+}
+
+// Register of this lane after its 64 bytes, starting from s.
+__device__ __forceinline__ uint32_t chain64(const uint32_t* lds, uint32_t s, const Block& b, uint32_t c_slice) {
+	s = feed16(lds, s, b.r[0], c_slice);
+	s = feed16(lds, s, b.r[1], c_slice);
+	s = feed16(lds, s, b.r[2], c_slice);
+	s = feed16(lds, s, b.r[3], c_slice);
+	return s;
+}
+
+
+// Byte-serial register update (tiny pieces), wave-uniform.
+__device__ __forceinline__ uint32_t byte_step(const uint32_t* lds, uint32_t s, uint32_t b, uint32_t c_slice) {
+	const uint32_t a = __builtin_amdgcn_perm(s ^ b, c_slice, 0x0c0c0400u);
+	return (s >> 8) ^ lds_rd(lds, a + kTabT0);
+}
+
+__device__ inline uint32_t feed_bytes(const uint32_t* lds, uint32_t s, const uint8_t* p, const uint8_t* e, uint32_t c_slice) {
+	for (; p < e; ++p) s = byte_step(lds, s, ld1(p), c_slice);
+	return s;
+}
+
+}  // namespace fdbcrc

@@ -11,6 +11,8 @@ struct DevTables {
 	uint32_t block[8][16];      // nibble tables of x^(8*4096): block-to-block shift
 	uint32_t lane[64][8][16];   // nibble tables of x^(8*64*(63-l)): lane l to end of block
 	uint32_t slice4[4][256];    // [k]: byte followed by 3-k zero bytes (4-byte slicing T3..T0)
+	uint32_t inv_z[16][8][16];  // nibble tables of x^(-8z), z = 0..15: drop z trailing zero bytes
+	uint32_t pow2[64][8][16];   // nibble tables of x^(8*2^m): shift by arbitrary byte counts
 };
 
 // Build the tables on the host (crc32c_tables.cpp).
@@ -18,8 +20,14 @@ void build_dev_tables(DevTables* t);
 
 int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream);
-int launch_general(const uint8_t* base, uint64_t stride, uint64_t length, const uint64_t* offsets,
-                   const uint64_t* lengths, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
-                   const DevTables* tabs, int num_cus, hipStream_t stream);
+// Variable-length engine (crc32c_varlen.hip).  ws: varlen_workspace_bytes().
+uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
+int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
+                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
+                  hipStream_t stream);
+int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
+                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus,
+                         hipStream_t stream);
+int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out, hipStream_t stream);
 
 }  // namespace fdbcrc

@@ -22,6 +22,14 @@ void build_dev_tables(DevTables* t) {
 	mul_tables_nibble(xpow8(4096), t->block);
 	// Lane l holds bytes [64l, 64l+64) of a block: 64*(63-l) bytes follow it.
 	for (int l = 0; l < 64; ++l) mul_tables_nibble(xpow8(64u * (63 - l)), t->lane[l]);
+	// Variable shifts for pieces of split buffers and trailing-zero removal.
+	for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(z), t->inv_z[z]);
+	for (int m = 0; m < 64; ++m) {
+		// x^(8*2^m) by repeated squaring of x^8
+		uint32_t c = kOne >> 8;
+		for (int k = 0; k < m; ++k) c = gf2_mul(c, c);
+		mul_tables_nibble(c, t->pow2[m]);
+	}
 }
 
 }  // namespace fdbcrc

@@ -78,9 +78,23 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
                            const uint32_t* d_seeds, uint32_t* d_out, void* stream);
 
 /* Buffer i is the d_lengths[i] bytes at d_base + d_offsets[i] (any alignment,
- * any order, overlaps allowed).  Seed as above.  Writes d_out[i]. */
+ * any order, overlaps allowed).  Seed as above.  Writes d_out[i].
+ * Work is balanced by bytes across the GPU, so one 1 MiB buffer among many
+ * 64 B packets is split over several wavefronts and merged on the device.
+ * Uses a library-owned workspace per (device, stream); it is allocated on
+ * first use and grown (with one stream synchronisation) when a larger batch
+ * arrives. */
 int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                             uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
+
+/* Same, with a caller-owned device workspace (no allocation, no implicit
+ * synchronisation: safe inside stream capture).  The workspace holds the
+ * per-tile byte prefix and the wave map of the byte-balanced planner;
+ * crc32c_gpu_varlen_workspace_bytes(count) gives its size (16-byte aligned). */
+uint64_t crc32c_gpu_varlen_workspace_bytes(uint64_t count);
+int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                               uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
+                               uint64_t workspace_bytes, void* stream);
 
 /* Text of the last error recorded on the calling thread ("" if none). */
 const char* crc32c_gpu_last_error(void);

@@ -1,0 +1,21 @@
+"""Workload driver for rocprofv3 --pmc passes (development)."""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import foundationdb_amd as F
+
+mode = sys.argv[1] if len(sys.argv) > 1 else "pages4k"
+dev = torch.device("cuda:0")
+F.gpu_init()
+n = 1 << 20
+big = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
+F.fill_splitmix64(big, 0x5EED)
+out = torch.empty(n, dtype=torch.uint32, device=dev)
+torch.cuda.synchronize()
+for _ in range(5):
+    if mode == "pages4k":
+        F.batch_fixed(big, 4096, 4096, n, out=out)
+    elif mode == "stride0":
+        F.batch_fixed(big, 0, 4096, n, out=out)
+torch.cuda.synchronize()
+print("done", mode)
