@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--workload", default="pages4k", choices=sorted(W.WORKLOADS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--dry-cpu", action="store_true",
+                   help="test the multi-rank harness on CPU (gloo, host checksums); not a measurement")
     return p.parse_args()
 
 
@@ -97,35 +99,49 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    F.gpu_init()
-
-    wl = W.WORKLOADS[args.workload](dev, rank)
-    stream = torch.cuda.current_stream(dev)
+    dry = args.dry_cpu
+    if dry:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        wl = W.DryCpuPages(rank)
+        sync = lambda: None  # noqa: E731
+        stream = None
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        F.gpu_init()
+        wl = W.WORKLOADS[args.workload](dev, rank)
+        stream = torch.cuda.current_stream(dev)
+        sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
     for _ in range(args.warmup):
         wl.step(stream)
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    timed = not dry and not getattr(wl, "host_timed", False)
+    if timed:
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        starts[i].record(stream)
+        if timed:
+            starts[i].record(stream)
         wl.step(stream)
-        ends[i].record(stream)
-    torch.cuda.synchronize(dev)
+        if timed:
+            ends[i].record(stream)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])) if timed else \
+        elapsed / args.steps * 1e3
 
     ok = True
     if not args.no_verify:
@@ -147,7 +163,9 @@ def main():
 
     if rank == 0:
         value = total_bytes / elapsed / GIB
+        host_timed = getattr(wl, "host_timed", False)
         achieved = wl.algorithmic_bytes_per_step / (kernel_ms * 1e-3) / 1e9
+        peak = wl.pcie_peak_gbs if host_timed else HBM_PEAK_GBS
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -166,18 +184,20 @@ def main():
             "pct_of_hbm_read_peak": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS, 2),
             "parity_ok": bool(ok),
             "roofline": {
-                "bound": "hbm",
+                "bound": "pcie" if host_timed else "hbm",
                 "kernel": wl.kernel_name,
                 "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
+                "peak": peak,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac": round(achieved / peak, 4),
                 "avg_launch_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": wl.algorithmic_bytes_per_step,
                 "traffic": W.pmc_traffic(args.workload),
             },
         }
-        if args.cpu_seconds > 0:
+        if dry:
+            rec["data"] = "DRY RUN on CPU (harness test, not a measurement)"
+        elif args.cpu_seconds > 0:
             rec["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -179,6 +179,82 @@ def chunk_lengths(total_bytes=1 << 30, seed=5):
     return np.array(out, dtype=np.uint64)
 
 
+class HostChunks:
+    """configs[4], host-to-host: backup chunks in pinned host memory, checksummed
+    through the pinned H2D -> kernel -> D2H pipeline (4 streams, 64 MiB segments).
+    The rate includes both PCIe copies; it is PCIe-bound by design."""
+    kernel_name = "host pipeline (H2D + fdbcrc::k_varlen + D2H)"
+    host_timed = True
+    pcie_peak_gbs = 63.0  # PCIe Gen5 x16 per direction, MI355X_MICROARCH.md
+
+    def __init__(self, dev, rank, seed=0):
+        lengths = chunk_lengths()
+        padded = (lengths + 4095) // 4096 * 4096
+        offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.uint64)
+        total = int(offsets[-1] + padded[-1])
+        self.buf = torch.empty(total, dtype=torch.uint8).pin_memory()
+        dbuf = torch.empty(total, dtype=torch.uint8, device=dev)
+        F.fill_splitmix64(dbuf, STATE)
+        self.buf.copy_(dbuf)
+        del dbuf
+        self.h_offsets, self.h_lengths, self.seed = offsets, lengths.astype(np.uint64), seed
+        self.out = torch.empty(lengths.size, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
+        self.pipe = F.Pipeline(segment_bytes=64 << 20, nstreams=4)
+        self.bytes_per_step = int(lengths.sum())
+        self.algorithmic_bytes_per_step = self.bytes_per_step + 20 * lengths.size
+        self.data_desc = (f"synthetic: splitmix64 stream (state 0x{STATE:X}) in PINNED HOST memory; "
+                          "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch, host-to-host")
+        self.config = {"workload": "log-uniform 4 KiB - 1 MiB chunks, host-resident, pinned H2D/D2H overlapped "
+                                   "(4 streams x 64 MiB segments)", "buffers": int(lengths.size),
+                       "total_bytes": self.bytes_per_step, "seed": seed}
+
+    def step(self, stream):
+        self.pipe.varlen(self.buf, self.h_offsets, self.h_lengths, seed=self.seed, out=self.out)
+
+    def verify(self):
+        host = self.buf.numpy()
+        rng = np.random.default_rng(0)
+        for i in rng.choice(self.h_offsets.size, size=256, replace=False):
+            o, l = int(self.h_offsets[i]), int(self.h_lengths[i])
+            if F.crc32c_append(self.seed, host[o:o + l]) != int(self.out[i]):
+                return False
+        return True
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        csum = np.cumsum(self.h_lengths)
+        k = min(int(np.searchsorted(csum, 256 << 20)) + 1, self.h_lengths.size)
+        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        buf = self.buf.numpy()[:end]
+        return CpuSample(f"first {k} buffers ({int(csum[k - 1]) >> 20} MiB) of the same list", int(csum[k - 1]), buf,
+                         offsets=self.h_offsets[:k].copy(), lengths=self.h_lengths[:k].copy(), seed=self.seed)
+
+
+class DryCpuPages:
+    """--dry-cpu: exercises bench.py's multi-rank harness on CPU with the
+    library's host crc32c_append over a small page batch.  Not a measurement."""
+    kernel_name = "host crc32c_append (dry run)"
+    host_timed = True
+    pcie_peak_gbs = 1.0
+
+    def __init__(self, rank, count=2048):
+        self.count = count
+        rng = np.random.default_rng(rank)
+        self.buf = rng.integers(0, 256, count * 4096, dtype=np.uint8)
+        self.out = np.zeros(count, dtype=np.uint32)
+        self.bytes_per_step = count * 4096
+        self.algorithmic_bytes_per_step = count * 4100
+        self.data_desc = "dry run"
+        self.config = {"workload": f"dry run: {count} x 4096 B pages on CPU"}
+
+    def step(self, stream):
+        for i in range(self.count):
+            self.out[i] = F.crc32c_append(0, self.buf[4096 * i:4096 * (i + 1)])
+
+    def verify(self):
+        return int(self.out[0]) == F.crc32c_append(0, self.buf[:4096].tobytes())
+
+
 WORKLOADS = {
     "pages4k": lambda dev, rank: Pages(dev, rank, 4096, 1 << 20, 0),
     "pages8k": lambda dev, rank: Pages(dev, rank, 8192, 1 << 19, 0xFDBEEFDB),
@@ -186,4 +262,5 @@ WORKLOADS = {
                                      "Zipf(1.0) packet sizes 64 B - 16 KiB, ~1 GiB per batch, 256 B-aligned offsets"),
     "chunks": lambda dev, rank: VarLen(dev, rank, chunk_lengths(), 4096,
                                        "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch"),
+    "chunks-host": lambda dev, rank: HostChunks(dev, rank),
 }

@@ -7,6 +7,7 @@ batched device entry points over torch-allocated HBM buffers.
 """
 from .crc32c import (  # noqa: F401
     CRC32CError,
+    Pipeline,
     LIB_PATH,
     batch_fixed,
     batch_varlen,

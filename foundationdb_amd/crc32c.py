@@ -56,6 +56,18 @@ def lib():
         L.crc32c_gpu_last_error.argtypes = []
         L.crc32c_gpu_version.restype = ctypes.c_char_p
         L.crc32c_gpu_version.argtypes = []
+        L.crc32c_pipeline_create.restype = ctypes.c_int
+        L.crc32c_pipeline_create.argtypes = [ctypes.POINTER(vp), u64, ctypes.c_int]
+        L.crc32c_pipeline_destroy.restype = None
+        L.crc32c_pipeline_destroy.argtypes = [vp]
+        L.crc32c_pipeline_varlen.restype = ctypes.c_int
+        L.crc32c_pipeline_varlen.argtypes = [vp, vp, vp, vp, u64, u32, vp, vp]
+        L.crc32c_pipeline_fixed.restype = ctypes.c_int
+        L.crc32c_pipeline_fixed.argtypes = [vp, vp, u64, u64, u64, u32, vp, vp]
+        L.crc32c_host_register.restype = ctypes.c_int
+        L.crc32c_host_register.argtypes = [vp, u64]
+        L.crc32c_host_unregister.restype = ctypes.c_int
+        L.crc32c_host_unregister.argtypes = [vp]
         L.crc32c_testutil_fill_splitmix64.restype = ctypes.c_int
         L.crc32c_testutil_fill_splitmix64.argtypes = [vp, u64, u64, vp]
         _lib = L
@@ -185,3 +197,73 @@ def fill_splitmix64(buf, state, stream=None):
                                                    _stream_handle(stream))
     _check(rc, "crc32c_testutil_fill_splitmix64")
     return buf
+
+
+# ---------------------------------------------------------------- host pipeline
+
+class Pipeline:
+    """Host-resident batches: pinned H2D -> kernel -> D2H over `nstreams` streams.
+
+    Arguments are host buffers (numpy arrays or pinned torch CPU tensors);
+    results come back in host memory.  Mirrors crc32c_pipeline_* in
+    include/fdb_crc32c.h.
+    """
+
+    def __init__(self, segment_bytes=64 << 20, nstreams=4, device=None):
+        import numpy as np  # noqa: F401
+        self._p = ctypes.c_void_p()
+        ctx = torch.cuda.device(device) if device is not None else _NullCtx()
+        with ctx:
+            _check(lib().crc32c_pipeline_create(ctypes.byref(self._p), segment_bytes, nstreams),
+                   "crc32c_pipeline_create")
+
+    def close(self):
+        if self._p:
+            lib().crc32c_pipeline_destroy(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _addr(a):
+        if isinstance(a, torch.Tensor):
+            if a.is_cuda:
+                raise CRC32CError("Pipeline takes host buffers")
+            return a.data_ptr()
+        return a.ctypes.data
+
+    def varlen(self, buf, offsets, lengths, seed=0, seeds=None, out=None):
+        import numpy as np
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        n = offsets.size
+        if out is None:
+            out = np.empty(n, dtype=np.uint32)
+        sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+        _check(lib().crc32c_pipeline_varlen(self._p, ctypes.c_void_p(self._addr(buf)), offsets.ctypes.data,
+                                            lengths.ctypes.data, n, seed & 0xFFFFFFFF,
+                                            None if sd is None else sd.ctypes.data, ctypes.c_void_p(self._addr(out))),
+               "crc32c_pipeline_varlen")
+        return out
+
+    def fixed(self, buf, stride, length, count, seed=0, seeds=None, out=None):
+        import numpy as np
+        if out is None:
+            out = np.empty(count, dtype=np.uint32)
+        sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+        _check(lib().crc32c_pipeline_fixed(self._p, ctypes.c_void_p(self._addr(buf)), stride, length, count,
+                                           seed & 0xFFFFFFFF, None if sd is None else sd.ctypes.data,
+                                           ctypes.c_void_p(self._addr(out))), "crc32c_pipeline_fixed")
+        return out
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -97,6 +97,17 @@ int check_launch(const char* what) {
 }
 
 }  // namespace
+
+// used by the host pipeline (crc32c_pipeline.cpp)
+int device_tables(const DevTables** tabs, int* num_cus) {
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	*tabs = st->tables;
+	*num_cus = st->num_cus;
+	return 0;
+}
+int set_error(int code, const char* what, hipError_t e) { return fail(code, what, e); }
+
 }  // namespace fdbcrc
 
 using namespace fdbcrc;

@@ -96,6 +96,28 @@ int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, co
                                uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
                                uint64_t workspace_bytes, void* stream);
 
+/* ---- Batched, host-resident (pinned H2D -> kernel -> D2H, overlapped) -- */
+
+/* The bytes start and end in host memory (pages read from disk, chunks of a
+ * file, packets from a socket).  The pipeline cuts the batch into segments of
+ * at most `segment_bytes` (covering byte range), round-robins them over
+ * `nstreams` HIP streams on the current device, and overlaps each segment's
+ * H2D copy with the previous segments' kernels and result copies.  Calls are
+ * synchronous: h_out is complete on return.  Host memory registered with
+ * crc32c_host_register (or allocated pinned) is copied directly; pageable
+ * memory is staged through the pipeline's pinned buffers.  A pipeline object
+ * is not thread-safe; use one per thread. */
+typedef struct fdb_crc32c_pipeline fdb_crc32c_pipeline;
+int crc32c_pipeline_create(fdb_crc32c_pipeline** out, uint64_t segment_bytes, int nstreams);
+void crc32c_pipeline_destroy(fdb_crc32c_pipeline* p);
+int crc32c_pipeline_varlen(fdb_crc32c_pipeline* p, const void* h_base, const uint64_t* h_offsets,
+                           const uint64_t* h_lengths, uint64_t count, uint32_t seed, const uint32_t* h_seeds,
+                           uint32_t* h_out);
+int crc32c_pipeline_fixed(fdb_crc32c_pipeline* p, const void* h_base, uint64_t stride, uint64_t length,
+                          uint64_t count, uint32_t seed, const uint32_t* h_seeds, uint32_t* h_out);
+int crc32c_host_register(void* h_ptr, uint64_t bytes);
+int crc32c_host_unregister(void* h_ptr);
+
 /* Text of the last error recorded on the calling thread ("" if none). */
 const char* crc32c_gpu_last_error(void);
 

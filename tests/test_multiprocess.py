@@ -1,0 +1,96 @@
+"""N>1 paths on CPU: world_size-2 gloo process groups exercising the sharding
+helpers and bench.py's multi-rank aggregation (no GPU)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import foundationdb_amd as F
+    from foundationdb_amd import parallel as P
+    from oracle import oracle as O
+    data = O.splitmix64(512 * 1000, 0x5EED).view(np.uint8)
+    # fixed pages
+    b, e = P.shard_bounds(1000, rank, world)
+    local = torch.tensor([F.crc32c_append(0xAB12FD93, data[4096 * i:4096 * (i + 1)]) for i in range(b, e)],
+                         dtype=torch.int64)
+    counts = [P.shard_bounds(1000, r, world)[1] - P.shard_bounds(1000, r, world)[0] for r in range(world)]
+    full = P.gather_checksums(local, counts).numpy().astype(np.uint32)
+    ok_fixed = np.array_equal(full, O.batch_fixed(data, 4096, 4096, 1000, seed=0xAB12FD93))
+    # byte-balanced varlen shards + whole-stream fold
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 9000, 300).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    b, e = P.shard_bounds_by_bytes(lens, rank, world)
+    seg = data[int(offs[b]):int(offs[b] + lens[b:e].sum())] if e > b else data[:0]
+    part = torch.tensor([F.crc32c_append(0, seg), int(lens[b:e].sum())], dtype=torch.int64)
+    parts = [torch.empty_like(part) for _ in range(world)]
+    dist.all_gather(parts, part)
+    crc = P.fold_stream([int(p[0]) for p in parts], [int(p[1]) for p in parts], seed=7)
+    ok_stream = crc == O.crc32c(7, data[:int(lens.sum())])
+    out_q.put((rank, bool(ok_fixed), bool(ok_stream)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_shards_gather_and_fold():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(r[0] for r in res) == [0, 1]
+    assert all(r[1] and r[2] for r in res), res
+
+
+def test_shard_bounds_cover():
+    from foundationdb_amd import parallel as P
+    for count in (0, 1, 7, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            spans = [P.shard_bounds(count, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == count
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    lens = np.random.default_rng(0).integers(0, 1 << 20, 5000)
+    for world in (1, 2, 8):
+        spans = [P.shard_bounds_by_bytes(lens, r, world) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == lens.size
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+def test_bench_dry_run_two_ranks():
+    """bench.py's N>1 aggregation (barrier, max time over ranks, byte sum) under
+    torch.distributed.run with gloo on CPU (--dry-cpu: host checksums)."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "weak" and rec["parity_ok"]
+    assert rec["value"] > 0 and rec["steps"] == 3
