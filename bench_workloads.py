@@ -63,10 +63,10 @@ class CpuSample:
 
 
 class Pages:
-    kernel_name = "fdbcrc::k_pages"
 
     def __init__(self, dev, rank, page_bytes=4096, count=1 << 20, seed=0):
         self.dev, self.page_bytes, self.count, self.seed = dev, page_bytes, count, seed
+        self.kernel_name = "fdbcrc::k_pages4k" if page_bytes == 4096 else "fdbcrc::k_pages<2>"
         self.buf = torch.empty(count * page_bytes, dtype=torch.uint8, device=dev)
         F.fill_splitmix64(self.buf, STATE)
         self.out = torch.empty(count, dtype=torch.uint32, device=dev)
