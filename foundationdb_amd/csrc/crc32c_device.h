@@ -13,6 +13,7 @@ struct DevTables {
 	uint32_t slice4[4][256];    // [k]: byte followed by 3-k zero bytes (4-byte slicing T3..T0)
 	uint32_t inv_z[16][8][16];  // nibble tables of x^(-8z), z = 0..15: drop z trailing zero bytes
 	uint32_t pow2[64][8][16];   // nibble tables of x^(8*2^m): shift by arbitrary byte counts
+	uint32_t corr[4][16][8][16];  // x^(-8(z + 1024(3-t))): quarter t's team value -> piece register, minus z zeros
 };
 
 // Build the tables on the host (crc32c_tables.cpp).

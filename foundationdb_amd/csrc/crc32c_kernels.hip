@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include "crc32c_common.h"
 
 namespace fdbcrc {
@@ -118,27 +120,30 @@ __global__ __launch_bounds__(1024) void k_pages(const uint8_t* __restrict__ base
 
 // 4 KiB pages with the layout-B image (4-byte slicing: half the dependent
 // LDS round trips and a third less VALU than layout A).
-__device__ __forceinline__ uint32_t chain64_b(const uint32_t* lds, uint32_t s, const Block& b, uint32_t c4) {
-	s = feed16_b(lds, s, b.r[0], c4);
-	s = feed16_b(lds, s, b.r[1], c4);
-	s = feed16_b(lds, s, b.r[2], c4);
-	s = feed16_b(lds, s, b.r[3], c4);
-	return s;
-}
-
+// U pages per unit: U independent register chains interleave (ILP U) while
+// the next unit's U pages are in flight.  Groups of G = 2U*floor(64/2U) pages
+// share one seed vector load and one coalesced checksum store.
+template <int U>
 __device__ __forceinline__ void unit_crc_b(const uint32_t* lds, int lane, uint32_t c4, uint32_t c_lane,
-                                           Block (&u)[2], uint32_t sa, uint32_t sb, uint32_t& ca, uint32_t& cb) {
-	unswizzle(u[0]);
-	unswizzle(u[1]);
-	const uint32_t x0 = chain64_b(lds, lane == 0 ? ~sa : 0u, u[0], c4);
-	const uint32_t x1 = chain64_b(lds, lane == 0 ? ~sb : 0u, u[1], c4);
-	ca = ~wave_xor(mul_nibbles(lds, x0, c_lane));
-	cb = ~wave_xor(mul_nibbles(lds, x1, c_lane));
+                                           Block (&u)[U], const uint32_t (&s)[U], uint32_t (&crc)[U]) {
+#pragma unroll
+	for (int j = 0; j < U; ++j) unswizzle(u[j]);
+	uint32_t x[U];
+#pragma unroll
+	for (int j = 0; j < U; ++j) x[j] = lane == 0 ? ~s[j] : 0u;
+#pragma unroll
+	for (int r = 0; r < 4; ++r)
+#pragma unroll
+		for (int j = 0; j < U; ++j) x[j] = feed16_b(lds, x[j], u[j].r[r], c4);
+#pragma unroll
+	for (int j = 0; j < U; ++j) crc[j] = ~wave_xor(mul_nibbles(lds, x[j], c_lane));
 }
 
+template <int U>
 __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
                                                   uint32_t seed, const uint32_t* __restrict__ seeds,
                                                   uint32_t* __restrict__ out, const DevTables* __restrict__ tabs) {
+	constexpr uint64_t G = 2 * U * (64 / (2 * U));  // a whole number of loop iterations
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const LaneCtx c = make_ctx();
 	const uint32_t col4 = (c.lane & 31) * 4;
@@ -148,34 +153,42 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 	const uint64_t wave = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
 	const uint64_t waves = (uint64_t)gridDim.x * wpb;
 	uint64_t per = (count + waves - 1) / waves;
-	per = per > 64 ? (per + 63) & ~uint64_t(63) : (per + 1) & ~uint64_t(1);
+	per = per > G ? (per + G - 1) / G * G : (per + U - 1) / U * U;
 	const uint64_t begin = wave * per;
 	const uint64_t end = begin + per < count ? begin + per : count;
 	const uint64_t last = end ? end - 1 : 0;
+	// page index -> address, clamped into this wave's run: clamped duplicates
+	// are computed and discarded, so every load is consumed unconditionally
 	auto page = [&](uint64_t i) { return base + (i < end ? i : (begin < end ? last : 0)) * stride; };
-	Block u0[2], u1[2];
-	load_unit<1>(u0, page(begin), page(begin + 1), c.ld_off);  // in flight during the LDS fill
+	auto load_u = [&](Block (&u)[U], uint64_t i0) {
+#pragma unroll
+		for (int j = 0; j < U; ++j) load_block(u[j], page(i0 + j), c.ld_off);
+	};
+	Block u0[U], u1[U];
+	load_u(u0, begin);  // in flight during the LDS fill
 	fill_lds_b(lds, tabs);
 	if (begin >= end) return;
-	for (uint64_t first = begin; first < end; first += 64) {
-		const uint64_t n = end - first < 64 ? end - first : 64;
+	for (uint64_t first = begin; first < end; first += G) {
+		const uint64_t n = end - first < G ? end - first : G;
 		const uint32_t my_seed = seeds ? seeds[first + ((uint64_t)c.lane < n ? c.lane : 0)] : seed;
 		uint32_t mine = 0;  // lane k keeps the checksum of page first+k
-		for (uint64_t k = 0; k < n; k += 4) {
-			uint32_t ca, cb;
-			load_unit<1>(u1, page(first + k + 2), page(first + k + 3), c.ld_off);
+		for (uint64_t k = 0; k < n; k += 2 * U) {
+			uint32_t sd[U], crc[U];
+			load_u(u1, first + k + U);
 			__builtin_amdgcn_sched_barrier(0);
-			unit_crc_b(lds, c.lane, c4, c_lane, u0, rdlane(my_seed, (int)k),
-			           rdlane(my_seed, (int)(k + 1) & 63), ca, cb);
-			mine = (uint64_t)c.lane == k ? ca : mine;
-			mine = (uint64_t)c.lane == k + 1 ? cb : mine;
+#pragma unroll
+			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + j) & 63);
+			unit_crc_b<U>(lds, c.lane, c4, c_lane, u0, sd, crc);
+#pragma unroll
+			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + j ? crc[j] : mine;
 			__builtin_amdgcn_sched_barrier(0);
-			load_unit<1>(u0, page(first + k + 4), page(first + k + 5), c.ld_off);
+			load_u(u0, first + k + 2 * U);
 			__builtin_amdgcn_sched_barrier(0);
-			unit_crc_b(lds, c.lane, c4, c_lane, u1, rdlane(my_seed, (int)(k + 2) & 63),
-			           rdlane(my_seed, (int)(k + 3) & 63), ca, cb);
-			mine = (uint64_t)c.lane == k + 2 ? ca : mine;
-			mine = (uint64_t)c.lane == k + 3 ? cb : mine;
+#pragma unroll
+			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + U + j) & 63);
+			unit_crc_b<U>(lds, c.lane, c4, c_lane, u1, sd, crc);
+#pragma unroll
+			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + U + j ? crc[j] : mine;
 			__builtin_amdgcn_sched_barrier(0);
 		}
 		if ((uint64_t)c.lane < n) out[first + c.lane] = mine;
@@ -193,7 +206,16 @@ int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint
 	if (grid > (uint64_t)num_cus) grid = num_cus;
 	if (grid == 0) grid = 1;
 	switch (blocks_per_page) {
-		case 1: k_pages4k<<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
+		case 1: {
+			static const int u = getenv("FDBCRC_PAGES_U") ? atoi(getenv("FDBCRC_PAGES_U")) : 2;
+			if (u == 2)
+				k_pages4k<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs);
+			else if (u == 4)
+				k_pages4k<4><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs);
+			else
+				k_pages4k<3><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs);
+			break;
+		}
 		case 2: k_pages<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
 		default: return -1;
 	}

@@ -24,6 +24,8 @@ void build_dev_tables(DevTables* t) {
 	for (int l = 0; l < 64; ++l) mul_tables_nibble(xpow8(64u * (63 - l)), t->lane[l]);
 	// Variable shifts for pieces of split buffers and trailing-zero removal.
 	for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(z), t->inv_z[z]);
+	for (int q = 0; q < 4; ++q)
+		for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(z + 1024u * (3 - q)), t->corr[q][z]);
 	for (int m = 0; m < 64; ++m) {
 		// x^(8*2^m) by repeated squaring of x^8
 		uint32_t c = kOne >> 8;

@@ -36,9 +36,6 @@
 namespace fdbcrc {
 
 constexpr uint32_t kTile = 256;               // buffers per planning tile
-constexpr uint32_t kInvZOff = kLdsBytes;      // [16 z][8 nib][16 v] u32, broadcast reads       8 KiB
-constexpr uint32_t kTeamOff = kInvZOff + 0x2000;  // [8 nib][16 v][32 col] x^(8*64*(15-l%16))   16 KiB
-constexpr uint32_t kLdsVarlen = kTeamOff + 0x4000;  // 136 KiB
 constexpr uint64_t kSmall = 1024;             // pieces whose aligned span fits one 1 KiB quarter
 
 struct VarlenParams {
@@ -161,37 +158,20 @@ __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, ui
 // ---------------------------------------------------------------------------
 // main kernel helpers
 // ---------------------------------------------------------------------------
-__device__ void fill_lds_varlen(uint32_t* lds, const DevTables* __restrict__ t) {
-	const uint32_t* iz = &t->inv_z[0][0][0];
-	for (uint32_t q = threadIdx.x; q < 16 * 128; q += blockDim.x) lds[kInvZOff / 4 + q] = iz[q];
-	// team lane tables: column c multiplies by x^(8*64*(15 - c%16)) == lane[48 + c%16]
-	for (uint32_t q = threadIdx.x; q < 128 * 32; q += blockDim.x) {
-		const uint32_t col = q & 31, nv = q >> 5;
-		lds[kTeamOff / 4 + q] = (&t->lane[48 + (col & 15)][0][0])[nv];
-	}
-	fill_lds(lds, t);  // ends with __syncthreads()
-}
-
-// Uniform value times x^(-8z), z in [0, 15]: broadcast LDS reads.
-__device__ __forceinline__ uint32_t mul_inv_z(const uint32_t* lds, uint32_t v, uint32_t z) {
-	if (z == 0) return v;
-	const uint32_t base = kInvZOff + z * 512;
+// Uniform (wave-wide) multiply through nibble tables in global memory: the
+// value is uniform, so these are scalar-cache loads, off the LDS path.
+__device__ __forceinline__ uint32_t umul(const uint32_t (*tab)[16], uint32_t v) {
+	v = rdfirst(v);
 	uint32_t r = 0;
 #pragma unroll
-	for (int n = 0; n < 8; ++n) r ^= lds_rd(lds, base + n * 64 + ((v >> (4 * n)) & 15u) * 4);
+	for (int n = 0; n < 8; ++n) r ^= tab[n][(v >> (4 * n)) & 15u];
 	return r;
 }
 
-// Uniform value times x^(8d), d >= 0: one table multiply per set bit of d
-// (tables of x^(8*2^m) in global memory).
+// Uniform value times x^(8d), d >= 0: one table multiply per set bit of d.
 __device__ uint32_t mul_xpow(const DevTables* __restrict__ t, uint32_t v, uint64_t d) {
-	for (int m = 0; d; ++m, d >>= 1) {
-		if (!(d & 1)) continue;
-		uint32_t r = 0;
-#pragma unroll
-		for (int n = 0; n < 8; ++n) r ^= t->pow2[m][n][(v >> (4 * n)) & 15u];
-		v = r;
-	}
+	for (int m = 0; d; ++m, d >>= 1)
+		if (d & 1) v = umul(t->pow2[m], v);
 	return v;
 }
 
@@ -208,57 +188,81 @@ __device__ __forceinline__ uint64_t span_aligned(const Piece& p) {
 	return ((p.P1 + 15) & ~uint64_t(15)) - (p.P0 & ~uint64_t(15));
 }
 
-// Mask one loaded 16-byte chunk at address ca to the bytes of [P0, P1) and,
-// for a buffer's first piece, XOR the register value ~seed into the four
-// message bytes at P0.  Only called for loads whose 1 KiB window touches an
-// unaligned edge or the seed position.
-__device__ __forceinline__ u32x4 fix_chunk(u32x4 v, uint64_t ca, uint64_t P0, uint64_t P1, bool first,
-                                           uint32_t s0) {
-	const int64_t lo = (int64_t)P0 - (int64_t)ca;
-	const int64_t hi = (int64_t)P1 - (int64_t)ca;
-	const int lo16 = lo < 0 ? 0 : (lo > 16 ? 16 : (int)lo);
-	const int hi16 = hi < 0 ? 0 : (hi > 16 ? 16 : (int)hi);
-	const int il = lo < -8 ? -8 : (lo > 16 ? 16 : (int)lo);
+// Edge fix-ups of a piece, precomputed once (uniform):
+//   lead chunk  (P0 & ~15): keep bytes >= P0%16, XOR the register value ~seed
+//                           into the four message bytes at P0 (first piece)
+//   spill chunk (lead+16):  the seed bytes that cross into the next chunk
+//   tail chunk ((P1-1)&~15): keep bytes < P1 - tail
+struct Edges {
+	uint64_t lead, tail;
+	uint32_t lm[4], inj[4], tm[4], spill;
+	bool any_lead, any_tail, any_spill;
+};
+
+__device__ __forceinline__ Edges make_edges(const Piece& p) {
+	Edges e;
+	const int k0 = (int)(p.P0 & 15);
+	const int k1 = (int)((p.P1 - 1) & 15) + 1;
+	const uint32_t s0 = (p.flags & 1) ? ~p.seed : 0u;
+	e.lead = p.P0 & ~uint64_t(15);
+	e.tail = (p.P1 - 1) & ~uint64_t(15);
 #pragma unroll
 	for (int d = 0; d < 4; ++d) {
-		const int a = lo16 - 4 * d, b = hi16 - 4 * d;
-		const int ac = a < 0 ? 0 : (a > 4 ? 4 : a), bc = b < 0 ? 0 : (b > 4 ? 4 : b);
-		const uint64_t m64 = ((1ull << (8 * bc)) - 1) & ~((1ull << (8 * ac)) - 1);
-		uint32_t x = v[d] & (uint32_t)m64;
-		if (first) {
-			const int dl = il - 4 * d;
-			if (dl >= 0 && dl < 4) x ^= s0 << (8 * dl);
-			else if (dl < 0 && dl > -4) x ^= s0 >> (-8 * dl);
-		}
-		v[d] = x;
+		const int lo = k0 - 4 * d, hi = k1 - 4 * d;  // kept byte range of dword d: [lo, hi)
+		e.lm[d] = lo <= 0 ? ~0u : (lo >= 4 ? 0u : ~0u << (8 * lo));
+		e.tm[d] = hi >= 4 ? ~0u : (hi <= 0 ? 0u : ~0u >> (8 * (4 - hi)));
+		e.inj[d] = (lo >= 0 && lo < 4) ? s0 << (8 * lo) : ((lo < 0 && lo > -4) ? s0 >> (-8 * lo) : 0u);
 	}
-	return v;
+	e.spill = k0 > 12 ? s0 >> (8 * (16 - k0)) : 0u;
+	e.any_lead = k0 != 0 || (p.flags & 1);
+	e.any_tail = k1 != 16;
+	e.any_spill = e.spill != 0;
+	return e;
 }
 
-// Does the 1 KiB window [w, w+1024) need fix_chunk for piece p?
-__device__ __forceinline__ bool window_needs_fix(uint64_t w, const Piece& p) {
-	const bool e0 = (p.P0 & 15) && p.P0 >= w && p.P0 < w + 1024;
-	const bool e1 = (p.P1 & 15) && p.P1 > w && p.P1 < w + 1024;
-	const bool sd = (p.flags & 1) && p.P0 + 4 > w && p.P0 < w + 1024;
-	return e0 || e1 || sd;
+// Apply the edge fix-ups to the chunk this lane loaded at `ca` for one load
+// whose 1 KiB window starts at `w` (uniform early-out when the window has no edge).
+__device__ __forceinline__ void fix_edges(u32x4& r, uint64_t w, uint64_t ca, const Edges& e) {
+	const bool wl = e.any_lead && e.lead >= w && e.lead < w + 1024;
+	const bool wt = e.any_tail && e.tail >= w && e.tail < w + 1024;
+	const bool ws = e.any_spill && e.lead + 16 >= w && e.lead + 16 < w + 1024;
+	if (!(wl || wt || ws)) return;
+	const bool il = ca == e.lead, it = ca == e.tail, is = ca == e.lead + 16;
+#pragma unroll
+	for (int d = 0; d < 4; ++d) {
+		uint32_t m = (il ? e.lm[d] : ~0u) & (it ? e.tm[d] : ~0u);
+		uint32_t inj = il ? e.inj[d] : ((is && d == 0) ? e.spill : 0u);
+		r[d] = (r[d] & m) ^ inj;
+	}
 }
 
-__device__ __forceinline__ u32x4 load_window_chunk(uint64_t ca, const Piece& p) {
+__device__ __forceinline__ u32x4 load_chunk_if(uint64_t ca, const Piece& p) {
 	const bool ok = ca + 16 > p.P0 && ca < p.P1;
 	return ok ? ld16(reinterpret_cast<const uint8_t*>(ca)) : u32x4{0u, 0u, 0u, 0u};
 }
 
-__global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
-	__shared__ uint32_t lds[kLdsVarlen / 4];
-	fill_lds_varlen(lds, P.tabs);
+// Register chain over the lane's 64 contiguous bytes (layout B, 4-byte slicing).
+__device__ __forceinline__ uint32_t chain64_b(const uint32_t* lds, uint32_t s, const Block& b, uint32_t c4) {
+	s = feed16_b(lds, s, b.r[0], c4);
+	s = feed16_b(lds, s, b.r[1], c4);
+	s = feed16_b(lds, s, b.r[2], c4);
+	s = feed16_b(lds, s, b.r[3], c4);
+	return s;
+}
+
+__global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables* __restrict__ T) {
+	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const LaneCtx c = make_ctx();
-	const uint32_t c_team = kTeamOff | ((c.lane & 31) * 4);
+	const uint32_t col4 = (c.lane & 31) * 4;
+	const uint32_t c4 = col4 | 0x10000u;
+	const uint32_t c_lane = (kS4LaneOff + (c.lane >> 5) * 0x4000) | col4;
+	fill_lds_b(lds, T);
 	const uint64_t wpb = blockDim.x >> 6;
 	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
 	const uint64_t w = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
 	const bool fixed = P.offsets == nullptr;
 	uint64_t total = P.total, Q = P.quantum;
-	if (!fixed) {  // planner output (global address space, scalar loads)
+	if (!fixed) {  // planner output (global address space)
 		typedef __attribute__((address_space(1))) const uint64_t g_u64;
 		const g_u64* h = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
 		total = rdfirst64(h[0]);
@@ -277,12 +281,6 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 		start0 = i0 * P.length;
 	} else {
 		const uint64_t t = P.wave_tile[w];
-#ifdef FDBCRC_DEBUG
-		if (t * kTile >= P.count + kTile) {
-			if (c.lane == 0 && atomicAdd(&g_dbg[2], 1ull) == 0) { g_dbg[3] = t; g_dbg[4] = 4; }
-			return;
-		}
-#endif
 		i0 = t * kTile;
 		start0 = P.prefix[t];
 		bool found = false;
@@ -315,13 +313,9 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 		fetch(g.bi0, g.m_off, g.m_len, g.m_sd);
 		fetch(g.bi0 + 64, g.n_off, g.n_len, g.n_sd);
 	};
-	// next piece whose smallness == want_small; zero-length buffers and tiny
-	// (< 16 B) pieces are finished on the spot by the small sweep.
-	auto finish = [&](const Piece& p, uint32_t r, uint32_t z) {
-		// r: raw register contribution of the piece, extended with z zero bytes
-		const int64_t d = (int64_t)p.after - (int64_t)z;
-		if (d < 0) r = mul_inv_z(lds, r, (uint32_t)(-d));
-		else if (d > 0) r = mul_xpow(P.tabs, r, (uint64_t)d);
+	// final register contribution r of a piece (already aligned to the piece end)
+	auto store = [&](const Piece& p, uint32_t r) {
+		if (p.after) r = mul_xpow(T, r, p.after);
 #ifdef FDBCRC_DEBUG
 		if (p.buf >= P.count) {
 			if (c.lane == 0 && atomicAdd(&g_dbg[2], 1ull) == 0) { g_dbg[3] = p.buf; g_dbg[4] = 3; }
@@ -333,6 +327,8 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 			else atomicXor(P.out + p.buf, (p.flags & 1) ? ~r : r);
 		}
 	};
+	// next piece whose smallness == want_small; zero-length buffers and tiny
+	// (< 16 B) pieces are finished on the spot by the small sweep.
 	auto gen_next = [&](Gen& g, Piece& p, bool want_small) -> bool {
 		for (;;) {
 			if (g.i >= P.count || g.start >= hi) return false;
@@ -359,25 +355,28 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 			p.after = len - b;
 			p.seed = sd;
 			p.flags = (a == 0 ? 1u : 0u) | ((a != 0 || b != len) ? 2u : 0u);
-			if (b - a < 16) {  // tiny piece: byte-serial, wave-uniform
+			if (b - a < 16) {  // tiny piece: byte-serial, wave-uniform, layout-B T0
 				if (want_small) {
 					uint32_t s = (p.flags & 1) ? ~sd : 0u;
-					s = feed_bytes(lds, s, reinterpret_cast<const uint8_t*>(p.P0),
-					               reinterpret_cast<const uint8_t*>(p.P1), c.c_slice);
-					finish(p, s, 0);
+					for (uint64_t q2 = p.P0; q2 < p.P1; ++q2) {
+						const uint32_t x = s ^ ld1(reinterpret_cast<const uint8_t*>(q2));
+						s = (s >> 8) ^ lds_rd(lds, __builtin_amdgcn_perm(x, c4, 0x0c020400u) + 128);
+					}
+					store(p, s);
 				}
 				continue;
 			}
-			const bool small = span_aligned(p) <= kSmall;
-			if (small == want_small) return true;
+			if ((span_aligned(p) <= kSmall) == want_small) return true;
 		}
 	};
 
 	// ======================= sweep 1: small pieces, four per pass ==========
-	// Load k (k = 0..3) feeds quarter qk = {0,2,1,3}[k] = 16-lane team qk after
-	// unswizzle; team t checksums piece t inside the 1 KiB window ending at
-	// its aligned end.  The (up to) four piece descriptors live in lanes 0..3
-	// of a few VGPRs (writelane / readlane), keeping the SGPR budget free.
+	// Load k (k = 0..3) fetches quarter qk = {0,2,1,3}[k] = 16-lane team qk
+	// after unswizzle; team t checksums piece t inside the 1 KiB window ending
+	// at its aligned end.  Lane tables multiply lane l by x^(8*64*(63-l)), so
+	// team t's row sum carries an extra x^(8*1024*(3-t)), removed together
+	// with the z trailing zeros by one uniform multiply (corr tables).
+	// The four piece descriptors live in lanes 0..3 of a few VGPRs.
 	{
 		struct Quad {
 			uint64_t P0, P1, buf, after;
@@ -412,15 +411,15 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 			}
 		};
 		auto win = [](const Piece& p) -> uint64_t { return ((p.P1 + 15) & ~uint64_t(15)) - 1024; };
+		const int quarter[4] = {0, 2, 1, 3};
 		auto load_quad = [&](Block& b, const Quad& q) {
-			const int quarter[4] = {0, 2, 1, 3};
 #pragma unroll
 			for (int k = 0; k < 4; ++k) {
 				const int t = quarter[k];
 				b.r[k] = u32x4{0u, 0u, 0u, 0u};
 				if (t < q.n) {
 					const Piece p = piece_of(q, t);
-					b.r[k] = load_window_chunk(win(p) + c.ld_off, p);
+					b.r[k] = load_chunk_if(win(p) + c.ld_off, p);
 				}
 			}
 		};
@@ -432,21 +431,21 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 			gather(nxt);
 			if (nxt.n) load_quad(nb, nxt);
 			__builtin_amdgcn_sched_barrier(0);
-			const int quarter[4] = {0, 2, 1, 3};
 #pragma unroll
 			for (int k = 0; k < 4; ++k) {
 				const int t = quarter[k];
 				if (t < cur.n) {
 					const Piece p = piece_of(cur, t);
-					if (window_needs_fix(win(p), p))
-						b.r[k] = fix_chunk(b.r[k], win(p) + c.ld_off, p.P0, p.P1, p.flags & 1, ~p.seed);
+					const Edges e = make_edges(p);
+					fix_edges(b.r[k], win(p), win(p) + c.ld_off, e);
 				}
 			}
 			unswizzle(b);
-			const uint32_t x = row_xor(mul_nibbles(lds, chain64(lds, 0u, b, c.c_slice), c_team));
+			const uint32_t x = row_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
 			for (int t = 0; t < cur.n; ++t) {
 				const Piece p = piece_of(cur, t);
-				finish(p, rdlane(x, 16 * t), (uint32_t)(-p.P1 & 15));
+				const uint32_t z = (uint32_t)(-p.P1 & 15);
+				store(p, umul(T->corr[t][z], rdlane(x, 16 * t)));
 			}
 			__builtin_amdgcn_sched_barrier(0);
 			cur = nxt;
@@ -455,6 +454,8 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 	}
 
 	// ======================= sweep 2: large pieces, 4 KiB blocks ===========
+	// Blocks aligned to the piece's aligned end; each block's register sum is
+	// reduced to a uniform value and folded Horner-style with x^(8*4096).
 	{
 		Gen g;
 		gen_init(g);
@@ -464,17 +465,18 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 		auto vbase_of = [&](const Piece& p) -> uint64_t {
 			return ((p.P1 + 15) & ~uint64_t(15)) - 4096 * nblk_of(p);
 		};
+		const uint32_t koff[4] = {0, 2048, 1024, 3072};
 		auto load_blk = [&](Block& b, const Piece& p, uint64_t blk) {
 			const uint64_t bb = vbase_of(p) + 4096 * blk;
 			if (bb >= p.P0 && bb + 4096 <= p.P1) {
 				load_block(b, reinterpret_cast<const uint8_t*>(bb), c.ld_off);
 			} else {
-				const uint32_t koff[4] = {0, 2048, 1024, 3072};
 #pragma unroll
-				for (int k = 0; k < 4; ++k) b.r[k] = load_window_chunk(bb + koff[k] + c.ld_off, p);
+				for (int k = 0; k < 4; ++k) b.r[k] = load_chunk_if(bb + koff[k] + c.ld_off, p);
 			}
 		};
 		uint64_t blk = 0, cur_nblk = nblk_of(cur);
+		Edges e = make_edges(cur);
 		Block b, nb;
 		load_blk(b, cur, 0);
 		uint32_t acc = 0;
@@ -491,18 +493,21 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P) {
 			if (more) load_blk(nb, nxt, nblk_idx);
 			__builtin_amdgcn_sched_barrier(0);
 			const uint64_t bb = vbase_of(cur) + 4096 * blk;
-			const uint32_t koff[4] = {0, 2048, 1024, 3072};
+			// edges live in the first block, the last block, and (seed bytes
+			// spilling over a chunk boundary) possibly the second: fix_edges'
+			// uniform per-window test decides
 #pragma unroll
-			for (int k = 0; k < 4; ++k)
-				if (window_needs_fix(bb + koff[k], cur))
-					b.r[k] = fix_chunk(b.r[k], bb + koff[k] + c.ld_off, cur.P0, cur.P1, cur.flags & 1, ~cur.seed);
+			for (int k = 0; k < 4; ++k) fix_edges(b.r[k], bb + koff[k], bb + koff[k] + c.ld_off, e);
 			unswizzle(b);
-			const uint32_t x = chain64(lds, 0u, b, c.c_slice);
-			acc = blk ? mul_nibbles(lds, acc, c.c_block) ^ x : x;
-			if (blk + 1 == cur_nblk) finish(cur, wave_xor(mul_nibbles(lds, acc, c.c_lane)), (uint32_t)(-cur.P1 & 15));
+			const uint32_t v = wave_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
+			acc = blk ? umul(T->block, acc) ^ v : v;
+			if (blk + 1 == cur_nblk) store(cur, umul(T->corr[3][(uint32_t)(-cur.P1 & 15)], acc));
 			__builtin_amdgcn_sched_barrier(0);
 			if (!more) break;
-			if (nblk_idx == 0) cur_nblk = nblk_of(nxt);
+			if (nblk_idx == 0) {
+				cur_nblk = nblk_of(nxt);
+				e = make_edges(nxt);
+			}
 			cur = nxt;
 			blk = nblk_idx;
 			b = nb;
@@ -534,7 +539,7 @@ int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 	P.base = base; P.offsets = offsets; P.lengths = lengths; P.count = count;
 	P.seed = seed; P.seeds = seeds; P.out = out;
 	P.prefix = prefix; P.wave_tile = wave_tile; P.hdr = hdr; P.tabs = tabs;
-	k_varlen<<<(unsigned)grid, 1024, 0, stream>>>(P);
+	k_varlen<<<(unsigned)grid, 1024, 0, stream>>>(P, tabs);
 	return 0;
 }
 
@@ -556,7 +561,7 @@ int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, 
 		P.quantum = per < 4096 ? 4096 : (per + 4095) & ~uint64_t(4095);
 		if (hipMemsetAsync(out, 0, 4 * count, stream) != hipSuccess) return -1;
 	}
-	k_varlen<<<(unsigned)grid, 1024, 0, stream>>>(P);
+	k_varlen<<<(unsigned)grid, 1024, 0, stream>>>(P, tabs);
 	return 0;
 }
 
