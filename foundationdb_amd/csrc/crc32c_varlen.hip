@@ -33,6 +33,10 @@
 
 #include "crc32c_common.h"
 
+#ifndef FDBCRC_EXP
+#define FDBCRC_EXP 0  // development timing experiments only (wrong results when set)
+#endif
+
 namespace fdbcrc {
 
 constexpr uint32_t kTile = 256;               // buffers per planning tile
@@ -199,21 +203,43 @@ struct Edges {
 	bool any_lead, any_tail, any_spill;
 };
 
+// Byte masks of a 16-byte chunk from 64-bit shifts: keep bytes >= k0 (lead),
+// keep bytes < k1 (tail), and the register value s0 placed at byte k0
+// (its bytes past the chunk end spill into the next chunk).
+struct Masks {
+	uint32_t lm[4], tm[4], inj[4], spill;
+};
+__device__ __forceinline__ Masks edge_masks(uint32_t k0, uint32_t k1, uint32_t s0) {
+	const uint64_t ones = ~uint64_t(0), s = s0;
+	const uint64_t lmLo = k0 >= 8 ? 0 : ones << (8 * k0);
+	const uint64_t lmHi = k0 <= 8 ? ones : ones << (8 * (k0 - 8));
+	const uint64_t tmLo = k1 >= 8 ? ones : ones >> (64 - 8 * k1);
+	const uint64_t tmHi = k1 <= 8 ? 0 : ones >> (128 - 8 * k1);
+	const uint64_t injLo = k0 >= 8 ? 0 : s << (8 * k0);
+	const uint64_t injHi = k0 >= 8 ? s << (8 * (k0 - 8)) : (k0 > 4 ? s >> (8 * (8 - k0)) : 0);
+	Masks m;
+	m.lm[0] = (uint32_t)lmLo; m.lm[1] = (uint32_t)(lmLo >> 32); m.lm[2] = (uint32_t)lmHi; m.lm[3] = (uint32_t)(lmHi >> 32);
+	m.tm[0] = (uint32_t)tmLo; m.tm[1] = (uint32_t)(tmLo >> 32); m.tm[2] = (uint32_t)tmHi; m.tm[3] = (uint32_t)(tmHi >> 32);
+	m.inj[0] = (uint32_t)injLo; m.inj[1] = (uint32_t)(injLo >> 32); m.inj[2] = (uint32_t)injHi; m.inj[3] = (uint32_t)(injHi >> 32);
+	m.spill = k0 > 12 ? s0 >> (8 * (16 - k0)) : 0u;
+	return m;
+}
+
 __device__ __forceinline__ Edges make_edges(const Piece& p) {
 	Edges e;
-	const int k0 = (int)(p.P0 & 15);
-	const int k1 = (int)((p.P1 - 1) & 15) + 1;
+	const uint32_t k0 = (uint32_t)(p.P0 & 15);
+	const uint32_t k1 = (uint32_t)((p.P1 - 1) & 15) + 1;
 	const uint32_t s0 = (p.flags & 1) ? ~p.seed : 0u;
+	const Masks m = edge_masks(rdfirst(k0), rdfirst(k1), rdfirst(s0));
 	e.lead = p.P0 & ~uint64_t(15);
 	e.tail = (p.P1 - 1) & ~uint64_t(15);
 #pragma unroll
 	for (int d = 0; d < 4; ++d) {
-		const int lo = k0 - 4 * d, hi = k1 - 4 * d;  // kept byte range of dword d: [lo, hi)
-		e.lm[d] = lo <= 0 ? ~0u : (lo >= 4 ? 0u : ~0u << (8 * lo));
-		e.tm[d] = hi >= 4 ? ~0u : (hi <= 0 ? 0u : ~0u >> (8 * (4 - hi)));
-		e.inj[d] = (lo >= 0 && lo < 4) ? s0 << (8 * lo) : ((lo < 0 && lo > -4) ? s0 >> (-8 * lo) : 0u);
+		e.lm[d] = m.lm[d];
+		e.tm[d] = m.tm[d];
+		e.inj[d] = m.inj[d];
 	}
-	e.spill = k0 > 12 ? s0 >> (8 * (16 - k0)) : 0u;
+	e.spill = m.spill;
 	e.any_lead = k0 != 0 || (p.flags & 1);
 	e.any_tail = k1 != 16;
 	e.any_spill = e.spill != 0;
@@ -250,12 +276,61 @@ __device__ __forceinline__ uint32_t chain64_b(const uint32_t* lds, uint32_t s, c
 	return s;
 }
 
+// ---------------------------------------------------------------------------
+// main kernel
+// ---------------------------------------------------------------------------
+// Per-lane metadata of one BATCH of 64 consecutive buffers: lane j describes
+// the piece of buffer bi0 + j that lies in this wave's byte range.
+constexpr uint32_t kNone = 0, kDirect = 1, kSmallC = 2, kLargeC = 3;  // info bits 0-1
+constexpr uint32_t kFirst = 4, kSplit = 8;                              // info bits 2, 3
+struct Meta {
+	uint64_t P0, P1;   // piece [P0, P1), device addresses
+	uint64_t after;    // bytes of the buffer after P1
+	uint32_t s0;       // register value entering at P0: ~seed for a buffer's first piece, else 0
+	uint32_t info;
+	uint32_t geo;      // small pieces: k0 = P0%16 | k1 = (P1-1)%16+1 << 8 | lead chunk offset in the 1 KiB window << 16
+};
+// Uniform state of one ring slot (a built batch).
+struct Slot {
+	uint64_t bi0;
+	uint64_t mask;      // pieces of the current sweep's class not yet taken
+	uint32_t pending;   // taken work items not yet computed
+	bool valid;
+};
+
+__device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d); }
+
+// Inclusive prefix sum of a 64-bit value over the wave.
+__device__ __forceinline__ uint64_t scan64(uint64_t v, int lane) {
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint64_t y = ((uint64_t)shup((uint32_t)(v >> 32), d) << 32) | shup((uint32_t)v, d);
+		if (lane >= d) v += y;
+	}
+	return v;
+}
+
+__device__ __forceinline__ uint32_t gld32(const uint32_t* p) {
+	typedef __attribute__((address_space(1))) const uint32_t g_u32;
+	return *((g_u32*)reinterpret_cast<uintptr_t>(p));
+}
+
+// Lane-parallel multiply by the per-lane constant whose nibble tables start
+// at `tab` (global memory, 8 x 16 words).
+__device__ __forceinline__ uint32_t vmul(const uint32_t* tab, uint32_t v) {
+	uint32_t r = 0;
+#pragma unroll
+	for (int n = 0; n < 8; ++n) r ^= gld32(tab + n * 16 + ((v >> (4 * n)) & 15u));
+	return r;
+}
+
 __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables* __restrict__ T) {
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const LaneCtx c = make_ctx();
-	const uint32_t col4 = (c.lane & 31) * 4;
+	const int lane = c.lane;
+	const uint32_t col4 = (lane & 31) * 4;
 	const uint32_t c4 = col4 | 0x10000u;
-	const uint32_t c_lane = (kS4LaneOff + (c.lane >> 5) * 0x4000) | col4;
+	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
 	fill_lds_b(lds, T);
 	const uint64_t wpb = blockDim.x >> 6;
 	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
@@ -272,101 +347,148 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 	const uint64_t hi = w + 1 == nwave ? ~uint64_t(0) : lo + Q;
 	if (lo > total || P.count == 0) return;
 
-	auto rd64 = [](uint64_t v, int k) -> uint64_t { return rdlane64(v, k); };
-
-	// ---- locate the first buffer touching [lo, hi)
-	uint64_t i0, start0;
+	// first batch of the range: the planning tile holding byte lo (buffers
+	// before lo are classified kNone by build())
+	uint64_t first_bi0, first_start;
 	if (fixed) {
-		i0 = P.length ? lo / P.length : 0;
-		start0 = i0 * P.length;
+		first_bi0 = P.length ? lo / P.length : 0;
+		if (P.length == 0) first_bi0 = 0;
+		first_start = first_bi0 * P.length;
 	} else {
 		const uint64_t t = P.wave_tile[w];
-		i0 = t * kTile;
-		start0 = P.prefix[t];
-		bool found = false;
-		while (!found && i0 < P.count) {
-			const uint64_t mylen = i0 + c.lane < P.count ? P.lengths[i0 + c.lane] : 0;
-			for (int k = 0; k < 64 && i0 < P.count; ++k) {
-				const uint64_t len = rd64(mylen, k);
-				if (start0 + len > lo || (len == 0 && start0 >= lo)) { found = true; break; }
-				start0 += len;
-				++i0;
-			}
-		}
+		first_bi0 = t * kTile;
+		first_start = P.prefix[t];
 	}
 
-	// ---- piece generator over [lo, hi); metadata 64 buffers per batch
-	struct Gen {
-		uint64_t i, start, bi0;
-		uint64_t m_off, m_len, n_off, n_len;
-		uint32_t m_sd, n_sd;
-	};
-	auto fetch = [&](uint64_t b0, uint64_t& off, uint64_t& len, uint32_t& sd) {
-		const uint64_t j = b0 + c.lane;
+	// ---- batch builder (lane-parallel) ----------------------------------
+	uint64_t nb_bi0 = first_bi0, nb_start = first_start;
+	bool more = true;
+	auto build = [&](Meta& m, Slot& s, uint32_t want) {
+		const uint64_t bi0 = nb_bi0;
+		const uint64_t j = bi0 + lane;
 		const bool ok = j < P.count;
-		off = fixed ? j * P.stride : (ok ? P.offsets[j] : 0);
-		len = fixed ? P.length : (ok ? P.lengths[j] : 0);
-		sd = P.seeds ? (ok ? P.seeds[j] : 0) : P.seed;
-	};
-	auto gen_init = [&](Gen& g) {
-		g.i = i0; g.start = start0; g.bi0 = i0;
-		fetch(g.bi0, g.m_off, g.m_len, g.m_sd);
-		fetch(g.bi0 + 64, g.n_off, g.n_len, g.n_sd);
-	};
-	// final register contribution r of a piece (already aligned to the piece end)
-	auto store = [&](const Piece& p, uint32_t r) {
-		if (p.after) r = mul_xpow(T, r, p.after);
-#ifdef FDBCRC_DEBUG
-		if (p.buf >= P.count) {
-			if (c.lane == 0 && atomicAdd(&g_dbg[2], 1ull) == 0) { g_dbg[3] = p.buf; g_dbg[4] = 3; }
-			return;
+		uint64_t off = 0, len = 0, st;
+		uint32_t sd = P.seed;
+		if (fixed) {
+			off = j * P.stride;
+			len = ok ? P.length : 0;
+			st = j * P.length;
+			nb_start = (bi0 + 64) * P.length;
+		} else {
+			if (ok) {
+				off = P.offsets[j];
+				len = P.lengths[j];
+			}
+			const uint64_t incl = scan64(len, lane);
+			st = nb_start + incl - len;
+			nb_start += rdlane64(incl, 63);
 		}
-#endif
-		if (c.lane == 0) {
-			if (!(p.flags & 2)) P.out[p.buf] = ~r;
-			else atomicXor(P.out + p.buf, (p.flags & 1) ? ~r : r);
+		if (P.seeds && ok) sd = P.seeds[j];
+		nb_bi0 = bi0 + 64;
+		more = nb_bi0 < P.count && nb_start < hi;
+		const bool in = ok && st < hi && (st + len > lo || (len == 0 && st >= lo));
+		const uint64_t a = lo > st ? lo - st : 0;
+		const uint64_t b = in ? (hi - st < len ? hi - st : len) : 0;
+		const uint64_t q = reinterpret_cast<uint64_t>(P.base) + off;
+		m.P0 = q + a;
+		m.P1 = q + b;
+		m.after = in ? len - b : 0;
+		m.s0 = a == 0 ? ~sd : 0u;
+		const uint64_t wend = (m.P1 + 15) & ~uint64_t(15);
+		m.geo = (uint32_t)(m.P0 & 15) | (((uint32_t)((m.P1 - 1) & 15) + 1) << 8) |
+		        ((uint32_t)((m.P0 & ~uint64_t(15)) - (wend - 1024)) << 16);
+		uint32_t cls = kNone;
+		if (in) {
+			const uint64_t span = ((m.P1 + 15) & ~uint64_t(15)) - (m.P0 & ~uint64_t(15));
+			cls = b - a < 16 ? kDirect : (span <= kSmall ? kSmallC : kLargeC);
+		}
+		m.info = cls | (a == 0 ? kFirst : 0u) | ((a != 0 || b != len) ? kSplit : 0u);
+		s.bi0 = bi0;
+		s.mask = __ballot(cls == want);
+		s.pending = 0;
+		s.valid = true;
+	};
+	// Finish the pieces of class `want` (kSmallC also finishes kDirect) of a
+	// batch: remove the team offset and the z zero bytes (corr tables), shift
+	// split pieces by the bytes after them, store or XOR-merge.
+	auto finalize = [&](const Meta& m, uint64_t bi0, uint32_t x, uint32_t t, uint32_t want) {
+		const uint32_t cls = m.info & 3;
+		const bool mine = cls == want || (want == kSmallC && cls == kDirect);
+		uint32_t r = x;
+		if (mine && cls == kDirect) {  // < 16 bytes or empty: byte-serial per lane
+			r = m.s0;
+			for (uint64_t p = m.P0; p < m.P1; ++p) {
+				const uint32_t y = r ^ ld1(reinterpret_cast<const uint8_t*>(p));
+				r = (r >> 8) ^ lds_rd(lds, __builtin_amdgcn_perm(y, c4, 0x0c020400u) + 128);
+			}
+		} else if (mine) {
+			r = vmul(&T->corr[t][(uint32_t)(-m.P1 & 15)][0][0], x);
+		}
+		uint64_t am = __ballot(mine && m.after != 0);
+		while (am) {  // split pieces ending before their buffer does: at most one per wave
+			const int k = __builtin_ctzll(am);
+			am &= am - 1;
+			const uint32_t v = mul_xpow(T, rdlane(r, k), rdlane64(m.after, k));
+			r = lane == k ? v : r;
+		}
+		if (mine) {
+			uint32_t* o = P.out + bi0 + lane;
+			if (m.info & kSplit) atomicXor(o, (m.info & kFirst) ? ~r : r);
+			else *o = ~r;
 		}
 	};
-	// next piece whose smallness == want_small; zero-length buffers and tiny
-	// (< 16 B) pieces are finished on the spot by the small sweep.
-	auto gen_next = [&](Gen& g, Piece& p, bool want_small) -> bool {
-		for (;;) {
-			if (g.i >= P.count || g.start >= hi) return false;
-			if (g.i - g.bi0 == 64) {
-				g.bi0 += 64;
-				g.m_off = g.n_off; g.m_len = g.n_len; g.m_sd = g.n_sd;
-				fetch(g.bi0 + 64, g.n_off, g.n_len, g.n_sd);
-			}
-			const int k = (int)(g.i - g.bi0);
-			const uint64_t off = rd64(g.m_off, k), len = rd64(g.m_len, k);
-			const uint32_t sd = rdlane(g.m_sd, k);
-			const uint64_t a = lo > g.start ? lo - g.start : 0;
-			const uint64_t b = hi - g.start < len ? hi - g.start : len;
-			p.buf = g.i;
-			++g.i;
-			g.start += len;
-			if (len == 0) {
-				if (want_small && c.lane == 0) P.out[p.buf] = sd;
-				continue;
-			}
-			const uint64_t q = reinterpret_cast<uint64_t>(P.base) + off;
-			p.P0 = q + a;
-			p.P1 = q + b;
-			p.after = len - b;
-			p.seed = sd;
-			p.flags = (a == 0 ? 1u : 0u) | ((a != 0 || b != len) ? 2u : 0u);
-			if (b - a < 16) {  // tiny piece: byte-serial, wave-uniform, layout-B T0
-				if (want_small) {
-					uint32_t s = (p.flags & 1) ? ~sd : 0u;
-					for (uint64_t q2 = p.P0; q2 < p.P1; ++q2) {
-						const uint32_t x = s ^ ld1(reinterpret_cast<const uint8_t*>(q2));
-						s = (s >> 8) ^ lds_rd(lds, __builtin_amdgcn_perm(x, c4, 0x0c020400u) + 128);
-					}
-					store(p, s);
-				}
-				continue;
-			}
-			if ((span_aligned(p) <= kSmall) == want_small) return true;
+
+	Meta m0, m1;
+	Slot s0, s1;
+	uint32_t x0 = 0, x1 = 0, t0 = 0, t1 = 0;  // per-lane results awaiting finalize
+	auto reset = [&](uint32_t want) {
+		nb_bi0 = first_bi0;
+		nb_start = first_start;
+		more = true;
+		build(m0, s0, want);
+		s1.valid = false;
+		s1.mask = 0;
+		s1.pending = 0;
+		if (more) build(m1, s1, want);
+	};
+	// slot with work left, older batch first (-1: none)
+	auto pick = [&]() -> int {
+		const bool a = s0.valid && s0.mask, b = s1.valid && s1.mask;
+		if (a && b) return s0.bi0 < s1.bi0 ? 0 : 1;
+		return a ? 0 : (b ? 1 : -1);
+	};
+	auto deposit = [&](int slot, int j, uint32_t v, uint32_t t) {
+		if (slot) {
+			x1 = lane == j ? v : x1;
+			t1 = lane == j ? t : t1;
+		} else {
+			x0 = lane == j ? v : x0;
+			t0 = lane == j ? t : t0;
+		}
+	};
+	auto piece_at = [&](int slot, int j) -> Piece {
+		const Meta& m = slot ? m1 : m0;
+		Piece p;
+		p.P0 = rdlane64(m.P0, j);
+		p.P1 = rdlane64(m.P1, j);
+		p.seed = ~rdlane(m.s0, j);
+		p.flags = rdlane(m.info, j) & kFirst ? 1u : 0u;
+		p.buf = 0;
+		p.after = 0;
+		return p;
+	};
+	// finalize + rebuild every slot whose work is done; `busy` = slot of a
+	// large piece that still has blocks to take (-1: none)
+	auto retire = [&](uint32_t want, int busy) {
+		if (s0.valid && !s0.mask && !s0.pending && busy != 0) {
+			finalize(m0, s0.bi0, x0, t0, want);
+			s0.valid = false;
+			if (more) build(m0, s0, want);
+		}
+		if (s1.valid && !s1.mask && !s1.pending && busy != 1) {
+			finalize(m1, s1.bi0, x1, t1, want);
+			s1.valid = false;
+			if (more) build(m1, s1, want);
 		}
 	};
 
@@ -375,142 +497,194 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 	// after unswizzle; team t checksums piece t inside the 1 KiB window ending
 	// at its aligned end.  Lane tables multiply lane l by x^(8*64*(63-l)), so
 	// team t's row sum carries an extra x^(8*1024*(3-t)), removed together
-	// with the z trailing zeros by one uniform multiply (corr tables).
-	// The four piece descriptors live in lanes 0..3 of a few VGPRs.
+	// with the z trailing zeros by the corr tables in finalize().
 	{
-		struct Quad {
-			uint64_t P0, P1, buf, after;
-			uint32_t seed, flags;
-			int n;
+		struct Item {
+			int slot, n;
+			int j[4];
 		};
-		auto wl64 = [&](uint64_t old, uint64_t v, int k) -> uint64_t { return c.lane == k ? v : old; };
-		auto wl32 = [&](uint32_t old, uint32_t v, int k) -> uint32_t { return c.lane == k ? v : old; };
-		auto piece_of = [&](const Quad& q, int t) -> Piece {
-			Piece p;
-			p.P0 = rd64(q.P0, t);
-			p.P1 = rd64(q.P1, t);
-			p.buf = rd64(q.buf, t);
-			p.after = rd64(q.after, t);
-			p.seed = rdlane(q.seed, t);
-			p.flags = rdlane(q.flags, t);
-			return p;
-		};
-		Gen g;
-		gen_init(g);
-		auto gather = [&](Quad& q) {
-			q.n = 0;
-			Piece p;
-			while (q.n < 4 && gen_next(g, p, true)) {
-				q.P0 = wl64(q.P0, p.P0, q.n);
-				q.P1 = wl64(q.P1, p.P1, q.n);
-				q.buf = wl64(q.buf, p.buf, q.n);
-				q.after = wl64(q.after, p.after, q.n);
-				q.seed = wl32(q.seed, p.seed, q.n);
-				q.flags = wl32(q.flags, p.flags, q.n);
-				++q.n;
+		auto take = [&](Item& it) {
+			it.n = 0;
+			const int s = pick();
+			if (s < 0) return;
+			Slot& S = s ? s1 : s0;
+			it.slot = s;
+			uint64_t mk = S.mask;
+#pragma unroll
+			for (int t = 0; t < 4; ++t) {
+				if (mk) {
+					it.j[t] = __builtin_ctzll(mk);
+					mk &= mk - 1;
+					it.n = t + 1;
+				}
 			}
+			S.mask = mk;
+			S.pending += 1;
 		};
-		auto win = [](const Piece& p) -> uint64_t { return ((p.P1 + 15) & ~uint64_t(15)) - 1024; };
+		auto win = [](uint64_t P1) -> uint64_t { return ((P1 + 15) & ~uint64_t(15)) - 1024; };
 		const int quarter[4] = {0, 2, 1, 3};
-		auto load_quad = [&](Block& b, const Quad& q) {
+		// the window ends at the piece's aligned end, so chunk ld_off belongs
+		// to the piece iff ld_off >= the lead chunk's offset
+		auto load_item = [&](Block& b, const Item& it) {
 #pragma unroll
 			for (int k = 0; k < 4; ++k) {
 				const int t = quarter[k];
 				b.r[k] = u32x4{0u, 0u, 0u, 0u};
-				if (t < q.n) {
-					const Piece p = piece_of(q, t);
-					b.r[k] = load_chunk_if(win(p) + c.ld_off, p);
+				if (t < it.n) {
+					const Meta& m = it.slot ? m1 : m0;
+					const uint64_t w0 = win(rdlane64(m.P1, it.j[t]));
+					const uint32_t lead_rel = rdlane(m.geo, it.j[t]) >> 16;
+					if (c.ld_off >= lead_rel) b.r[k] = ld16(reinterpret_cast<const uint8_t*>(w0 + c.ld_off));
 				}
 			}
 		};
-		Quad cur{}, nxt{};
-		gather(cur);
-		Block b, nb;
-		if (cur.n) load_quad(b, cur);
-		while (cur.n) {
-			gather(nxt);
-			if (nxt.n) load_quad(nb, nxt);
-			__builtin_amdgcn_sched_barrier(0);
+		// lead chunk: mask + seed; next chunk: seed spill; lane 63 holds the
+		// window's last chunk = the tail chunk
+		auto fix_item = [&](u32x4& r, int slot, int j) {
+			const Meta& m = slot ? m1 : m0;
+			const uint32_t geo = rdlane(m.geo, j);
+			const Masks mk = edge_masks(geo & 15u, (geo >> 8) & 31u, rdlane(m.s0, j));
+			const uint32_t lead_rel = geo >> 16;
+			const bool il = c.ld_off == lead_rel, is = c.ld_off == lead_rel + 16, it = lane == 63;
 #pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const int t = quarter[k];
-				if (t < cur.n) {
-					const Piece p = piece_of(cur, t);
-					const Edges e = make_edges(p);
-					fix_edges(b.r[k], win(p), win(p) + c.ld_off, e);
-				}
+			for (int d = 0; d < 4; ++d) {
+				const uint32_t mm = il ? mk.lm[d] : (it ? mk.tm[d] : ~0u);
+				const uint32_t x = il ? mk.inj[d] : ((d == 0 && is) ? mk.spill : 0u);
+				r[d] = (r[d] & mm) ^ x;
 			}
-			unswizzle(b);
-			const uint32_t x = row_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
-			for (int t = 0; t < cur.n; ++t) {
-				const Piece p = piece_of(cur, t);
-				const uint32_t z = (uint32_t)(-p.P1 & 15);
-				store(p, umul(T->corr[t][z], rdlane(x, 16 * t)));
+		};
+		reset(kSmallC);
+		Item cur, nxt;
+		cur.n = 0;
+		Block b, nb;
+		for (;;) {
+			take(nxt);
+			if (nxt.n) load_item(nb, nxt);
+			__builtin_amdgcn_sched_barrier(0);
+			if (cur.n) {
+#pragma unroll
+				for (int k = 0; k < 4; ++k) {
+					const int t = quarter[k];
+					if (t < cur.n) fix_item(b.r[k], cur.slot, cur.j[t]);
+				}
+				unswizzle(b);
+				const uint32_t x = row_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
+#pragma unroll
+				for (int t = 0; t < 4; ++t)
+					if (t < cur.n) deposit(cur.slot, cur.j[t], rdlane(x, 16 * t), (uint32_t)t);
+				if (cur.slot) s1.pending -= 1; else s0.pending -= 1;
 			}
 			__builtin_amdgcn_sched_barrier(0);
+			retire(kSmallC, -1);
+			if (!nxt.n && !cur.n && !s0.valid && !s1.valid) break;
 			cur = nxt;
 			b = nb;
 		}
 	}
 
 	// ======================= sweep 2: large pieces, 4 KiB blocks ===========
-	// Blocks aligned to the piece's aligned end; each block's register sum is
-	// reduced to a uniform value and folded Horner-style with x^(8*4096).
+	// Blocks aligned to the piece's aligned end, taken two at a time (two
+	// register chains interleave, next two blocks in flight).  Each block's
+	// register sum is reduced to a uniform value and folded Horner-style with
+	// x^(8*4096); the piece total goes to its batch lane for finalize().
 	{
-		Gen g;
-		gen_init(g);
-		Piece cur, nxt;
-		if (!gen_next(g, cur, false)) return;
-		auto nblk_of = [](const Piece& p) -> uint64_t { return (span_aligned(p) + 4095) >> 12; };
-		auto vbase_of = [&](const Piece& p) -> uint64_t {
-			return ((p.P1 + 15) & ~uint64_t(15)) - 4096 * nblk_of(p);
+		struct Blk {
+			uint64_t bb;       // block address (aligned to the piece's aligned end)
+			int slot, j;
+			uint32_t flags;    // bit0 valid, bit1 first block, bit2 last block, bit3 may hold an edge
 		};
+		// active piece (uniform)
+		bool act = false;
+		int a_slot = 0, a_j = 0;
+		uint64_t a_blk = 0, a_nblk = 0, a_vbase = 0, a_P0 = 0, a_P1 = 0;
 		const uint32_t koff[4] = {0, 2048, 1024, 3072};
-		auto load_blk = [&](Block& b, const Piece& p, uint64_t blk) {
-			const uint64_t bb = vbase_of(p) + 4096 * blk;
-			if (bb >= p.P0 && bb + 4096 <= p.P1) {
+		// take the next block of the stream and issue its loads
+		auto take = [&](Blk& d, Block& b) {
+			d.flags = 0;
+			if (!act) {
+				const int s = pick();
+				if (s < 0) {
+#pragma unroll
+					for (int k = 0; k < 4; ++k) b.r[k] = u32x4{0u, 0u, 0u, 0u};
+					return;
+				}
+				Slot& S = s ? s1 : s0;
+				const Meta& m = s ? m1 : m0;
+				a_slot = s;
+				a_j = __builtin_ctzll(S.mask);
+				S.mask &= S.mask - 1;
+				a_P0 = rdlane64(m.P0, a_j);
+				a_P1 = rdlane64(m.P1, a_j);
+				const uint64_t end = (a_P1 + 15) & ~uint64_t(15);
+				a_nblk = (end - (a_P0 & ~uint64_t(15)) + 4095) >> 12;
+				a_vbase = end - 4096 * a_nblk;
+				a_blk = 0;
+				act = true;
+			}
+			const uint64_t bb = a_vbase + 4096 * a_blk;
+			d.bb = bb;
+			d.slot = a_slot;
+			d.j = a_j;
+			d.flags = 1u | (a_blk == 0 ? 2u : 0u) | (a_blk + 1 == a_nblk ? 4u : 0u) |
+			          ((a_blk <= 1 || a_blk + 1 == a_nblk) ? 8u : 0u);
+			if (a_slot) s1.pending += 1; else s0.pending += 1;
+			if (++a_blk == a_nblk) act = false;
+			if (bb >= a_P0 && bb + 4096 <= a_P1) {
 				load_block(b, reinterpret_cast<const uint8_t*>(bb), c.ld_off);
 			} else {
+				Piece p;
+				p.P0 = a_P0;
+				p.P1 = a_P1;
 #pragma unroll
 				for (int k = 0; k < 4; ++k) b.r[k] = load_chunk_if(bb + koff[k] + c.ld_off, p);
 			}
 		};
-		uint64_t blk = 0, cur_nblk = nblk_of(cur);
-		Edges e = make_edges(cur);
-		Block b, nb;
-		load_blk(b, cur, 0);
-		uint32_t acc = 0;
-		for (;;) {
-			bool more;
-			uint64_t nblk_idx = 0;
-			if (blk + 1 < cur_nblk) {
-				nxt = cur;
-				nblk_idx = blk + 1;
-				more = true;
-			} else {
-				more = gen_next(g, nxt, false);
-			}
-			if (more) load_blk(nb, nxt, nblk_idx);
-			__builtin_amdgcn_sched_barrier(0);
-			const uint64_t bb = vbase_of(cur) + 4096 * blk;
-			// edges live in the first block, the last block, and (seed bytes
-			// spilling over a chunk boundary) possibly the second: fix_edges'
-			// uniform per-window test decides
+		// edge fix-ups: the lead chunk is in block 0, its seed spill in block 0
+		// or 1, the tail chunk in the last block
+		auto edges = [&](Block& b, const Blk& d) {
+			if (!(d.flags & 8u)) return;
+			const Edges e = make_edges(piece_at(d.slot, d.j));
 #pragma unroll
-			for (int k = 0; k < 4; ++k) fix_edges(b.r[k], bb + koff[k], bb + koff[k] + c.ld_off, e);
-			unswizzle(b);
-			const uint32_t v = wave_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
-			acc = blk ? umul(T->block, acc) ^ v : v;
-			if (blk + 1 == cur_nblk) store(cur, umul(T->corr[3][(uint32_t)(-cur.P1 & 15)], acc));
+			for (int k = 0; k < 4; ++k) fix_edges(b.r[k], d.bb + koff[k], d.bb + koff[k] + c.ld_off, e);
+		};
+		uint32_t acc = 0;
+		auto fold = [&](const Blk& d, uint32_t v) {
+			if (!(d.flags & 1u)) return;
+			acc = (d.flags & 2u) ? v : umul(T->block, acc) ^ v;
+			if (d.flags & 4u) deposit(d.slot, d.j, acc, 3u);
+			if (d.slot) s1.pending -= 1; else s0.pending -= 1;
+		};
+		reset(kLargeC);
+		Blk cur[2], nxt[2];
+		cur[0].flags = cur[1].flags = 0;
+		Block b[2], nb[2];
+		for (;;) {
+			take(nxt[0], nb[0]);
+			take(nxt[1], nb[1]);
 			__builtin_amdgcn_sched_barrier(0);
-			if (!more) break;
-			if (nblk_idx == 0) {
-				cur_nblk = nblk_of(nxt);
-				e = make_edges(nxt);
+			if (cur[0].flags) {
+				edges(b[0], cur[0]);
+				edges(b[1], cur[1]);
+				unswizzle(b[0]);
+				unswizzle(b[1]);
+				uint32_t y0 = 0u, y1 = 0u;
+#pragma unroll
+				for (int r = 0; r < 4; ++r) {
+					y0 = feed16_b(lds, y0, b[0].r[r], c4);
+					y1 = feed16_b(lds, y1, b[1].r[r], c4);
+				}
+				const uint32_t v0 = wave_xor(mul_nibbles(lds, y0, c_lane));
+				const uint32_t v1 = wave_xor(mul_nibbles(lds, y1, c_lane));
+				fold(cur[0], v0);
+				fold(cur[1], v1);
 			}
-			cur = nxt;
-			blk = nblk_idx;
-			b = nb;
+			__builtin_amdgcn_sched_barrier(0);
+			retire(kLargeC, act ? a_slot : -1);
+			if (!nxt[0].flags && !cur[0].flags && !s0.valid && !s1.valid) break;
+			cur[0] = nxt[0];
+			cur[1] = nxt[1];
+			b[0] = nb[0];
+			b[1] = nb[1];
 		}
 	}
 }

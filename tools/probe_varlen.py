@@ -12,7 +12,12 @@ buf = torch.empty(1 << 31, dtype=torch.uint8, device=dev)
 F.fill_splitmix64(buf, 0x5EED)
 
 
+ONLY = sys.argv[1:]
+
+
 def run(name, lengths, align=256, reps=10):
+    if ONLY and not any(o in name for o in ONLY):
+        return
     lengths = np.asarray(lengths, dtype=np.int64)
     padded = (lengths + align - 1) // align * align
     offs = np.concatenate([[0], np.cumsum(padded)[:-1]])
