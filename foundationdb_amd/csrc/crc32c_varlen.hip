@@ -288,7 +288,8 @@ struct Meta {
 	uint64_t after;    // bytes of the buffer after P1
 	uint32_t s0;       // register value entering at P0: ~seed for a buffer's first piece, else 0
 	uint32_t info;
-	uint32_t geo;      // small pieces: k0 = P0%16 | k1 = (P1-1)%16+1 << 8 | lead chunk offset in the 1 KiB window << 16
+	uint32_t geo;      // k0 = P0%16 | k1 = (P1-1)%16+1 << 8 | lead chunk offset << 16, inside the
+	                   // piece's first 1 KiB window (small) or 4 KiB block (large)
 };
 // Uniform state of one ring slot (a built batch).
 struct Slot {
@@ -394,14 +395,11 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 		m.P1 = q + b;
 		m.after = in ? len - b : 0;
 		m.s0 = a == 0 ? ~sd : 0u;
-		const uint64_t wend = (m.P1 + 15) & ~uint64_t(15);
-		m.geo = (uint32_t)(m.P0 & 15) | (((uint32_t)((m.P1 - 1) & 15) + 1) << 8) |
-		        ((uint32_t)((m.P0 & ~uint64_t(15)) - (wend - 1024)) << 16);
 		uint32_t cls = kNone;
-		if (in) {
-			const uint64_t span = ((m.P1 + 15) & ~uint64_t(15)) - (m.P0 & ~uint64_t(15));
-			cls = b - a < 16 ? kDirect : (span <= kSmall ? kSmallC : kLargeC);
-		}
+		const uint64_t span = ((m.P1 + 15) & ~uint64_t(15)) - (m.P0 & ~uint64_t(15));
+		if (in) cls = b - a < 16 ? kDirect : (span <= kSmall ? kSmallC : kLargeC);
+		m.geo = (uint32_t)(m.P0 & 15) | (((uint32_t)((m.P1 - 1) & 15) + 1) << 8) |
+		        (((uint32_t)(-span) & (cls == kSmallC ? 1023u : 4095u)) << 16);
 		m.info = cls | (a == 0 ? kFirst : 0u) | ((a != 0 || b != len) ? kSplit : 0u);
 		s.bi0 = bi0;
 		s.mask = __ballot(cls == want);
@@ -591,12 +589,14 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 		struct Blk {
 			uint64_t bb;       // block address (aligned to the piece's aligned end)
 			int slot, j;
-			uint32_t flags;    // bit0 valid, bit1 first block, bit2 last block, bit3 may hold an edge
+			uint32_t flags;    // bit0 valid, bit1 first block, bit2 last block, bit3 holds an edge,
+			                   // bit4 block 1 holding the seed spill
 		};
 		// active piece (uniform)
 		bool act = false;
 		int a_slot = 0, a_j = 0;
 		uint64_t a_blk = 0, a_nblk = 0, a_vbase = 0, a_P0 = 0, a_P1 = 0;
+		uint32_t a_geo = 0;
 		const uint32_t koff[4] = {0, 2048, 1024, 3072};
 		// take the next block of the stream and issue its loads
 		auto take = [&](Blk& d, Block& b) {
@@ -615,6 +615,7 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 				S.mask &= S.mask - 1;
 				a_P0 = rdlane64(m.P0, a_j);
 				a_P1 = rdlane64(m.P1, a_j);
+				a_geo = rdlane(m.geo, a_j);
 				const uint64_t end = (a_P1 + 15) & ~uint64_t(15);
 				a_nblk = (end - (a_P0 & ~uint64_t(15)) + 4095) >> 12;
 				a_vbase = end - 4096 * a_nblk;
@@ -625,8 +626,13 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 			d.bb = bb;
 			d.slot = a_slot;
 			d.j = a_j;
+			// edges: lead chunk (+ seed) in block 0, seed spill in block 0 or 1
+			// when k0 > 12, tail chunk (k1 < 16) at offset 4080 of the last block
+			const uint32_t k0 = a_geo & 15u, k1 = (a_geo >> 8) & 31u, o = a_geo >> 16;
+			const bool spill1 = k0 > 12 && o == 4080;
 			d.flags = 1u | (a_blk == 0 ? 2u : 0u) | (a_blk + 1 == a_nblk ? 4u : 0u) |
-			          ((a_blk <= 1 || a_blk + 1 == a_nblk) ? 8u : 0u);
+			          ((a_blk == 0 || (a_blk == 1 && spill1) || (a_blk + 1 == a_nblk && k1 != 16)) ? 8u : 0u) |
+			          (a_blk == 1 && spill1 ? 16u : 0u);
 			if (a_slot) s1.pending += 1; else s0.pending += 1;
 			if (++a_blk == a_nblk) act = false;
 			if (bb >= a_P0 && bb + 4096 <= a_P1) {
@@ -643,9 +649,29 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 		// or 1, the tail chunk in the last block
 		auto edges = [&](Block& b, const Blk& d) {
 			if (!(d.flags & 8u)) return;
-			const Edges e = make_edges(piece_at(d.slot, d.j));
+			const Meta& m = d.slot ? m1 : m0;
+			const uint32_t geo = rdlane(m.geo, d.j);
+			const uint32_t k0 = geo & 15u, k1 = (geo >> 8) & 31u, o = geo >> 16;
+			const Masks mk = edge_masks(k0, k1, rdlane(m.s0, d.j));
+			const bool first = d.flags & 2u, last = d.flags & 4u;
+			// block offsets of the edge chunks (0xFFFF: none in this block)
+			const uint32_t ol = first ? o : 0xFFFFu;
+			const uint32_t os = (d.flags & 16u) ? 0u : ((first && k0 > 12 && o + 16 < 4096) ? o + 16 : 0xFFFFu);
+			const uint32_t ot = (last && k1 != 16) ? 4080u : 0xFFFFu;
 #pragma unroll
-			for (int k = 0; k < 4; ++k) fix_edges(b.r[k], d.bb + koff[k], d.bb + koff[k] + c.ld_off, e);
+			for (int k = 0; k < 4; ++k) {
+				const uint32_t w = koff[k];
+				const bool any = (ol - w < 1024u) || (os - w < 1024u) || (ot - w < 1024u);
+				if (!any) continue;
+				const uint32_t off = w + c.ld_off;
+				const bool il = off == ol, is = off == os, it = off == ot;
+#pragma unroll
+				for (int dd = 0; dd < 4; ++dd) {
+					const uint32_t mm = (il ? mk.lm[dd] : ~0u) & (it ? mk.tm[dd] : ~0u);
+					const uint32_t x = il ? mk.inj[dd] : ((dd == 0 && is) ? mk.spill : 0u);
+					b.r[k][dd] = (b.r[k][dd] & mm) ^ x;
+				}
+			}
 		};
 		uint32_t acc = 0;
 		auto fold = [&](const Blk& d, uint32_t v) {
