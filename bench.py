@@ -68,7 +68,7 @@ def cpu_baseline(wl, seconds):
     """Reference crc32c_append (oracle/_ref), 1 thread pinned to one core."""
     from oracle import oracle as O
     sample = wl.cpu_sample()
-    kind = "reference" if O.reference_available() else "port"
+    kind = "reference" if sample.available(O) else "port"
     old = os.sched_getaffinity(0)
     core = min(old)
     os.sched_setaffinity(0, {core})
@@ -167,7 +167,7 @@ def main():
         achieved = wl.algorithmic_bytes_per_step / (kernel_ms * 1e-3) / 1e9
         peak = wl.pcie_peak_gbs if host_timed else HBM_PEAK_GBS
         rec = {
-            "metric": METRIC,
+            "metric": getattr(wl, "metric", METRIC),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,

@@ -38,12 +38,19 @@ def pmc_traffic(workload):
 
 
 class CpuSample:
-    def __init__(self, desc, nbytes, buf, stride=None, length=None, count=None, offsets=None, lengths=None, seed=0):
+    def __init__(self, desc, nbytes, buf, stride=None, length=None, count=None, offsets=None, lengths=None, seed=0,
+                 ref=None, port=None):
         self.desc, self.nbytes, self.buf = desc, nbytes, buf
         self.stride, self.length, self.count = stride, length, count
         self.offsets, self.lengths, self.seed = offsets, lengths, seed
+        self.ref, self.port = ref, port  # optional callables(O) for non-CRC workloads
+
+    def available(self, O):
+        return O.xxh3_reference_available() if self.ref else O.reference_available()
 
     def run_reference(self, O):
+        if self.ref:
+            return self.ref(O)
         if self.offsets is None:
             return O.reference_batch_fixed(self.buf, self.stride, self.length, self.count, seed=self.seed)
         L = O.reference().lib
@@ -57,6 +64,8 @@ class CpuSample:
         return out
 
     def run_port(self, O):
+        if self.port:
+            return self.port(O)
         if self.offsets is None:
             return O.batch_fixed(self.buf, self.stride, self.length, self.count, seed=self.seed, threads=1)
         return O.batch_varlen(self.buf, self.offsets, self.lengths, seed=self.seed, threads=1)
@@ -255,6 +264,45 @@ class DryCpuPages:
         return int(self.out[0]) == F.crc32c_append(0, self.buf[:4096].tobytes())
 
 
+class Xxh3Pages:
+    """Batched XXH3-64 over 4 KiB pages in the SQLite page-checksum layout:
+    XXH3_64bits(page, 4088) per page (fdbserver/kvstore/KeyValueStoreSQLite.cpp:112),
+    1 Mi pages resident in HBM."""
+    metric = "device-resident XXH3-64 GiB/s on 4 KiB page batches (4088 B hashed per page); % of HBM-read peak"
+    kernel_name = "fdbxxh::k_xxh3<true>"
+
+    def __init__(self, dev, rank, count=1 << 20, length=4088, seed=0):
+        import foundationdb_amd.xxh3 as X
+        self.X, self.dev, self.count, self.length, self.seed = X, dev, count, length, seed
+        self.buf = torch.empty(count * 4096, dtype=torch.uint8, device=dev)
+        F.fill_splitmix64(self.buf, STATE)
+        self.out = torch.empty(count, dtype=torch.uint64, device=dev)
+        self.bytes_per_step = count * length
+        self.algorithmic_bytes_per_step = count * (length + 8)
+        self.data_desc = (f"synthetic: splitmix64 stream (state 0x{STATE:X}) generated in HBM, {count} pages x "
+                          f"4096 B, XXH3-64 of the first {length} B of each (seed {seed})")
+        self.config = {"workload": f"{count} x 4096 B pages, XXH3-64 over {length} B each, device-resident",
+                       "pages": count, "page_bytes": 4096, "hashed_bytes": length, "seed": seed}
+
+    def step(self, stream):
+        self.X.batch_fixed(self.buf, 4096, self.length, self.count, seed=self.seed, out=self.out, stream=stream)
+
+    def verify(self):
+        with open(os.path.join(ROOT, "tests", "golden", "xxh3_golden.json")) as fh:
+            g = json.load(fh)["pages_full"]
+        a = self.out.cpu().numpy().view(np.uint64)
+        return ("%016x" % int(np.bitwise_xor.reduce(a)) == g["xor"] and
+                "%016x" % int(a.sum(dtype=np.uint64)) == g["sum"])
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        n = 65536
+        buf = O.splitmix64(n * 4096 // 8, STATE).view(np.uint8)
+        return CpuSample(f"{n} x 4096 B pages, XXH3_64bits over {self.length} B each (reference flow/xxhash.c)",
+                         n * self.length, buf, ref=lambda O: O.ref_xxh3_batch_fixed(buf, 4096, self.length, n),
+                         port=lambda O: O.xxh3_batch_fixed(buf, 4096, self.length, n, threads=1))
+
+
 WORKLOADS = {
     "pages4k": lambda dev, rank: Pages(dev, rank, 4096, 1 << 20, 0),
     "pages8k": lambda dev, rank: Pages(dev, rank, 8192, 1 << 19, 0xFDBEEFDB),
@@ -263,4 +311,5 @@ WORKLOADS = {
     "chunks": lambda dev, rank: VarLen(dev, rank, chunk_lengths(), 4096,
                                        "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch"),
     "chunks-host": lambda dev, rank: HostChunks(dev, rank),
+    "xxh3-pages4k": lambda dev, rank: Xxh3Pages(dev, rank),
 }

@@ -8,7 +8,9 @@
 #include <string>
 
 #include "../../include/fdb_crc32c.h"
+#include "../../include/fdb_xxh3.h"
 #include "crc32c_device.h"
+#include "xxh3_device.h"
 
 namespace fdbcrc {
 namespace {
@@ -170,11 +172,18 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
 	const uint64_t blocks = length / 4096;
 	const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && (stride % 16 == 0) && length % 4096 == 0 &&
 	                     (blocks == 1 || blocks == 2);
+	// a window [h, 4096 - t) of 16-byte aligned 4 KiB pages (h, t < 16): the
+	// SQLite (4088 B at +0) and DiskQueue (4092 B at +4) checksum layouts
+	const uint64_t h = reinterpret_cast<uintptr_t>(base) % 16;
+	const bool window = !aligned && length > 0 && stride % 16 == 0 && h + length <= 4096 && h + length + 16 > 4096;
 	int rc;
 	if (length == 0)
 		rc = launch_fill_seeds(count, seed, d_seeds, d_out, s);
 	else if (aligned)
 		rc = launch_pages((int)blocks, base, stride, count, seed, d_seeds, d_out, st->tables, st->num_cus, s);
+	else if (window)
+		rc = launch_pages_window(base - h, stride, count, (uint32_t)h, (uint32_t)(4096 - h - length), seed, d_seeds,
+		                         d_out, st->tables, st->num_cus, s);
 	else {
 #ifdef FDBCRC_DEBUG
 		crc32c_debug_bounds((uint64_t)base, (uint64_t)base + (count - 1) * stride + length);
@@ -231,6 +240,72 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 	                              varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have))
 		return rc;
 	return crc32c_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
+}
+
+// ---- XXH3-64 (include/fdb_xxh3.h) -------------------------------------------
+
+int xxh3_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length, uint64_t count, uint64_t seed,
+                         const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
+	if (count == 0) return 0;
+	if (!d_out || (!d_base && length)) return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_fixed: null pointer");
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	fdbxxh::XxhParams P{};
+	P.base = static_cast<const uint8_t*>(d_base);
+	P.stride = stride;
+	P.length = length;
+	P.count = count;
+	P.seed = seed;
+	P.seeds = d_seeds;
+	P.out = d_out;
+	if (fdbxxh::launch_xxh3(P, st->num_cus, nullptr, reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "xxh3_gpu_batch_fixed: launch setup failed");
+	return check_launch("xxh3_gpu_batch_fixed launch");
+}
+
+uint64_t xxh3_gpu_varlen_workspace_bytes(uint64_t count) {
+	DeviceState* st;
+	if (device_state(&st)) return 0;
+	return fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus));
+}
+
+int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                             uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
+                             uint64_t workspace_bytes, void* stream) {
+	if (count == 0) return 0;
+	if (!d_out || !d_offsets || !d_lengths || !d_base)
+		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: null pointer");
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	const uint64_t need = fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus));
+	if (!d_workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: workspace too small or misaligned");
+	fdbxxh::XxhParams P{};
+	P.base = static_cast<const uint8_t*>(d_base);
+	P.offsets = d_offsets;
+	P.lengths = d_lengths;
+	P.count = count;
+	P.seed = seed;
+	P.seeds = d_seeds;
+	P.out = d_out;
+	if (fdbxxh::launch_xxh3(P, st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "xxh3_gpu_batch_varlen: launch setup failed");
+	return check_launch("xxh3_gpu_batch_varlen launch");
+}
+
+int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                          uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
+	if (count == 0) return 0;
+	if (!d_out || !d_offsets || !d_lengths || !d_base)
+		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: null pointer");
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
+	                              fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus)), &ws, &have))
+		return rc;
+	return xxh3_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
 }
 
 const char* crc32c_gpu_last_error(void) { return t_err.c_str(); }

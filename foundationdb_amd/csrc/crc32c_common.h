@@ -173,6 +173,28 @@ __device__ __forceinline__ uint32_t mul_nibbles(const uint32_t* lds, uint32_t s,
 	return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 
+// Byte masks of a 16-byte chunk from 64-bit shifts: keep bytes >= k0 (lead),
+// keep bytes < k1 (tail), and the register value s0 placed at byte k0
+// (its bytes past the chunk end spill into the next chunk).
+struct Masks {
+	uint32_t lm[4], tm[4], inj[4], spill;
+};
+__device__ __forceinline__ Masks edge_masks(uint32_t k0, uint32_t k1, uint32_t s0) {
+	const uint64_t ones = ~uint64_t(0), s = s0;
+	const uint64_t lmLo = k0 >= 8 ? 0 : ones << (8 * k0);
+	const uint64_t lmHi = k0 <= 8 ? ones : ones << (8 * (k0 - 8));
+	const uint64_t tmLo = k1 >= 8 ? ones : ones >> (64 - 8 * k1);
+	const uint64_t tmHi = k1 <= 8 ? 0 : ones >> (128 - 8 * k1);
+	const uint64_t injLo = k0 >= 8 ? 0 : s << (8 * k0);
+	const uint64_t injHi = k0 >= 8 ? s << (8 * (k0 - 8)) : (k0 > 4 ? s >> (8 * (8 - k0)) : 0);
+	Masks m;
+	m.lm[0] = (uint32_t)lmLo; m.lm[1] = (uint32_t)(lmLo >> 32); m.lm[2] = (uint32_t)lmHi; m.lm[3] = (uint32_t)(lmHi >> 32);
+	m.tm[0] = (uint32_t)tmLo; m.tm[1] = (uint32_t)(tmLo >> 32); m.tm[2] = (uint32_t)tmHi; m.tm[3] = (uint32_t)(tmHi >> 32);
+	m.inj[0] = (uint32_t)injLo; m.inj[1] = (uint32_t)(injLo >> 32); m.inj[2] = (uint32_t)injHi; m.inj[3] = (uint32_t)(injHi >> 32);
+	m.spill = k0 > 12 ? s0 >> (8 * (16 - k0)) : 0u;
+	return m;
+}
+
 // Cross-lane reads with unsigned results.  The builtins return `int`: widening
 // that to 64 bits sign-extends, so every 64-bit value is rebuilt from
 // explicitly unsigned halves.

@@ -27,8 +27,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <stdlib.h>
-
 #include "crc32c_common.h"
 
 namespace fdbcrc {
@@ -123,26 +121,60 @@ __global__ __launch_bounds__(1024) void k_pages(const uint8_t* __restrict__ base
 // U pages per unit: U independent register chains interleave (ILP U) while
 // the next unit's U pages are in flight.  Groups of G = 2U*floor(64/2U) pages
 // share one seed vector load and one coalesced checksum store.
-template <int U>
+// WINDOW: checksum bytes [h, 4096 - t) of every page (h, t < 16): before the
+// unswizzle, lane 0's first chunk (page bytes 0..15) is masked below h and
+// gets the seed register at byte h (lane 32's chunk 16..31 takes the bytes
+// spilling past 16), lane 63's last chunk (4080..4095) is masked from 16 - t;
+// the t zero bytes are removed from the raw register when the group is stored.
+template <int U, bool WINDOW>
 __device__ __forceinline__ void unit_crc_b(const uint32_t* lds, int lane, uint32_t c4, uint32_t c_lane,
-                                           Block (&u)[U], const uint32_t (&s)[U], uint32_t (&crc)[U]) {
+                                           Block (&u)[U], const uint32_t (&s)[U], uint32_t (&crc)[U],
+                                           uint32_t h, uint32_t t) {
+	if (WINDOW) {
+#pragma unroll
+		for (int j = 0; j < U; ++j) {
+			const Masks mk = edge_masks(h, 16 - t, ~s[j]);
+#pragma unroll
+			for (int d = 0; d < 4; ++d) {
+				const uint32_t m0 = lane == 0 ? mk.lm[d] : ~0u;
+				const uint32_t x0 = lane == 0 ? mk.inj[d] : ((d == 0 && lane == 32) ? mk.spill : 0u);
+				u[j].r[0][d] = (u[j].r[0][d] & m0) ^ x0;
+				u[j].r[3][d] &= lane == 63 ? mk.tm[d] : ~0u;
+			}
+		}
+	}
 #pragma unroll
 	for (int j = 0; j < U; ++j) unswizzle(u[j]);
 	uint32_t x[U];
 #pragma unroll
-	for (int j = 0; j < U; ++j) x[j] = lane == 0 ? ~s[j] : 0u;
+	for (int j = 0; j < U; ++j) x[j] = (!WINDOW && lane == 0) ? ~s[j] : 0u;
 #pragma unroll
 	for (int r = 0; r < 4; ++r)
 #pragma unroll
 		for (int j = 0; j < U; ++j) x[j] = feed16_b(lds, x[j], u[j].r[r], c4);
 #pragma unroll
-	for (int j = 0; j < U; ++j) crc[j] = ~wave_xor(mul_nibbles(lds, x[j], c_lane));
+	for (int j = 0; j < U; ++j) {
+		const uint32_t r = wave_xor(mul_nibbles(lds, x[j], c_lane));
+		crc[j] = WINDOW ? r : ~r;  // WINDOW: raw register, finished at the store
+	}
 }
 
-template <int U>
+// Lane-parallel multiply of a per-lane value by a constant whose nibble tables
+// live in global memory (8 gathers, L2-resident).
+__device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t v) {
+	typedef __attribute__((address_space(1))) const uint32_t g_u32;
+	uint32_t r = 0;
+#pragma unroll
+	for (int n = 0; n < 8; ++n)
+		r ^= *((g_u32*)reinterpret_cast<uintptr_t>(&tab[n][(v >> (4 * n)) & 15u]));
+	return r;
+}
+
+template <int U, bool WINDOW = false>
 __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
                                                   uint32_t seed, const uint32_t* __restrict__ seeds,
-                                                  uint32_t* __restrict__ out, const DevTables* __restrict__ tabs) {
+                                                  uint32_t* __restrict__ out, const DevTables* __restrict__ tabs,
+                                                  uint32_t h = 0, uint32_t t = 0) {
 	constexpr uint64_t G = 2 * U * (64 / (2 * U));  // a whole number of loop iterations
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const LaneCtx c = make_ctx();
@@ -178,7 +210,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 			__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + j) & 63);
-			unit_crc_b<U>(lds, c.lane, c4, c_lane, u0, sd, crc);
+			unit_crc_b<U, WINDOW>(lds, c.lane, c4, c_lane, u0, sd, crc, h, t);
 #pragma unroll
 			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + j ? crc[j] : mine;
 			__builtin_amdgcn_sched_barrier(0);
@@ -186,11 +218,12 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 			__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + U + j) & 63);
-			unit_crc_b<U>(lds, c.lane, c4, c_lane, u1, sd, crc);
+			unit_crc_b<U, WINDOW>(lds, c.lane, c4, c_lane, u1, sd, crc, h, t);
 #pragma unroll
 			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + U + j ? crc[j] : mine;
 			__builtin_amdgcn_sched_barrier(0);
 		}
+		if (WINDOW) mine = ~(t ? vmul_tab(tabs->inv_z[t], mine) : mine);
 		if ((uint64_t)c.lane < n) out[first + c.lane] = mine;
 	}
 }
@@ -206,19 +239,22 @@ int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint
 	if (grid > (uint64_t)num_cus) grid = num_cus;
 	if (grid == 0) grid = 1;
 	switch (blocks_per_page) {
-		case 1: {
-			static const int u = getenv("FDBCRC_PAGES_U") ? atoi(getenv("FDBCRC_PAGES_U")) : 2;
-			if (u == 2)
-				k_pages4k<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs);
-			else if (u == 4)
-				k_pages4k<4><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs);
-			else
-				k_pages4k<3><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs);
-			break;
-		}
+		case 1: k_pages4k<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
 		case 2: k_pages<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
 		default: return -1;
 	}
+	return 0;
+}
+
+// Bytes [h, 4096 - t) of 4 KiB pages; `pages` is 16-byte aligned (the page
+// start, h bytes before the caller's window).
+int launch_pages_window(const uint8_t* pages, uint64_t stride, uint64_t count, uint32_t h, uint32_t t, uint32_t seed,
+                        const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream) {
+	const uint64_t units = (count + 63) / 64;
+	uint64_t grid = (units + 15) / 16;
+	if (grid > (uint64_t)num_cus) grid = num_cus;
+	if (grid == 0) grid = 1;
+	k_pages4k<2, true><<<(unsigned)grid, 1024, 0, stream>>>(pages, stride, count, seed, seeds, out, tabs, h, t);
 	return 0;
 }
 

@@ -1,0 +1,25 @@
+// Device-side interface of the batched XXH3-64 kernels (xxh3_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fdbxxh {
+
+struct XxhParams {
+	const uint8_t* base;
+	const uint64_t* offsets;     // nullptr: fixed mode, buffer i at base + i*stride
+	const uint64_t* lengths;     // varlen lengths
+	uint64_t stride, length, count, seed;
+	const uint64_t* seeds;       // per-buffer seeds or nullptr
+	uint64_t* out;
+	const uint64_t* wave_first;  // varlen: first buffer of every wave [nwave + 1] (planner output)
+};
+
+constexpr unsigned kWavesPerBlock = 4;
+// Resident 256-thread blocks per CU of the main kernel (occupancy query, cached).
+int xxh3_blocks_per_cu();
+inline uint64_t xxh3_nwave(int num_cus) { return (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock; }
+uint64_t xxh3_workspace_bytes(uint64_t count, uint64_t nwave);
+int launch_xxh3(const XxhParams& P, int num_cus, void* ws, hipStream_t stream);
+
+}  // namespace fdbxxh

@@ -1,0 +1,521 @@
+// Batched XXH3-64 (xxHash v0.8.0 XXH3_64bits / XXH3_64bits_withSeed) on
+// MI355X (gfx950).  Bit-identical to flow/include/flow/xxhash.h:3800-3837 for
+// every (bytes, length, seed).  Callers: SQLite page checksums
+// (fdbserver/kvstore/KeyValueStoreSQLite.cpp:112,138), DiskQueue V2 pages
+// (fdbserver/kvstore/DiskQueue.cpp:1086-1088), Redwood page encodings
+// (fdbserver/kvstore/IPager.h:300-361), FlowTransport packets
+// (fdbrpc/FlowTransport.cpp:1346,2043).
+//
+// Long inputs (> 240 B), xxhash.h:3641-3718: one wave per buffer.  A 1 KiB
+// block is 16 stripes x 64 B; lane m loads the 16 B at 16m (one coalesced
+// 1 KiB load per block), i.e. stripe s = m/4, accumulator pair k = m%4, and
+// computes that stripe's contributions to accumulators 2k and 2k+1
+// (accumulate_512 swaps adjacent lanes, so the pair is closed).  The 16
+// lanes of a pair sum their contributions (DPP row rotates + permlane swaps),
+// lanes 0..3 then hold acc[2k], acc[2k+1] and apply the element-wise
+// scramble after every full block.  The final partial block has at most 15
+// stripes, so lanes 60..63 take the last stripe (at len-64, secret+121).
+// Short inputs (<= 240 B), xxhash.h:2734-2951: one lane per buffer.
+// No lookup tables: no LDS, occupancy bounded by VGPRs only.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xxh3_device.h"
+
+namespace fdbxxh {
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+constexpr uint64_t P32_1 = 0x9E3779B1u, P32_2 = 0x85EBCA77u, P32_3 = 0xC2B2AE3Du;
+constexpr uint64_t P64_1 = 0x9E3779B185EBCA87ull, P64_2 = 0xC2B2AE3D27D4EB4Full, P64_3 = 0x165667B19E3779F9ull;
+constexpr uint64_t P64_4 = 0x85EBCA77C2B2AE63ull, P64_5 = 0x27D4EB2F165667C5ull;
+
+// The default secret as 24 little-endian words (xxhash.h:2500-2511).
+__constant__ uint64_t kSec[24] = {
+    0xbe4ba423396cfeb8ull, 0x1cad21f72c81017cull, 0xdb979083e96dd4deull, 0x1f67b3b7a4a44072ull,
+    0x78e5c0cc4ee679cbull, 0x2172ffcc7dd05a82ull, 0x8e2443f7744608b8ull, 0x4c263a81e69035e0ull,
+    0xcb00c391bb52283cull, 0xa32e531b8b65d088ull, 0x4ef90da297486471ull, 0xd8acdea946ef1938ull,
+    0x3f349ce33f76faa8ull, 0x1d4f0bc7c7bbdcf9ull, 0x3159b4cd4be0518aull, 0x647378d9c97e9fc8ull,
+    0xc3ebd33483acc5eaull, 0xeb6313faffa081c5ull, 0x49daf0b751dd0d17ull, 0x9e68d429265516d3ull,
+    0xfca1477d58be162bull, 0xce31d07ad1b8f88full, 0x280416958f3acb45ull, 0x7e404bbbcafbd7afull,
+};
+
+// Word j of the secret for `seed` (custom secret, xxhash.h:3550-3566; the
+// seed-0 secret is the default one).
+__device__ __forceinline__ uint64_t sec_word(int j, uint64_t seed) {
+	const uint64_t w = kSec[j];
+	return (j & 1) ? w - seed : w + seed;
+}
+// Secret bytes [8j + r, 8j + r + 8), 0 < r < 8.
+__device__ __forceinline__ uint64_t sec_at(int j, int r, uint64_t seed) {
+	return (sec_word(j, seed) >> (8 * r)) | (sec_word(j + 1, seed) << (64 - 8 * r));
+}
+// Default-secret bytes at any offset (short paths never use a custom secret).
+__device__ __forceinline__ uint64_t ksec(int off) {
+	const int j = off >> 3, r = off & 7;
+	return r ? (kSec[j] >> (8 * r)) | (kSec[j + 1] << (64 - 8 * r)) : kSec[j];
+}
+__device__ __forceinline__ uint32_t ksec32(int off) { return (uint32_t)ksec(off); }
+
+__device__ __forceinline__ uint64_t mulfold(uint64_t a, uint64_t b) { return a * b ^ __umul64hi(a, b); }
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t xxh64_aval(uint64_t h) {
+	h ^= h >> 33;
+	h *= P64_2;
+	h ^= h >> 29;
+	h *= P64_3;
+	return h ^ (h >> 32);
+}
+__device__ __forceinline__ uint64_t xxh3_aval(uint64_t h) {
+	h ^= h >> 37;
+	h *= 0x165667919E3779F9ull;
+	return h ^ (h >> 32);
+}
+__device__ __forceinline__ uint64_t rrmxmx(uint64_t h, uint64_t len) {
+	h ^= rotl64(h, 49) ^ rotl64(h, 24);
+	h *= 0x9FB21C651E98DF25ull;
+	h ^= (h >> 35) + len;
+	h *= 0x9FB21C651E98DF25ull;
+	return h ^ (h >> 28);
+}
+
+typedef __attribute__((address_space(1))) const uint64_t g_u64;
+typedef __attribute__((address_space(1))) const u64x2 g_u64x2;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+
+// Little-endian 8-byte read at any address: aligned 8-byte words only (a word
+// holding a wanted byte never crosses a page, so nothing past the buffer's
+// last 8-byte word is touched).
+__device__ __forceinline__ uint64_t ldu64(uint64_t p) {
+	const uint64_t a = p & ~uint64_t(7);
+	const int sh = (int)(p & 7);
+	const uint64_t lo = *((g_u64*)a);
+	if (!sh) return lo;
+	const uint64_t hi = *((g_u64*)(a + 8));
+	return (lo >> (8 * sh)) | (hi << (64 - 8 * sh));
+}
+__device__ __forceinline__ uint32_t ldu32(uint64_t p) {
+	// bytes p..p+3 lie in at most two aligned words; read only what is needed
+	const uint64_t a = p & ~uint64_t(3);
+	const int sh = (int)(p & 3);
+	typedef __attribute__((address_space(1))) const uint32_t g_u32;
+	const uint32_t lo = *((g_u32*)a);
+	if (!sh) return lo;
+	const uint32_t hi = *((g_u32*)(a + 4));
+	return (lo >> (8 * sh)) | (hi << (32 - 8 * sh));
+}
+__device__ __forceinline__ uint32_t ldu8(uint64_t p) { return *((g_u8*)p); }
+
+// ---------------------------------------------------------------------------
+// Short inputs, one lane per buffer (xxhash.h:2734-2951, default secret).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix16(uint64_t p, int soff, uint64_t seed) {
+	return mulfold(ldu64(p) ^ (ksec(soff) + seed), ldu64(p + 8) ^ (ksec(soff + 8) - seed));
+}
+
+__device__ uint64_t xxh3_short(uint64_t p, uint64_t len, uint64_t seed) {
+	if (len <= 16) {
+		if (len > 8) {
+			const uint64_t f1 = (ksec(24) ^ ksec(32)) + seed, f2 = (ksec(40) ^ ksec(48)) - seed;
+			const uint64_t lo = ldu64(p) ^ f1, hi = ldu64(p + len - 8) ^ f2;
+			return xxh3_aval(len + __builtin_bswap64(lo) + hi + mulfold(lo, hi));
+		}
+		if (len >= 4) {
+			const uint64_t s2 = seed ^ ((uint64_t)__builtin_bswap32((uint32_t)seed) << 32);
+			const uint32_t i1 = ldu32(p), i2 = ldu32(p + len - 4);
+			const uint64_t flip = (ksec(8) ^ ksec(16)) - s2;
+			return rrmxmx(((uint64_t)i2 + ((uint64_t)i1 << 32)) ^ flip, len);
+		}
+		if (len) {
+			const uint32_t c1 = ldu8(p), c2 = ldu8(p + (len >> 1)), c3 = ldu8(p + len - 1);
+			const uint32_t comb = (c1 << 16) | (c2 << 24) | c3 | ((uint32_t)len << 8);
+			return xxh64_aval((uint64_t)comb ^ ((uint64_t)(ksec32(0) ^ ksec32(4)) + seed));
+		}
+		return xxh64_aval(seed ^ (ksec(56) ^ ksec(64)));
+	}
+	uint64_t acc = len * P64_1;
+	if (len <= 128) {
+		const int pairs = (int)((len - 1) >> 5);  // 0..3 extra pairs beyond the first
+		for (int i = pairs; i >= 1; --i) {
+			acc += mix16(p + 16 * i, 32 * i, seed);
+			acc += mix16(p + len - 16 * (i + 1), 32 * i + 16, seed);
+		}
+		acc += mix16(p, 0, seed);
+		acc += mix16(p + len - 16, 16, seed);
+		return xxh3_aval(acc);
+	}
+	const int rounds = (int)len / 16;
+	for (int i = 0; i < 8; ++i) acc += mix16(p + 16 * i, 16 * i, seed);
+	acc = xxh3_aval(acc);
+	for (int i = 8; i < rounds; ++i) acc += mix16(p + 16 * i, 16 * (i - 8) + 3, seed);
+	acc += mix16(p + len - 16, 136 - 17, seed);
+	return xxh3_aval(acc);
+}
+
+// ---------------------------------------------------------------------------
+// Long inputs, one wave per buffer.
+// ---------------------------------------------------------------------------
+// Sum over the 16 lanes m' == m (mod 4) (the stripes of one pair): DPP row
+// rotates by 4 and 8, then the permlane16/32 swaps add the four rows.
+template <int CTRL>
+__device__ __forceinline__ void add_dpp(uint32_t& lo, uint32_t& hi) {
+	const uint32_t l2 = __builtin_amdgcn_update_dpp(0u, lo, CTRL, 0xF, 0xF, false);
+	const uint32_t h2 = __builtin_amdgcn_update_dpp(0u, hi, CTRL, 0xF, 0xF, false);
+	const uint64_t s = (((uint64_t)hi << 32) | lo) + (((uint64_t)h2 << 32) | l2);
+	lo = (uint32_t)s;
+	hi = (uint32_t)(s >> 32);
+}
+
+__device__ __forceinline__ uint64_t pair_sum(uint64_t v) {
+	uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+	add_dpp<0x124>(lo, hi);  // row_ror:4
+	add_dpp<0x128>(lo, hi);  // row_ror:8
+	{
+		const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+		const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+		const uint64_t s = (((uint64_t)b[0] << 32) | a[0]) + (((uint64_t)b[1] << 32) | a[1]);
+		lo = (uint32_t)s;
+		hi = (uint32_t)(s >> 32);
+	}
+	{
+		const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+		const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+		const uint64_t s = (((uint64_t)b[0] << 32) | a[0]) + (((uint64_t)b[1] << 32) | a[1]);
+		lo = (uint32_t)s;
+		hi = (uint32_t)(s >> 32);
+	}
+	return ((uint64_t)hi << 32) | lo;
+}
+
+// Per-lane secret words of one seed.
+struct Keys {
+	uint64_t k0, k1;   // normal stripe: secret + 8s + 16k, +8
+	uint64_t l0, l1;   // last stripe (lanes 60..63): secret + 121 + 16k, +8
+	uint64_t c0, c1;   // scramble (lanes 0..3): secret + 128 + 16k, +8
+	uint64_t g0, g1;   // merge (lanes 0..3): secret + 11 + 16k, +8
+};
+__device__ __forceinline__ Keys make_keys(int lane, uint64_t seed) {
+	const int s = lane >> 2, k = lane & 3;
+	Keys K;
+	K.k0 = sec_word(s + 2 * k, seed);
+	K.k1 = sec_word(s + 2 * k + 1, seed);
+	K.l0 = sec_at(15 + 2 * k, 1, seed);
+	K.l1 = sec_at(16 + 2 * k, 1, seed);
+	K.c0 = sec_word(16 + 2 * k, seed);
+	K.c1 = sec_word(17 + 2 * k, seed);
+	K.g0 = sec_at(1 + 2 * k, 3, seed);
+	K.g1 = sec_at(2 + 2 * k, 3, seed);
+	return K;
+}
+
+struct Acc {
+	uint64_t a0, a1;  // lanes 0..3: acc[2k], acc[2k+1]
+};
+__device__ __forceinline__ Acc acc_init(int lane) {
+	const int k = lane & 3;
+	Acc A;
+	A.a0 = k == 0 ? P32_3 : (k == 1 ? P64_2 : (k == 2 ? P64_4 : P64_5));
+	A.a1 = k == 0 ? P64_1 : (k == 1 ? P64_3 : (k == 2 ? P32_2 : P32_1));
+	return A;
+}
+
+// One block's contributions: v0/v1 = the lane's two data words, key words
+// per lane (normal or last-stripe), `on` = lane takes part.
+__device__ __forceinline__ void block_step(Acc& A, uint64_t v0, uint64_t v1, uint64_t key0, uint64_t key1, bool on) {
+	const uint64_t x0 = v0 ^ key0, x1 = v1 ^ key1;
+	uint64_t d0 = v1 + (uint64_t)(uint32_t)x0 * (x0 >> 32);
+	uint64_t d1 = v0 + (uint64_t)(uint32_t)x1 * (x1 >> 32);
+	d0 = on ? d0 : 0;
+	d1 = on ? d1 : 0;
+	A.a0 += pair_sum(d0);
+	A.a1 += pair_sum(d1);
+}
+__device__ __forceinline__ void scramble(Acc& A, const Keys& K) {
+	A.a0 = ((A.a0 ^ (A.a0 >> 47)) ^ K.c0) * P32_1;
+	A.a1 = ((A.a1 ^ (A.a1 >> 47)) ^ K.c1) * P32_1;
+}
+// mergeAccs (xxhash.h:3678-3700), result valid in every lane
+__device__ __forceinline__ uint64_t merge(const Acc& A, const Keys& K, uint64_t len, int lane) {
+	uint64_t r = (lane < 4) ? mulfold(A.a0 ^ K.g0, A.a1 ^ K.g1) : 0;
+	uint32_t lo = (uint32_t)r, hi = (uint32_t)(r >> 32);
+	add_dpp<0xB1>(lo, hi);  // quad_perm [1,0,3,2]
+	add_dpp<0x4E>(lo, hi);  // quad_perm [2,3,0,1]: lane 0 = sum of lanes 0..3
+	const uint64_t tot = ((uint64_t)__builtin_amdgcn_readlane(hi, 0) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 0);
+	return xxh3_aval(len * P64_1 + tot);
+}
+
+// A unit: up to 4 consecutive blocks of one buffer, loaded together.
+struct Unit {
+	uint64_t p, len, seed, buf;
+	uint64_t b0;   // first block index
+	int n;         // blocks in the unit (0: none)
+	bool first, fin;
+};
+struct Data {
+	uint64_t v[4][2];
+};
+
+template <bool ALIGNED>
+__device__ __forceinline__ void load_unit(Data& D, const Unit& u, int lane) {
+	const uint64_t nfull = (u.len - 1) >> 10;
+	const uint64_t ns = ((u.len - 1) - (nfull << 10)) >> 6;
+#pragma unroll
+	for (int j = 0; j < 4; ++j) {
+		D.v[j][0] = D.v[j][1] = 0;
+		if (j < u.n) {
+			const uint64_t blk = u.b0 + j;
+			const bool fin = blk == nfull;
+			uint64_t q = u.p + (blk << 10) + 16 * lane;
+			bool on = true;
+			bool aligned = ALIGNED;
+			if (fin) {
+				if (lane >= 60) {
+					q = u.p + u.len - 64 + 16 * (lane - 60);
+					aligned = false;
+				} else {
+					on = (uint64_t)lane < 4 * ns;
+				}
+			}
+			if (on) {
+				if (aligned) {
+					const u64x2 w = __builtin_nontemporal_load((g_u64x2*)q);
+					D.v[j][0] = w[0];
+					D.v[j][1] = w[1];
+				} else {
+					D.v[j][0] = ldu64(q);
+					D.v[j][1] = ldu64(q + 8);
+				}
+			}
+		}
+	}
+}
+
+__device__ __forceinline__ void compute_unit(Acc& A, const Keys& K, const Data& D, const Unit& u, int lane,
+                                             uint64_t* __restrict__ out) {
+	const uint64_t nfull = (u.len - 1) >> 10;
+	const uint64_t ns = ((u.len - 1) - (nfull << 10)) >> 6;
+	if (u.first) A = acc_init(lane);
+#pragma unroll
+	for (int j = 0; j < 4; ++j) {
+		if (j < u.n) {
+			const uint64_t blk = u.b0 + j;
+			if (blk < nfull) {
+				block_step(A, D.v[j][0], D.v[j][1], K.k0, K.k1, true);
+				scramble(A, K);
+			} else {
+				const bool last = lane >= 60;
+				block_step(A, D.v[j][0], D.v[j][1], last ? K.l0 : K.k0, last ? K.l1 : K.k1,
+				           last || (uint64_t)lane < 4 * ns);
+			}
+		}
+	}
+	if (u.fin) {
+		const uint64_t h = merge(A, K, u.len, lane);
+		if (lane == 0) out[u.buf] = h;
+	}
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_xxh3(XxhParams P) {
+	const int lane = threadIdx.x & 63;
+	const uint64_t wpb = blockDim.x >> 6;
+	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
+	const uint64_t w = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const bool fixed = P.offsets == nullptr;
+	// this wave's buffers [begin, end)
+	uint64_t begin, end;
+	if (fixed) {
+		const uint64_t per = (P.count + nwave - 1) / nwave;
+		begin = w * per;
+		end = begin + per < P.count ? begin + per : P.count;
+	} else {
+		begin = P.wave_first[w];
+		end = P.wave_first[w + 1];
+		end = end < P.count ? end : P.count;
+	}
+	if (begin >= end) return;
+	const uint64_t base = reinterpret_cast<uint64_t>(P.base);
+	auto off_of = [&](uint64_t i) -> uint64_t { return fixed ? i * P.stride : P.offsets[i]; };
+	auto len_of = [&](uint64_t i) -> uint64_t { return fixed ? P.length : P.lengths[i]; };
+	auto seed_of = [&](uint64_t i) -> uint64_t { return P.seeds ? P.seeds[i] : P.seed; };
+
+	// ---- short buffers: one lane each, 64 per pass
+	for (uint64_t b0 = begin; b0 < end; b0 += 64) {
+		const uint64_t i = b0 + lane;
+		if (i < end) {
+			const uint64_t len = len_of(i);
+			if (len <= 240) P.out[i] = xxh3_short(base + off_of(i), len, seed_of(i));
+		}
+	}
+
+	// ---- long buffers: one wave each, units of up to 4 blocks, next unit in flight
+	uint64_t gi = begin;       // next buffer to start
+	uint64_t gblk = 0, gtot = 0;  // next block of the current buffer, its block count
+	Unit g{};                  // current buffer (uniform)
+	auto next_unit = [&](Unit& u) {
+		u.n = 0;
+		if (gblk == gtot) {  // find the next long buffer
+			for (;;) {
+				if (gi >= end) return;
+				if (len_of(gi) > 240) break;
+				++gi;
+			}
+			g.len = len_of(gi);
+			g.p = base + off_of(gi);
+			g.seed = seed_of(gi);
+			g.buf = gi;
+			++gi;
+			gblk = 0;
+			gtot = ((g.len - 1) >> 10) + 1;
+		}
+		u = g;
+		u.b0 = gblk;
+		u.n = gtot - gblk < 4 ? (int)(gtot - gblk) : 4;
+		u.first = gblk == 0;
+		gblk += u.n;
+		u.fin = gblk == gtot;
+	};
+	Unit cur, nxt;
+	Data dc, dn;
+	Acc A{0, 0};
+	Keys K{};
+	uint64_t kseed = ~uint64_t(0);
+	bool have_keys = false;
+	next_unit(cur);
+	if (cur.n) load_unit<ALIGNED>(dc, cur, lane);
+	while (cur.n) {
+		next_unit(nxt);
+		if (nxt.n) load_unit<ALIGNED>(dn, nxt, lane);
+		__builtin_amdgcn_sched_barrier(0);
+		if (!have_keys || cur.seed != kseed) {
+			K = make_keys(lane, cur.seed);
+			kseed = cur.seed;
+			have_keys = true;
+		}
+		compute_unit(A, K, dc, cur, lane, P.out);
+		__builtin_amdgcn_sched_barrier(0);
+		cur = nxt;
+		dc = dn;
+	}
+}
+
+// ---------------------------------------------------------------------------
+// Varlen planning: whole buffers per wave, balanced by bytes.  Wave w takes
+// the buffers whose start lies in [w*Q, (w+1)*Q) of the concatenated stream.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_xplan(const uint64_t* __restrict__ lengths, uint64_t count,
+                                               uint64_t* __restrict__ tile_sum) {
+	__shared__ uint64_t part[4];
+	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	uint64_t v = i < count ? lengths[i] + 64 : 0;  // +64: per-buffer cost floor
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+	__syncthreads();
+	if (threadIdx.x == 0) tile_sum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// Single workgroup: in-place exclusive scan of the tile sums; tiles[ntile] =
+// total cost, tiles[ntile + 1] = quantum Q = ceil(total / nwave).
+__global__ __launch_bounds__(1024) void k_xscan(uint64_t* __restrict__ tiles, uint64_t ntile, uint64_t nwave) {
+	__shared__ uint64_t wsum[16];
+	__shared__ uint64_t carry_s;
+	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+	if (t == 0) carry_s = 0;
+	__syncthreads();
+	for (uint64_t c0 = 0; c0 < ntile; c0 += 1024) {
+		const uint64_t k = c0 + t;
+		const uint64_t x = k < ntile ? tiles[k] : 0;
+		uint64_t inc = x;
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint64_t y = __shfl_up(inc, o);
+			if ((int)lane >= o) inc += y;
+		}
+		if (lane == 63) wsum[wv] = inc;
+		__syncthreads();
+		uint64_t wb = 0;
+		for (uint32_t q = 0; q < wv; ++q) wb += wsum[q];
+		const uint64_t carry = carry_s;
+		if (k < ntile) tiles[k] = carry + wb + inc - x;
+		__syncthreads();
+		if (t == 1023) carry_s = carry + wb + inc;
+		__syncthreads();
+	}
+	if (t == 0) {
+		const uint64_t total = carry_s;
+		tiles[ntile] = total;
+		tiles[ntile + 1] = (total + nwave - 1) / nwave;
+	}
+}
+
+// One workgroup per tile of 256 buffers: buffer i (cost c_i, start s_i) is
+// the first buffer of every wave w with s_{i-1} < w*Q <= s_i; waves past
+// the last buffer get `count`.
+__global__ __launch_bounds__(256) void k_xassign(const uint64_t* __restrict__ lengths, uint64_t count,
+                                                 const uint64_t* __restrict__ tiles, uint64_t ntile,
+                                                 uint64_t* __restrict__ wave_first, uint64_t nwave) {
+	__shared__ uint64_t wsum[4];
+	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+	const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+	const uint64_t cost = i < count ? lengths[i] + 64 : 0;
+	uint64_t inc = cost;
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint64_t y = __shfl_up(inc, o);
+		if ((int)lane >= o) inc += y;
+	}
+	if (lane == 63) wsum[wv] = inc;
+	__syncthreads();
+	uint64_t wb = 0;
+	for (uint32_t q = 0; q < wv; ++q) wb += wsum[q];
+	const uint64_t q = tiles[ntile + 1];
+	const uint64_t start = tiles[blockIdx.x] + wb + inc - cost;
+	if (i < count) {
+		// waves w with s_{i-1} < w*q <= s_i, i.e. [floor(s_{i-1}/q) + 1, floor(s_i/q)];
+		// buffer 0 takes w = 0
+		const uint64_t prev = i == 0 ? 0 : start - (lengths[i - 1] + 64);
+		const uint64_t w_lo = i == 0 ? 0 : prev / q + 1;
+		const uint64_t w_hi = start / q;
+		for (uint64_t w = w_lo; w <= w_hi && w < nwave; ++w) wave_first[w] = i;
+		if (i + 1 == count)  // waves whose first byte lies past the last buffer's start: none
+			for (uint64_t w = start / q + 1; w <= nwave; ++w) wave_first[w] = count;
+	}
+}
+
+uint64_t xxh3_workspace_bytes(uint64_t count, uint64_t nwave) {
+	const uint64_t ntile = (count + 255) / 256;
+	return 8 * (ntile + 2) + 8 * (nwave + 1) + 64;
+}
+
+int xxh3_blocks_per_cu() {
+	static const int n = [] {
+		int a = 0, b = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xxh3<true>, 256, 0) != hipSuccess) a = 4;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_xxh3<false>, 256, 0) != hipSuccess) b = 4;
+		const int m = a < b ? a : b;
+		return m < 1 ? 1 : m;
+	}();
+	return n;
+}
+
+int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) {
+	XxhParams P = P0;
+	const unsigned wpb = kWavesPerBlock;
+	const uint64_t grid = (uint64_t)num_cus * xxh3_blocks_per_cu();
+	const uint64_t nwave = grid * wpb;
+	const bool aligned = ((reinterpret_cast<uint64_t>(P.base) | (P.offsets ? 1 : P.stride)) & 15) == 0;
+	if (P.offsets) {
+		const uint64_t ntile = (P.count + 255) / 256;
+		uint64_t* tiles = static_cast<uint64_t*>(ws);
+		uint64_t* wave_first = tiles + ntile + 2;
+		k_xplan<<<(unsigned)ntile, 256, 0, stream>>>(P.lengths, P.count, tiles);
+		k_xscan<<<1, 1024, 0, stream>>>(tiles, ntile, nwave);
+		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(P.lengths, P.count, tiles, ntile, wave_first, nwave);
+		P.wave_first = wave_first;
+	}
+	if (aligned)
+		k_xxh3<true><<<(unsigned)grid, 256, 0, stream>>>(P);
+	else
+		k_xxh3<false><<<(unsigned)grid, 256, 0, stream>>>(P);
+	return 0;
+}
+
+}  // namespace fdbxxh

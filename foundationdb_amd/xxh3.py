@@ -1,0 +1,82 @@
+"""Python host mirror of the batched XXH3-64 C ABI (include/fdb_xxh3.h).
+
+Reference interface: ``XXH3_64bits(data, len)`` and
+``XXH3_64bits_withSeed(data, len, seed)`` (flow/include/flow/xxhash.h:456,465,
+xxHash v0.8.0) -- same results for every input, length and seed.  Device
+(HBM) tensors in, uint64 digests out, asynchronous on a HIP stream; there is
+no CPU fallback: a missing library or GPU raises.
+"""
+import ctypes
+
+import torch
+
+from .crc32c import CRC32CError, _check, _require_device, _stream_handle, lib
+
+_bound = False
+
+
+def _lib():
+    global _bound
+    L = lib()
+    if not _bound:
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.xxh3_gpu_batch_fixed.restype = ctypes.c_int
+        L.xxh3_gpu_batch_fixed.argtypes = [vp, u64, u64, u64, u64, vp, vp, vp]
+        L.xxh3_gpu_batch_varlen.restype = ctypes.c_int
+        L.xxh3_gpu_batch_varlen.argtypes = [vp, vp, vp, u64, u64, vp, vp, vp]
+        L.xxh3_gpu_varlen_workspace_bytes.restype = u64
+        L.xxh3_gpu_varlen_workspace_bytes.argtypes = [u64]
+        L.xxh3_gpu_batch_varlen_ws.restype = ctypes.c_int
+        L.xxh3_gpu_batch_varlen_ws.argtypes = [vp, vp, vp, u64, u64, vp, vp, vp, u64, vp]
+        _bound = True
+    return L
+
+
+def _vp(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def batch_fixed(buf, stride, length, count, seed=0, seeds=None, out=None, stream=None, byte_offset=0):
+    """XXH3-64 of bytes [byte_offset + i*stride, +length) of device tensor `buf`, i < count."""
+    _require_device(buf, "buf")
+    count = int(count)
+    if count and byte_offset + (count - 1) * stride + length > buf.numel() * buf.element_size():
+        raise CRC32CError("xxh3 batch_fixed: buffers extend past the end of `buf`")
+    if out is None:
+        out = torch.empty(count, dtype=torch.uint64, device=buf.device)
+    _require_device(out, "out")
+    if seeds is not None:
+        _require_device(seeds, "seeds")
+    with torch.cuda.device(buf.device):
+        rc = _lib().xxh3_gpu_batch_fixed(ctypes.c_void_p(buf.data_ptr() + byte_offset), stride, length, count,
+                                         seed & 0xFFFFFFFFFFFFFFFF, _vp(seeds), _vp(out), _stream_handle(stream))
+    _check(rc, "xxh3_gpu_batch_fixed")
+    return out
+
+
+def varlen_workspace_bytes(count):
+    return int(_lib().xxh3_gpu_varlen_workspace_bytes(int(count)))
+
+
+def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=None, workspace=None):
+    """XXH3-64 of bytes [offsets[i], +lengths[i]) of device tensor `buf` (int64 device tensors)."""
+    _require_device(buf, "buf")
+    _require_device(offsets, "offsets")
+    _require_device(lengths, "lengths")
+    n = offsets.numel()
+    if lengths.numel() != n:
+        raise CRC32CError("xxh3 batch_varlen: offsets and lengths differ in size")
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint64, device=buf.device)
+    if seeds is not None:
+        _require_device(seeds, "seeds")
+    with torch.cuda.device(buf.device):
+        if workspace is None:
+            rc = _lib().xxh3_gpu_batch_varlen(_vp(buf), _vp(offsets), _vp(lengths), n, seed & 0xFFFFFFFFFFFFFFFF,
+                                              _vp(seeds), _vp(out), _stream_handle(stream))
+        else:
+            rc = _lib().xxh3_gpu_batch_varlen_ws(_vp(buf), _vp(offsets), _vp(lengths), n, seed & 0xFFFFFFFFFFFFFFFF,
+                                                 _vp(seeds), _vp(out), _vp(workspace),
+                                                 workspace.numel() * workspace.element_size(), _stream_handle(stream))
+    _check(rc, "xxh3_gpu_batch_varlen")
+    return out

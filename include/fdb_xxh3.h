@@ -1,0 +1,54 @@
+/*
+ * Batched XXH3-64 on MI355X (gfx950) -- C ABI of libfdb_crc32c.so.
+ *
+ * Replaces, for device-resident batches, the per-buffer calls
+ *   XXH64_hash_t XXH3_64bits(const void* data, size_t len);
+ *   XXH64_hash_t XXH3_64bits_withSeed(const void* data, size_t len, XXH64_hash_t seed);
+ * declared at flow/include/flow/xxhash.h:456,465 (xxHash v0.8.0, default
+ * secret) and called per page/packet at
+ *   fdbserver/kvstore/KeyValueStoreSQLite.cpp:112,138   (SQLite page checksum, 4088 B)
+ *   fdbserver/kvstore/DiskQueue.cpp:1086-1088           (DiskQueue V2 page, 4088 B at +8)
+ *   fdbserver/kvstore/IPager.h:300,308,325,330          (Redwood headers / payloads, seeded)
+ *   fdbrpc/FlowTransport.cpp:1346,2043                  (packet checksums)
+ * Results are bit-identical to those functions for every input, length
+ * (0 .. 2^64-1) and seed; `seed` 0 is XXH3_64bits.
+ *
+ * Conventions (shared with include/fdb_crc32c.h): device pointers, caller
+ * owns every buffer, calls are asynchronous on `stream` (a hipStream_t, NULL
+ * = default stream), return 0 or a negative FDB_CRC32C_E* status; the
+ * message of the last failure on this thread is crc32c_gpu_last_error().
+ */
+#ifndef FDB_XXH3_H
+#define FDB_XXH3_H
+
+#include <stdint.h>
+
+#include "fdb_crc32c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Buffer i is bytes [d_base + i*stride, +length); d_out[i] = XXH3_64bits_withSeed(
+ * buffer i, length, d_seeds ? d_seeds[i] : seed). */
+int xxh3_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length, uint64_t count, uint64_t seed,
+                         const uint64_t* d_seeds, uint64_t* d_out, void* stream);
+
+/* Buffer i is bytes [d_base + d_offsets[i], +d_lengths[i]) (any alignment,
+ * any order, overlaps allowed).  Work is balanced over the GPU by bytes,
+ * whole buffers per wavefront. */
+int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                          uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* stream);
+
+/* Same with a caller-owned device workspace (16-byte aligned, size from
+ * xxh3_gpu_varlen_workspace_bytes): no allocation, capture-safe. */
+uint64_t xxh3_gpu_varlen_workspace_bytes(uint64_t count);
+int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                             uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
+                             uint64_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FDB_XXH3_H */

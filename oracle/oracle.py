@@ -157,3 +157,129 @@ def splitmix64(nwords, state):
     out = np.empty(nwords, dtype=np.uint64)
     oracle().lib.oracle_splitmix64_fill(out.ctypes.data, nwords, state)
     return out
+
+
+# ---------------------------------------------------------------- XXH3-64 / lookup3
+# liboracle_xxh3.so: our restatement (xxh3_oracle.c); _ref/libxxhash_ref.so:
+# the reference's flow/xxhash.c + flow/Hash3.c compiled unmodified.
+XXH3_SO = os.path.join(_HERE, "liboracle_xxh3.so")
+XXH3_REF_SO = os.path.join(_HERE, "_ref", "libxxhash_ref.so")
+_x = None
+_xref = None
+
+
+def _xxh3():
+    global _x
+    if _x is None:
+        if not os.path.exists(XXH3_SO):
+            build()
+        L = ctypes.CDLL(XXH3_SO)
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.oracle_xxh3_64.restype = u64
+        L.oracle_xxh3_64.argtypes = [vp, ctypes.c_size_t, u64]
+        L.oracle_hashlittle2.restype = None
+        L.oracle_hashlittle2.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_uint32)]
+        L.oracle_xxh3_batch_fixed.restype = None
+        L.oracle_xxh3_batch_fixed.argtypes = [vp, u64, u64, u64, u64, vp, vp, ctypes.c_int]
+        L.oracle_xxh3_batch_varlen.restype = None
+        L.oracle_xxh3_batch_varlen.argtypes = [vp, vp, vp, u64, u64, vp, vp, ctypes.c_int]
+        _x = L
+    return _x
+
+
+def _as_bytes(data):
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data).view(np.uint8)
+        return a, a.ctypes.data, a.nbytes
+    b = bytes(data)
+    return b, b, len(b)
+
+
+def xxh3_64(data, seed=0):
+    keep, p, n = _as_bytes(data)
+    return _xxh3().oracle_xxh3_64(p, n, seed & 0xFFFFFFFFFFFFFFFF)
+
+
+def hashlittle2(data, pc, pb):
+    keep, p, n = _as_bytes(data)
+    c, b = ctypes.c_uint32(pc), ctypes.c_uint32(pb)
+    _xxh3().oracle_hashlittle2(p, n, ctypes.byref(c), ctypes.byref(b))
+    return c.value, b.value
+
+
+def xxh3_batch_fixed(buf, stride, length, count, seed=0, seeds=None, threads=None):
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    if count:
+        assert (count - 1) * stride + length <= buf.nbytes
+    out = np.zeros(count, dtype=np.uint64)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint64)
+    threads = threads or min(16, os.cpu_count() or 1)
+    _xxh3().oracle_xxh3_batch_fixed(buf.ctypes.data, stride, length, count, seed & 0xFFFFFFFFFFFFFFFF,
+                                    None if sd is None else sd.ctypes.data, out.ctypes.data, threads)
+    return out
+
+
+def xxh3_batch_varlen(buf, offsets, lengths, seed=0, seeds=None, threads=None):
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+    n = offsets.size
+    if n:
+        assert int((offsets + lengths).max()) <= buf.nbytes
+    out = np.zeros(n, dtype=np.uint64)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint64)
+    threads = threads or min(16, os.cpu_count() or 1)
+    _xxh3().oracle_xxh3_batch_varlen(buf.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, n,
+                                     seed & 0xFFFFFFFFFFFFFFFF, None if sd is None else sd.ctypes.data,
+                                     out.ctypes.data, threads)
+    return out
+
+
+def xxh3_reference_available():
+    return os.path.exists(XXH3_REF_SO)
+
+
+def xxh3_reference():
+    """The reference's XXH3_64bits / XXH3_64bits_withSeed / hashlittle2 (compiled unmodified)."""
+    global _xref
+    if _xref is None:
+        if not os.path.exists(XXH3_REF_SO):
+            raise FileNotFoundError(XXH3_REF_SO + " (run `make -C oracle` where /root/reference exists)")
+        L = ctypes.CDLL(XXH3_REF_SO)
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.XXH3_64bits.restype = u64
+        L.XXH3_64bits.argtypes = [vp, ctypes.c_size_t]
+        L.XXH3_64bits_withSeed.restype = u64
+        L.XXH3_64bits_withSeed.argtypes = [vp, ctypes.c_size_t, u64]
+        L.hashlittle2.restype = None
+        L.hashlittle2.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+        _xref = L
+    return _xref
+
+
+def ref_xxh3_64(data, seed=0):
+    keep, p, n = _as_bytes(data)
+    L = xxh3_reference()
+    return L.XXH3_64bits(p, n) if seed == 0 else L.XXH3_64bits_withSeed(p, n, seed & 0xFFFFFFFFFFFFFFFF)
+
+
+def ref_hashlittle2(data, pc, pb):
+    keep, p, n = _as_bytes(data)
+    c, b = ctypes.c_uint32(pc), ctypes.c_uint32(pb)
+    xxh3_reference().hashlittle2(p, n, ctypes.byref(c), ctypes.byref(b))
+    return c.value, b.value
+
+
+def ref_xxh3_batch_fixed(buf, stride, length, count, seed=0):
+    """Single-threaded C loop over the reference XXH3_64bits (ref_bench_xxh3.c; bench cpu_baseline)."""
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    if count:
+        assert (count - 1) * stride + length <= buf.nbytes
+    L = xxh3_reference()
+    f = L.ref_xxh3_batch_fixed
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+    out = np.zeros(count, dtype=np.uint64)
+    f(buf.ctypes.data, stride, length, count, seed & 0xFFFFFFFFFFFFFFFF, out.ctypes.data)
+    return out

@@ -1,0 +1,185 @@
+"""Batched XXH3-64 (include/fdb_xxh3.h) and the lookup3 checker.
+
+CPU tests pin the oracle restatement (oracle/xxh3_oracle.c) to the fixtures
+the reference's own flow/xxhash.c and flow/Hash3.c produced
+(tests/golden/make_golden_xxh3.py) and to the known answers in
+flow/Hash3.c:1248-1263.  GPU tests run the gfx950 kernels through the C ABI
+and compare bit-for-bit with the fixtures and the oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "xxh3_golden.json")
+
+
+@pytest.fixture(scope="module")
+def xg():
+    with open(GOLDEN) as fh:
+        return json.load(fh)
+
+
+def sm_bytes(nbytes, state):
+    return O.splitmix64((nbytes + 7) // 8, state).view(np.uint8)[:nbytes].copy()
+
+
+def hexs(a):
+    return ["%016x" % int(v) for v in a]
+
+
+def digest(a):
+    a = np.asarray(a, dtype=np.uint64)
+    return {"xor": "%016x" % int(np.bitwise_xor.reduce(a)), "sum": "%016x" % int(a.sum(dtype=np.uint64))}
+
+
+# ------------------------------------------------------------------ CPU (oracle)
+
+def test_oracle_grid_matches_reference_fixtures(xg):
+    data = sm_bytes((1 << 20) + 64, 0x5EED)
+    for row in xg["grid"]:
+        off, seed = row["offset"], row["seed"]
+        got = [O.xxh3_64(data[off:off + L], seed) for L in xg["lengths"]]
+        assert hexs(got) == row["xxh3"], (off, seed)
+
+
+def test_oracle_pages_match_reference_fixtures(xg):
+    p = xg["pages"]
+    pages = sm_bytes(p["count"] * 4096, p["state"])
+    sq = O.xxh3_batch_fixed(pages, 4096, 4088, p["count"])
+    assert hexs(sq[:4]) == p["sqlite_4088"]["first"]
+    assert digest(sq) == {k: p["sqlite_4088"][k] for k in ("xor", "sum")}
+    dq = O.xxh3_batch_fixed(pages[8:], 4096, 4088, p["count"] - 1)
+    assert digest(dq) == {k: p["diskqueue_4088_at8"][k] for k in ("xor", "sum")}
+    idx = np.arange(0, p["count"], 16, dtype=np.uint64)
+    rw = O.xxh3_batch_varlen(pages, idx * 4096, np.full(idx.size, 4096, np.uint64), seeds=idx)
+    assert digest(rw) == p["redwood_seeded_4096_every16"]
+
+
+def test_hashlittle2_known_answers(xg):
+    # the reference's own expected outputs, flow/Hash3.c:1248-1259 (c, b)
+    s = b"Four score and seven years ago"
+    assert O.hashlittle2(b"", 0, 0) == (0xdeadbeef, 0xdeadbeef)
+    assert O.hashlittle2(b"", 0, 0xdeadbeef) == (0xbd5b7dde, 0xdeadbeef)
+    assert O.hashlittle2(b"", 0xdeadbeef, 0xdeadbeef) == (0x9c093ccd, 0xbd5b7dde)
+    assert O.hashlittle2(s, 0, 0) == (0x17770551, 0xce7226e6)
+    assert O.hashlittle2(s, 0, 1) == (0xe3607cae, 0xbd371de4)
+    assert O.hashlittle2(s, 1, 0) == (0xcd628161, 0x6cbea4b3)
+    for k in xg["hashlittle2"]["kat"]:
+        assert list(O.hashlittle2(bytes.fromhex(k["hex"]), k["pc"], k["pb"])) == k["out"]
+    pages = sm_bytes(64 * 4096, 0x5EED)
+    for row in xg["hashlittle2"]["pages"]:
+        pg = pages[4096 * row["page"]:4096 * (row["page"] + 1)]
+        assert list(O.hashlittle2(pg[:4088], row["page"] + 1, 0x5ca1ab1e)) == row["sqlite"]
+        assert list(O.hashlittle2(pg[16:], 0x12345678, 0xbeefabcd)) == row["diskqueue"]
+
+
+@pytest.mark.skipif(not O.xxh3_reference_available(), reason="reference build absent")
+def test_oracle_against_reference_random():
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, 1 << 18, dtype=np.uint8)
+    for _ in range(400):
+        n = int(rng.integers(0, 5000))
+        off = int(rng.integers(0, 64))
+        seed = int(rng.integers(0, 2 ** 63)) if rng.random() < 0.5 else 0
+        assert O.xxh3_64(data[off:off + n], seed) == O.ref_xxh3_64(data[off:off + n], seed)
+
+
+# ------------------------------------------------------------------ GPU parity
+
+def dev_bytes(h, cuda):
+    import torch
+    return torch.from_numpy(h).to(cuda)
+
+
+def i64(a, cuda):
+    import torch
+    return torch.tensor(np.asarray(a, dtype=np.int64), device=cuda)
+
+
+def host(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.gpu
+def test_gpu_grid_golden(xg, cuda):
+    import foundationdb_amd.xxh3 as X
+    data = sm_bytes((1 << 20) + 64, 0x5EED)
+    d = dev_bytes(data, cuda)
+    L = np.array(xg["lengths"], dtype=np.int64)
+    for row in xg["grid"]:
+        offs = np.full(L.size, row["offset"], dtype=np.int64)
+        got = host(X.batch_varlen(d, i64(offs, cuda), i64(L, cuda), seed=row["seed"]))
+        assert hexs(got) == row["xxh3"], (row["offset"], row["seed"])
+
+
+@pytest.mark.gpu
+def test_gpu_pages_golden(xg, cuda):
+    import torch
+    import foundationdb_amd.xxh3 as X
+    p = xg["pages"]
+    pages = sm_bytes(p["count"] * 4096, p["state"])
+    d = dev_bytes(pages, cuda)
+    sq = host(X.batch_fixed(d, 4096, 4088, p["count"]))
+    assert hexs(sq[:4]) == p["sqlite_4088"]["first"]
+    assert digest(sq) == {k: p["sqlite_4088"][k] for k in ("xor", "sum")}
+    dq = host(X.batch_fixed(d, 4096, 4088, p["count"] - 1, byte_offset=8))
+    assert digest(dq) == {k: p["diskqueue_4088_at8"][k] for k in ("xor", "sum")}
+    idx = np.arange(0, p["count"], 16, dtype=np.int64)
+    seeds = torch.tensor(idx, device=cuda)
+    rw = host(X.batch_fixed(d, 4096 * 16, 4096, idx.size, seeds=seeds))
+    assert digest(rw) == p["redwood_seeded_4096_every16"]
+
+
+@pytest.mark.gpu
+def test_gpu_fixed_lengths_vs_oracle(cuda):
+    import foundationdb_amd.xxh3 as X
+    h = sm_bytes(1 << 22, 0xC0FFEE)
+    d = dev_bytes(h, cuda)
+    for length in (0, 1, 3, 4, 8, 9, 16, 17, 128, 129, 240, 241, 1000, 1024, 1025, 4088, 4096, 5000, 16384):
+        for stride in (length or 1, ((length + 15) & ~15) or 16, 4096 * 5):
+            count = min(600, (h.size - length) // stride + 1)
+            for seed in (0, 0xFDBEEFDB):
+                got = host(X.batch_fixed(d, stride, length, count, seed=seed))
+                assert np.array_equal(got, O.xxh3_batch_fixed(h, stride, length, count, seed=seed)), (length, stride)
+
+
+@pytest.mark.gpu
+def test_gpu_varlen_random_vs_oracle(cuda):
+    import torch
+    import foundationdb_amd.xxh3 as X
+    rng = np.random.default_rng(5)
+    h = sm_bytes(1 << 24, 0xBEEF)
+    d = dev_bytes(h, cuda)
+    n = 30000
+    lens = np.where(rng.random(n) < 0.5, rng.integers(0, 300, n), rng.integers(0, 40000, n)).astype(np.int64)
+    offs = rng.integers(0, h.size - 40000, n).astype(np.int64)
+    seeds = rng.integers(0, 2 ** 63, n, dtype=np.int64)
+    got = host(X.batch_varlen(d, i64(offs, cuda), i64(lens, cuda)))
+    assert np.array_equal(got, O.xxh3_batch_varlen(h, offs, lens))
+    got = host(X.batch_varlen(d, i64(offs, cuda), i64(lens, cuda), seeds=torch.tensor(seeds, device=cuda)))
+    assert np.array_equal(got, O.xxh3_batch_varlen(h, offs, lens, seeds=seeds.view(np.uint64)))
+    # a few large buffers mixed with tiny ones (one wave per large buffer)
+    lens2 = np.array([1 << 20, 3, (1 << 20) + 17, 0, 100000, 241], dtype=np.int64)
+    offs2 = np.array([0, 5, 1 << 21, 77, (1 << 22) + 9, 1 << 23], dtype=np.int64)
+    got = host(X.batch_varlen(d, i64(offs2, cuda), i64(lens2, cuda), seed=7))
+    assert np.array_equal(got, O.xxh3_batch_varlen(h, offs2, lens2, seed=7))
+
+
+@pytest.mark.gpu
+def test_gpu_empty_and_workspace(cuda):
+    import torch
+    import foundationdb_amd.xxh3 as X
+    h = sm_bytes(1 << 16, 3)
+    d = dev_bytes(h, cuda)
+    assert X.batch_fixed(d, 4096, 4088, 0).numel() == 0
+    n = 1000
+    offs = np.arange(n, dtype=np.int64) * 37
+    lens = (np.arange(n, dtype=np.int64) * 13) % 2000
+    ws = torch.empty(X.varlen_workspace_bytes(n), dtype=torch.uint8, device=cuda)
+    got = host(X.batch_varlen(d, i64(offs, cuda), i64(lens, cuda), workspace=ws))
+    assert np.array_equal(got, O.xxh3_batch_varlen(h, offs, lens))
