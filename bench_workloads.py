@@ -269,7 +269,7 @@ class Xxh3Pages:
     XXH3_64bits(page, 4088) per page (fdbserver/kvstore/KeyValueStoreSQLite.cpp:112),
     1 Mi pages resident in HBM."""
     metric = "device-resident XXH3-64 GiB/s on 4 KiB page batches (4088 B hashed per page); % of HBM-read peak"
-    kernel_name = "fdbxxh::k_xxh3<true>"
+    kernel_name = "fdbxxh::k_xxh3_rows<false>"
 
     def __init__(self, dev, rank, count=1 << 20, length=4088, seed=0):
         import foundationdb_amd.xxh3 as X

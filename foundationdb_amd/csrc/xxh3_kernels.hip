@@ -400,6 +400,157 @@ __global__ __launch_bounds__(256) void k_xxh3(XxhParams P) {
 }
 
 // ---------------------------------------------------------------------------
+// Fixed-length long buffers (> 240 B): four buffers per wave in lockstep, one
+// per 16-lane row.  Lane (g, k) = (l/4, l%4) of row r takes stripes
+// g, g+4, g+8, g+12 of every block for accumulator pair k: four contributions
+// add up in registers, then two DPP row rotates close the 4-lane sum (no
+// cross-row traffic).  A load instruction covers 256 contiguous bytes per
+// row.  The block stream of the wave's buffer groups runs two blocks per
+// unit, the next unit's loads in flight.
+// ---------------------------------------------------------------------------
+struct RowKeys {
+	uint64_t k0[4], k1[4];  // stripe g + 4i: secret + 8(g + 4i) + 16k, +8
+	uint64_t l0, l1;        // last stripe: secret + 121 + 16k, +8
+	uint64_t c0, c1;        // scramble: secret + 128 + 16k, +8
+	uint64_t g0, g1;        // merge: secret + 11 + 16k, +8
+};
+__device__ __forceinline__ RowKeys row_keys(int lane, uint64_t seed) {
+	const int l = lane & 15, k = l & 3, g = l >> 2;
+	RowKeys K;
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		K.k0[i] = sec_word(g + 4 * i + 2 * k, seed);
+		K.k1[i] = sec_word(g + 4 * i + 2 * k + 1, seed);
+	}
+	K.l0 = sec_at(15 + 2 * k, 1, seed);
+	K.l1 = sec_at(16 + 2 * k, 1, seed);
+	K.c0 = sec_word(16 + 2 * k, seed);
+	K.c1 = sec_word(17 + 2 * k, seed);
+	K.g0 = sec_at(1 + 2 * k, 3, seed);
+	K.g1 = sec_at(2 + 2 * k, 3, seed);
+	return K;
+}
+
+struct RowData {
+	uint64_t v[4][2];
+};
+
+template <bool SEEDS>
+__global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
+	const int lane = threadIdx.x & 63;
+	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
+	const uint64_t wpb = blockDim.x >> 6;
+	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
+	const uint64_t w = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	uint64_t per = (P.count + nwave - 1) / nwave;
+	per = (per + 3) & ~uint64_t(3);
+	const uint64_t begin = w * per;
+	const uint64_t end = begin + per < P.count ? begin + per : P.count;
+	if (begin >= end) return;
+	const uint64_t len = P.length;
+	const uint64_t nfull = (len - 1) >> 10;
+	const uint64_t ns = ((len - 1) - (nfull << 10)) >> 6;
+	const uint64_t nblk = nfull + 1;
+	const uint64_t ngroups = (end - begin + 3) >> 2;
+	const uint64_t E = ngroups * nblk;
+	const uint64_t base = reinterpret_cast<uint64_t>(P.base);
+	auto page_of = [&](uint64_t q) -> uint64_t {  // this lane's row's buffer in group q (clamped)
+		const uint64_t i = begin + 4 * q + r;
+		return i < end ? i : end - 1;
+	};
+	// stream positions (group, block) of the next load and the next compute
+	uint64_t lq = 0, lb = 0, cq = 0, cb = 0;
+	auto load = [&](RowData& D) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i) D.v[i][0] = D.v[i][1] = 0;
+		if (lq >= ngroups) return;
+		const uint64_t q = lq, b = lb;
+		if (++lb == nblk) {
+			lb = 0;
+			++lq;
+		}
+		const uint64_t p = base + page_of(q) * P.stride;
+		const bool fin = b == nfull;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint64_t s = g + 4 * i;
+			if (fin && s == 15) {  // last stripe, any alignment
+				const uint64_t a = p + len - 64 + 16 * k;
+				D.v[i][0] = ldu64(a);
+				D.v[i][1] = ldu64(a + 8);
+			} else if (!fin || s < ns) {
+				const u64x2 x = __builtin_nontemporal_load((g_u64x2*)(p + (b << 10) + 64 * s + 16 * k));
+				D.v[i][0] = x[0];
+				D.v[i][1] = x[1];
+			}
+		}
+	};
+	RowKeys K = row_keys(lane, P.seed);
+	uint64_t a0 = 0, a1 = 0;
+	auto compute = [&](const RowData& D) {
+		if (cq >= ngroups) return;
+		const uint64_t q = cq, b = cb;
+		if (++cb == nblk) {
+			cb = 0;
+			++cq;
+		}
+		const bool fin = b == nfull;
+		if (b == 0) {
+			if (SEEDS) K = row_keys(lane, P.seeds[page_of(q)]);
+			a0 = k == 0 ? P32_3 : (k == 1 ? P64_2 : (k == 2 ? P64_4 : P64_5));
+			a1 = k == 0 ? P64_1 : (k == 1 ? P64_3 : (k == 2 ? P32_2 : P32_1));
+		}
+		uint64_t d0 = 0, d1 = 0;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint64_t s = g + 4 * i;
+			const bool last = fin && s == 15;
+			const bool on = !fin || s < ns || last;
+			const uint64_t x0 = D.v[i][0] ^ (last ? K.l0 : K.k0[i]);
+			const uint64_t x1 = D.v[i][1] ^ (last ? K.l1 : K.k1[i]);
+			const uint64_t c0 = D.v[i][1] + (uint64_t)(uint32_t)x0 * (x0 >> 32);
+			const uint64_t c1 = D.v[i][0] + (uint64_t)(uint32_t)x1 * (x1 >> 32);
+			d0 += on ? c0 : 0;
+			d1 += on ? c1 : 0;
+		}
+		// sum over g (lanes l, l+4, l+8, l+12 of the row)
+		uint32_t lo0 = (uint32_t)d0, hi0 = (uint32_t)(d0 >> 32), lo1 = (uint32_t)d1, hi1 = (uint32_t)(d1 >> 32);
+		add_dpp<0x124>(lo0, hi0);
+		add_dpp<0x124>(lo1, hi1);
+		add_dpp<0x128>(lo0, hi0);
+		add_dpp<0x128>(lo1, hi1);
+		a0 += ((uint64_t)hi0 << 32) | lo0;
+		a1 += ((uint64_t)hi1 << 32) | lo1;
+		if (!fin) {
+			a0 = ((a0 ^ (a0 >> 47)) ^ K.c0) * P32_1;
+			a1 = ((a1 ^ (a1 >> 47)) ^ K.c1) * P32_1;
+		} else {
+			// merge: lanes 0..3 of the row (g = 0) hold the 8 accumulators
+			const uint64_t m = mulfold(a0 ^ K.g0, a1 ^ K.g1);
+			uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+			add_dpp<0xB1>(lo, hi);
+			add_dpp<0x4E>(lo, hi);
+			const uint64_t h = xxh3_aval(len * P64_1 + (((uint64_t)hi << 32) | lo));
+			const uint64_t i = begin + 4 * q + r;
+			if (l == 0 && i < end) P.out[i] = h;
+		}
+	};
+	RowData c0, c1, n0, n1;
+	load(c0);
+	load(c1);
+	for (uint64_t e = 0; e < E; e += 2) {
+		load(n0);
+		load(n1);
+		__builtin_amdgcn_sched_barrier(0);
+		compute(c0);
+		compute(c1);
+		__builtin_amdgcn_sched_barrier(0);
+		c0 = n0;
+		c1 = n1;
+	}
+}
+
+// ---------------------------------------------------------------------------
 // Varlen planning: whole buffers per wave, balanced by bytes.  Wave w takes
 // the buffers whose start lies in [w*Q, (w+1)*Q) of the concatenated stream.
 // ---------------------------------------------------------------------------
@@ -511,7 +662,19 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(P.lengths, P.count, tiles, ntile, wave_first, nwave);
 		P.wave_first = wave_first;
 	}
-	if (aligned)
+	if (!P.offsets && P.length > 240 && aligned) {
+		// fixed-length pages: four per wave in lockstep
+		static const int rows_bpc = [] {
+			int a = 0;
+			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xxh3_rows<false>, 256, 0) != hipSuccess) a = 4;
+			return a < 1 ? 1 : a;
+		}();
+		const uint64_t g2 = (uint64_t)num_cus * rows_bpc;
+		if (P.seeds)
+			k_xxh3_rows<true><<<(unsigned)g2, 256, 0, stream>>>(P);
+		else
+			k_xxh3_rows<false><<<(unsigned)g2, 256, 0, stream>>>(P);
+	} else if (aligned)
 		k_xxh3<true><<<(unsigned)grid, 256, 0, stream>>>(P);
 	else
 		k_xxh3<false><<<(unsigned)grid, 256, 0, stream>>>(P);
