@@ -8,8 +8,10 @@
 #include <string>
 
 #include "../../include/fdb_crc32c.h"
+#include "../../include/fdb_pagecheck.h"
 #include "../../include/fdb_xxh3.h"
 #include "crc32c_device.h"
+#include "pagecheck.h"
 #include "xxh3_device.h"
 
 namespace fdbcrc {
@@ -306,6 +308,80 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
 	                              fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus)), &ws, &have))
 		return rc;
 	return xxh3_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
+}
+
+// ---- page verifiers (include/fdb_pagecheck.h) ---------------------------------
+
+uint64_t fdb_pagecheck_workspace_bytes(uint64_t count) { return fdbpc::workspace_bytes(count); }
+
+static int pages_ok(const void* d_pages, uint64_t page_size, uint64_t count, const void* d_out, const char* who) {
+	if (!d_pages || !d_out) return fail(FDB_CRC32C_EINVAL, who);
+	if (reinterpret_cast<uintptr_t>(d_pages) % 16) return fail(FDB_CRC32C_EINVAL, "pages must be 16-byte aligned");
+	if (page_size % 8 || page_size <= 248 || page_size >= (1ull << 31))
+		return fail(FDB_CRC32C_EINVAL, "page_size must be a multiple of 8 in (248, 2^31)");
+	if (count >= (1ull << 32)) return fail(FDB_CRC32C_EINVAL, "count must be < 2^32");
+	return 0;
+}
+
+int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno,
+                               uint8_t* d_status, uint64_t* d_bad, void* d_workspace, uint64_t workspace_bytes,
+                               void* stream) {
+	if (count == 0) {
+		if (d_bad) (void)hipMemsetAsync(d_bad, 0, 8, reinterpret_cast<hipStream_t>(stream));
+		return 0;
+	}
+	if (int rc = pages_ok(d_pages, page_size, count, d_status, "fdb_sqlite_verify_pages: null pointer")) return rc;
+	if (!d_workspace || workspace_bytes < fdbpc::workspace_bytes(count) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_sqlite_verify_pages: workspace too small or misaligned");
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	if (fdbpc::sqlite_verify(static_cast<const uint8_t*>(d_pages), page_size, count, first_pgno, d_status, d_bad,
+	                         st->tables, st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "fdb_sqlite_verify_pages: launch setup failed");
+	return check_launch("fdb_sqlite_verify_pages launch");
+}
+
+int fdb_sqlite_verify_pages(const void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno,
+                            uint8_t* d_status, uint64_t* d_bad, void* stream) {
+	if (count == 0) return fdb_sqlite_verify_pages_ws(d_pages, page_size, 0, first_pgno, d_status, d_bad, nullptr, 0,
+	                                                  stream);
+	if (int rc = pages_ok(d_pages, page_size, count, d_status, "fdb_sqlite_verify_pages: null pointer")) return rc;
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have))
+		return rc;
+	return fdb_sqlite_verify_pages_ws(d_pages, page_size, count, first_pgno, d_status, d_bad, ws, have, stream);
+}
+
+int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad,
+                                 void* d_workspace, uint64_t workspace_bytes, void* stream) {
+	if (count == 0) {
+		if (d_bad) (void)hipMemsetAsync(d_bad, 0, 8, reinterpret_cast<hipStream_t>(stream));
+		return 0;
+	}
+	if (int rc = pages_ok(d_pages, 4096, count, d_ok, "fdb_diskqueue_check_pages: null pointer")) return rc;
+	if (!d_workspace || workspace_bytes < fdbpc::workspace_bytes(count) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_diskqueue_check_pages: workspace too small or misaligned");
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	if (fdbpc::diskqueue_check(static_cast<const uint8_t*>(d_pages), count, d_ok, d_bad, st->tables, st->num_cus,
+	                           d_workspace, reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "fdb_diskqueue_check_pages: launch setup failed");
+	return check_launch("fdb_diskqueue_check_pages launch");
+}
+
+int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad, void* stream) {
+	if (count == 0) return fdb_diskqueue_check_pages_ws(d_pages, 0, d_ok, d_bad, nullptr, 0, stream);
+	if (int rc = pages_ok(d_pages, 4096, count, d_ok, "fdb_diskqueue_check_pages: null pointer")) return rc;
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have))
+		return rc;
+	return fdb_diskqueue_check_pages_ws(d_pages, count, d_ok, d_bad, ws, have, stream);
 }
 
 const char* crc32c_gpu_last_error(void) { return t_err.c_str(); }

@@ -24,6 +24,9 @@ int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint
 // Bytes [h, 4096 - t) of 4 KiB pages (h, t < 16); `pages` 16-byte aligned.
 int launch_pages_window(const uint8_t* pages, uint64_t stride, uint64_t count, uint32_t h, uint32_t t, uint32_t seed,
                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream);
+int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32_t* idx, const uint64_t* d_count,
+                             uint64_t max_count, uint32_t h, uint32_t t, uint32_t seed, uint32_t* out,
+                             const DevTables* tabs, int num_cus, hipStream_t stream);
 // Variable-length engine (crc32c_varlen.hip).  ws: varlen_workspace_bytes().
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,

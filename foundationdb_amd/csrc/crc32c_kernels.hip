@@ -170,11 +170,19 @@ __device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t
 	return r;
 }
 
-template <int U, bool WINDOW = false>
+// LIST: page i of the batch is page idx[i] of `base` and the batch size is
+// read from *d_count (device-side compaction output, pagecheck.hip).
+template <int U, bool WINDOW = false, bool LIST = false>
 __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
                                                   uint32_t seed, const uint32_t* __restrict__ seeds,
                                                   uint32_t* __restrict__ out, const DevTables* __restrict__ tabs,
-                                                  uint32_t h = 0, uint32_t t = 0) {
+                                                  uint32_t h = 0, uint32_t t = 0,
+                                                  const uint32_t* __restrict__ idx = nullptr,
+                                                  const uint64_t* __restrict__ d_count = nullptr) {
+	if (LIST) {
+		count = *d_count;
+		if (count == 0) return;  // the list is empty: idx[] holds nothing to read
+	}
 	constexpr uint64_t G = 2 * U * (64 / (2 * U));  // a whole number of loop iterations
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const LaneCtx c = make_ctx();
@@ -191,7 +199,10 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 	const uint64_t last = end ? end - 1 : 0;
 	// page index -> address, clamped into this wave's run: clamped duplicates
 	// are computed and discarded, so every load is consumed unconditionally
-	auto page = [&](uint64_t i) { return base + (i < end ? i : (begin < end ? last : 0)) * stride; };
+	auto page = [&](uint64_t i) {
+		const uint64_t j = i < end ? i : (begin < end ? last : 0);
+		return base + (LIST ? (uint64_t)idx[j] : j) * stride;
+	};
 	auto load_u = [&](Block (&u)[U], uint64_t i0) {
 #pragma unroll
 		for (int j = 0; j < U; ++j) load_block(u[j], page(i0 + j), c.ld_off);
@@ -255,6 +266,20 @@ int launch_pages_window(const uint8_t* pages, uint64_t stride, uint64_t count, u
 	if (grid > (uint64_t)num_cus) grid = num_cus;
 	if (grid == 0) grid = 1;
 	k_pages4k<2, true><<<(unsigned)grid, 1024, 0, stream>>>(pages, stride, count, seed, seeds, out, tabs, h, t);
+	return 0;
+}
+
+// Same over a device-side list: page j of the batch = page idx[j], j < *d_count
+// (max_count bounds the grid).
+int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32_t* idx, const uint64_t* d_count,
+                             uint64_t max_count, uint32_t h, uint32_t t, uint32_t seed, uint32_t* out,
+                             const DevTables* tabs, int num_cus, hipStream_t stream) {
+	const uint64_t units = (max_count + 63) / 64;
+	uint64_t grid = (units + 15) / 16;
+	if (grid > (uint64_t)num_cus) grid = num_cus;
+	if (grid == 0) grid = 1;
+	k_pages4k<2, true, true><<<(unsigned)grid, 1024, 0, stream>>>(pages, stride, max_count, seed, nullptr, out, tabs,
+	                                                              h, t, idx, d_count);
 	return 0;
 }
 

@@ -1,0 +1,16 @@
+// Batched page-format verifiers (pagecheck.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_device.h"
+
+namespace fdbpc {
+
+uint64_t workspace_bytes(uint64_t count);
+int sqlite_verify(const uint8_t* pages, uint64_t page_size, uint64_t count, uint32_t first_pgno, uint8_t* status,
+                  uint64_t* d_bad, const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s);
+int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t* d_bad,
+                    const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s);
+
+}  // namespace fdbpc

@@ -13,6 +13,8 @@ struct XxhParams {
 	const uint64_t* seeds;       // per-buffer seeds or nullptr
 	uint64_t* out;
 	const uint64_t* wave_first;  // varlen: first buffer of every wave [nwave + 1] (planner output)
+	const uint32_t* idx;         // fixed list mode: buffer i = base + idx[i]*stride, count = *d_count
+	const uint64_t* d_count;
 };
 
 constexpr unsigned kWavesPerBlock = 4;
@@ -21,5 +23,8 @@ int xxh3_blocks_per_cu();
 inline uint64_t xxh3_nwave(int num_cus) { return (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock; }
 uint64_t xxh3_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_xxh3(const XxhParams& P, int num_cus, void* ws, hipStream_t stream);
+// Fixed-length (> 240 B, 16-byte aligned base and stride) pages over a device
+// list: buffer j = base + idx[j]*stride, j < *d_count; P.count bounds the grid.
+int launch_xxh3_pages_list(const XxhParams& P, int num_cus, hipStream_t stream);
 
 }  // namespace fdbxxh

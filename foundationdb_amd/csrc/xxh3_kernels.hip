@@ -435,8 +435,11 @@ struct RowData {
 	uint64_t v[4][2];
 };
 
-template <bool SEEDS>
+// A16: base and stride 16-byte aligned (dwordx4 loads), else 8-byte aligned
+// (two dwordx2 loads per 16 B).
+template <bool SEEDS, bool LIST = false, bool A16 = true>
 __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
+	if (LIST) P.count = *P.d_count;
 	const int lane = threadIdx.x & 63;
 	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
 	const uint64_t wpb = blockDim.x >> 6;
@@ -458,6 +461,17 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 		const uint64_t i = begin + 4 * q + r;
 		return i < end ? i : end - 1;
 	};
+	// LIST: the four page numbers of a group as scalar loads (lgkmcnt, off the
+	// vmcnt queue of the data prefetch), selected by row
+	auto addr_of = [&](uint64_t q) -> uint64_t {
+		if (!LIST) return base + page_of(q) * P.stride;
+		const uint64_t i0 = begin + 4 * q;
+		const uint64_t c = end - 1;
+		const uint32_t p0 = P.idx[i0 < end ? i0 : c], p1 = P.idx[i0 + 1 < end ? i0 + 1 : c];
+		const uint32_t p2 = P.idx[i0 + 2 < end ? i0 + 2 : c], p3 = P.idx[i0 + 3 < end ? i0 + 3 : c];
+		const uint32_t pr = r == 0 ? p0 : (r == 1 ? p1 : (r == 2 ? p2 : p3));
+		return base + (uint64_t)pr * P.stride;
+	};
 	// stream positions (group, block) of the next load and the next compute
 	uint64_t lq = 0, lb = 0, cq = 0, cb = 0;
 	auto load = [&](RowData& D) {
@@ -469,7 +483,7 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 			lb = 0;
 			++lq;
 		}
-		const uint64_t p = base + page_of(q) * P.stride;
+		const uint64_t p = addr_of(q);
 		const bool fin = b == nfull;
 #pragma unroll
 		for (int i = 0; i < 4; ++i) {
@@ -479,9 +493,15 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 				D.v[i][0] = ldu64(a);
 				D.v[i][1] = ldu64(a + 8);
 			} else if (!fin || s < ns) {
-				const u64x2 x = __builtin_nontemporal_load((g_u64x2*)(p + (b << 10) + 64 * s + 16 * k));
-				D.v[i][0] = x[0];
-				D.v[i][1] = x[1];
+				const uint64_t a = p + (b << 10) + 64 * s + 16 * k;
+				if (A16) {
+					const u64x2 x = __builtin_nontemporal_load((g_u64x2*)a);
+					D.v[i][0] = x[0];
+					D.v[i][1] = x[1];
+				} else {
+					D.v[i][0] = __builtin_nontemporal_load((g_u64*)a);
+					D.v[i][1] = __builtin_nontemporal_load((g_u64*)(a + 8));
+				}
 			}
 		}
 	};
@@ -652,7 +672,8 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 	const unsigned wpb = kWavesPerBlock;
 	const uint64_t grid = (uint64_t)num_cus * xxh3_blocks_per_cu();
 	const uint64_t nwave = grid * wpb;
-	const bool aligned = ((reinterpret_cast<uint64_t>(P.base) | (P.offsets ? 1 : P.stride)) & 15) == 0;
+	const uint64_t mis = (reinterpret_cast<uint64_t>(P.base) | (P.offsets ? 1 : P.stride));
+	const bool aligned = (mis & 15) == 0;
 	if (P.offsets) {
 		const uint64_t ntile = (P.count + 255) / 256;
 		uint64_t* tiles = static_cast<uint64_t*>(ws);
@@ -662,22 +683,42 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(P.lengths, P.count, tiles, ntile, wave_first, nwave);
 		P.wave_first = wave_first;
 	}
-	if (!P.offsets && P.length > 240 && aligned) {
+	if (!P.offsets && P.length > 240 && (mis & 7) == 0) {
 		// fixed-length pages: four per wave in lockstep
 		static const int rows_bpc = [] {
 			int a = 0;
-			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xxh3_rows<false>, 256, 0) != hipSuccess) a = 4;
+			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xxh3_rows<true>, 256, 0) != hipSuccess) a = 3;
 			return a < 1 ? 1 : a;
 		}();
 		const uint64_t g2 = (uint64_t)num_cus * rows_bpc;
-		if (P.seeds)
-			k_xxh3_rows<true><<<(unsigned)g2, 256, 0, stream>>>(P);
+		if (P.seeds && aligned)
+			k_xxh3_rows<true, false, true><<<(unsigned)g2, 256, 0, stream>>>(P);
+		else if (P.seeds)
+			k_xxh3_rows<true, false, false><<<(unsigned)g2, 256, 0, stream>>>(P);
+		else if (aligned)
+			k_xxh3_rows<false, false, true><<<(unsigned)g2, 256, 0, stream>>>(P);
 		else
-			k_xxh3_rows<false><<<(unsigned)g2, 256, 0, stream>>>(P);
+			k_xxh3_rows<false, false, false><<<(unsigned)g2, 256, 0, stream>>>(P);
 	} else if (aligned)
 		k_xxh3<true><<<(unsigned)grid, 256, 0, stream>>>(P);
 	else
 		k_xxh3<false><<<(unsigned)grid, 256, 0, stream>>>(P);
+	return 0;
+}
+
+int launch_xxh3_pages_list(const XxhParams& P, int num_cus, hipStream_t stream) {
+	static const int bpc = [] {
+		int a = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xxh3_rows<false, true>, 256, 0) != hipSuccess) a = 3;
+		return a < 1 ? 1 : a;
+	}();
+	const unsigned grid = (unsigned)((uint64_t)num_cus * bpc);
+	const bool a16 = ((reinterpret_cast<uint64_t>(P.base) | P.stride) & 15) == 0;
+	if (((reinterpret_cast<uint64_t>(P.base) | P.stride) & 7) != 0 || P.length <= 240) return -1;
+	if (a16)
+		k_xxh3_rows<false, true, true><<<grid, 256, 0, stream>>>(P);
+	else
+		k_xxh3_rows<false, true, false><<<grid, 256, 0, stream>>>(P);
 	return 0;
 }
 

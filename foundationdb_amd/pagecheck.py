@@ -1,0 +1,66 @@
+"""Python host mirror of the batched page verifiers (include/fdb_pagecheck.h).
+
+Reference interfaces: PageChecksumCodec::checksum(pgno, page, pageLen,
+write=false) (fdbserver/kvstore/KeyValueStoreSQLite.cpp:100-201) and
+DiskQueue Page::checkHash (fdbserver/kvstore/DiskQueue.cpp:1047-1120), run
+over whole batches of device-resident pages.  No CPU fallback.
+"""
+import ctypes
+
+import torch
+
+from .crc32c import CRC32CError, _check, _require_device, _stream_handle, lib
+
+_bound = False
+
+STATUS_BAD, STATUS_CRC32C, STATUS_XXH3, STATUS_HASHLITTLE2 = 0, 1, 2, 3
+
+
+def _lib():
+    global _bound
+    L = lib()
+    if not _bound:
+        u32, u64, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
+        L.fdb_sqlite_verify_pages.restype = ctypes.c_int
+        L.fdb_sqlite_verify_pages.argtypes = [vp, u64, u64, u32, vp, vp, vp]
+        L.fdb_diskqueue_check_pages.restype = ctypes.c_int
+        L.fdb_diskqueue_check_pages.argtypes = [vp, u64, vp, vp, vp]
+        L.fdb_pagecheck_workspace_bytes.restype = u64
+        L.fdb_pagecheck_workspace_bytes.argtypes = [u64]
+        _bound = True
+    return L
+
+
+def _vp(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def sqlite_verify_pages(pages, page_size, count=None, first_pgno=1, stream=None):
+    """Returns (status uint8 tensor, bad-page count tensor) for a batch of SQLite pages."""
+    _require_device(pages, "pages")
+    nbytes = pages.numel() * pages.element_size()
+    count = nbytes // page_size if count is None else int(count)
+    if count * page_size > nbytes:
+        raise CRC32CError("sqlite_verify_pages: pages extend past the tensor")
+    status = torch.empty(count, dtype=torch.uint8, device=pages.device)
+    bad = torch.zeros(1, dtype=torch.uint64, device=pages.device)
+    with torch.cuda.device(pages.device):
+        rc = _lib().fdb_sqlite_verify_pages(_vp(pages), page_size, count, first_pgno, _vp(status), _vp(bad),
+                                            _stream_handle(stream))
+    _check(rc, "fdb_sqlite_verify_pages")
+    return status, bad
+
+
+def diskqueue_check_pages(pages, count=None, stream=None):
+    """Returns (ok uint8 tensor, bad-page count tensor) for a batch of 4 KiB DiskQueue pages."""
+    _require_device(pages, "pages")
+    nbytes = pages.numel() * pages.element_size()
+    count = nbytes // 4096 if count is None else int(count)
+    if count * 4096 > nbytes:
+        raise CRC32CError("diskqueue_check_pages: pages extend past the tensor")
+    ok = torch.empty(count, dtype=torch.uint8, device=pages.device)
+    bad = torch.zeros(1, dtype=torch.uint64, device=pages.device)
+    with torch.cuda.device(pages.device):
+        rc = _lib().fdb_diskqueue_check_pages(_vp(pages), count, _vp(ok), _vp(bad), _stream_handle(stream))
+    _check(rc, "fdb_diskqueue_check_pages")
+    return ok, bad

@@ -1,0 +1,55 @@
+/*
+ * Batched page-format verifiers on MI355X -- C ABI of libfdb_crc32c.so.
+ *
+ * fdb_sqlite_verify_pages replaces a loop of
+ *   PageChecksumCodec::checksum(pageNumber, page, pageLen, write = false)
+ * (fdbserver/kvstore/KeyValueStoreSQLite.cpp:100-201) over a batch of pages,
+ * e.g. the whole-file scan of SQLiteDB::checkAllPageChecksums (:1378-1470).
+ * Page i is bytes [d_pages + i*page_size, +page_size) with page number
+ * first_pgno + i.  d_status[i]:
+ *   1  the CRC-32C trailer matched   (part1 == 0, part2 == crc32c_append(0xfdbeefdb, page, page_size-8))
+ *   2  the XXH3 trailer matched      (part1 >> 24 == 0, (part1, part2) == XXH3_64bits split 24/32)
+ *   3  the hashlittle2 trailer matched (hashlittle2(page, page_size-8, pgno, 0x5ca1ab1e))
+ *   0  corrupt (the reference returns false and raises checksum_failed)
+ * checked in the reference's order, so the status is the check that the
+ * reference would have accepted.
+ *
+ * fdb_diskqueue_check_pages replaces a loop of DiskQueue Page::checkHash
+ * (fdbserver/kvstore/DiskQueue.cpp:1047-1120) over 4096-byte pages, by the
+ * header's implementationVersion: V0 hashlittle2 UID, V1 CRC-32C of [4,4096),
+ * V2 XXH3-64 of [8,4096); d_ok[i] = 1 when the stored hash matches, 0 otherwise.
+ *
+ * Both: device pointers, asynchronous on `stream`, d_bad (optional, device
+ * u64) receives the number of pages that failed.  Pages must be 16-byte
+ * aligned, page_size a multiple of 8 in (248, 2^31), count < 2^32.  Return
+ * 0 or a negative FDB_CRC32C_E* status (crc32c_gpu_last_error() explains).
+ */
+#ifndef FDB_PAGECHECK_H
+#define FDB_PAGECHECK_H
+
+#include <stdint.h>
+
+#include "fdb_crc32c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int fdb_sqlite_verify_pages(const void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno,
+                            uint8_t* d_status, uint64_t* d_bad, void* stream);
+int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad, void* stream);
+
+/* Caller-owned workspace variants (no allocation, capture-safe); size from
+ * fdb_pagecheck_workspace_bytes(count), 16-byte aligned. */
+uint64_t fdb_pagecheck_workspace_bytes(uint64_t count);
+int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno,
+                               uint8_t* d_status, uint64_t* d_bad, void* d_workspace, uint64_t workspace_bytes,
+                               void* stream);
+int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad,
+                                 void* d_workspace, uint64_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FDB_PAGECHECK_H */

@@ -283,3 +283,64 @@ def ref_xxh3_batch_fixed(buf, stride, length, count, seed=0):
     out = np.zeros(count, dtype=np.uint64)
     f(buf.ctypes.data, stride, length, count, seed & 0xFFFFFFFFFFFFFFFF, out.ctypes.data)
     return out
+
+
+# ---------------------------------------------------------------- page formats
+# Restatements of the reference's page checksum logic on top of the pinned
+# primitives above (checker side only).
+
+def sqlite_trailer_crc(page):
+    """Legacy writer: part1 = 0, part2 = crc32c_append(0xfdbeefdb, data) (KeyValueStoreSQLite.cpp:119-128)."""
+    data = bytes(page[:-8])
+    return (0).to_bytes(4, "little") + crc32c(0xFDBEEFDB, data).to_bytes(4, "little")
+
+
+def sqlite_trailer_xxh3(page):
+    """Current writer, KeyValueStoreSQLite.cpp:106-116."""
+    h = xxh3_64(bytes(page[:-8]))
+    return ((h >> 32) & 0x00FFFFFF).to_bytes(4, "little") + (h & 0xFFFFFFFF).to_bytes(4, "little")
+
+
+def sqlite_trailer_hl2(page, pgno):
+    c, b = hashlittle2(bytes(page[:-8]), pgno, 0x5CA1AB1E)
+    return c.to_bytes(4, "little") + b.to_bytes(4, "little")
+
+
+def sqlite_verify_page(page, pgno):
+    """PageChecksumCodec::checksum(write=false), KeyValueStoreSQLite.cpp:118-158: 1 CRC, 2 XXH3, 3 hashlittle2, 0 bad."""
+    page = bytes(page)
+    data, t = page[:-8], page[-8:]
+    part1, part2 = int.from_bytes(t[:4], "little"), int.from_bytes(t[4:], "little")
+    if part1 == 0 and part2 == crc32c(0xFDBEEFDB, data):
+        return 1
+    if (part1 >> 24) == 0:
+        h = xxh3_64(data)
+        if part1 == ((h >> 32) & 0x00FFFFFF) and part2 == (h & 0xFFFFFFFF):
+            return 2
+    c, b = hashlittle2(data, pgno, 0x5CA1AB1E)
+    return 3 if (c, b) == (part1, part2) else 0
+
+
+def diskqueue_hash(page, version):
+    """Page::updateHash (DiskQueue.cpp:1089-1106): the 16-byte hash field for `version`."""
+    page = bytes(page)
+    if version == 0:
+        c, b = hashlittle2(page[16:], 0x12345678, 0xBEEFABCD)
+        return ((c << 32) | b).to_bytes(8, "little") + (0xFDB).to_bytes(8, "little")
+    if version == 1:
+        return crc32c(0xFDBEEFDB, page[4:]).to_bytes(4, "little") + page[4:16]
+    return xxh3_64(page[8:]).to_bytes(8, "little") + page[8:16]
+
+
+def diskqueue_check_page(page):
+    """Page::checkHash (DiskQueue.cpp:1107-1120)."""
+    page = bytes(page)
+    ver = int.from_bytes(page[10:12], "little")
+    if ver == 0:
+        c, b = hashlittle2(page[16:], 0x12345678, 0xBEEFABCD)
+        return int(page[:8] == ((c << 32) | b).to_bytes(8, "little") and page[8:16] == (0xFDB).to_bytes(8, "little"))
+    if ver == 1:
+        return int(int.from_bytes(page[:4], "little") == crc32c(0xFDBEEFDB, page[4:]))
+    if ver == 2:
+        return int(int.from_bytes(page[:8], "little") == xxh3_64(page[8:]))
+    return 0

@@ -1,0 +1,133 @@
+"""Batched page verifiers (include/fdb_pagecheck.h) against the reference's
+page checksum logic (oracle restatement on the pinned CRC-32C / XXH3 / lookup3
+primitives) and the reference's own unit test
+/fdbserver/kvstore/SQLite/PageChecksum/LegacyCRC32
+(fdbserver/kvstore/KeyValueStoreSQLite.cpp:258-292)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def sm_bytes(nbytes, state):
+    return O.splitmix64((nbytes + 7) // 8, state).view(np.uint8)[:nbytes].copy()
+
+
+def legacy_page():
+    page = np.zeros(4096, np.uint8)
+    page[:4088] = (np.arange(4088) * 37 + 11) & 0xFF
+    page[4088:] = np.frombuffer(O.sqlite_trailer_crc(page), np.uint8)
+    return page
+
+
+def test_oracle_follows_reference_legacy_crc32_test():
+    page = legacy_page()
+    assert O.sqlite_verify_page(page, 2) == 1
+    page[4088 // 2] ^= 0xFF
+    assert O.sqlite_verify_page(page, 2) == 0
+    page[4088 // 2] ^= 0xFF
+    assert O.sqlite_verify_page(page, 2) == 1
+    page[4088:] = np.frombuffer(O.sqlite_trailer_xxh3(page), np.uint8)  # rewrite upgrades to xxHash3
+    assert O.sqlite_verify_page(page, 2) == 2
+    # golden trailer of the LegacyCRC32 page (0x23e52e01)
+    assert int.from_bytes(O.sqlite_trailer_crc(legacy_page())[4:], "little") == 0x23E52E01
+
+
+def make_sqlite_batch(n, page_size, first_pgno, seed):
+    rng = np.random.default_rng(seed)
+    pages = sm_bytes(n * page_size, seed).reshape(n, page_size)
+    kinds = rng.integers(0, 7, n)
+    for i in range(n):
+        pg, k = pages[i], kinds[i]
+        if k in (0, 4):
+            pg[-8:] = np.frombuffer(O.sqlite_trailer_crc(pg), np.uint8)
+        elif k in (1, 5):
+            pg[-8:] = np.frombuffer(O.sqlite_trailer_xxh3(pg), np.uint8)
+        elif k in (2, 6):
+            pg[-8:] = np.frombuffer(O.sqlite_trailer_hl2(pg, first_pgno + i), np.uint8)
+        if k >= 4:  # corrupt after writing: a data byte or a trailer byte
+            j = int(rng.integers(0, page_size))
+            pg[j] ^= 1 << int(rng.integers(0, 8))
+        # k == 3: random trailer (almost surely corrupt)
+    exp = np.array([O.sqlite_verify_page(pages[i], first_pgno + i) for i in range(n)], np.uint8)
+    return pages, exp
+
+
+def make_dq_batch(n, seed):
+    rng = np.random.default_rng(seed)
+    pages = sm_bytes(n * 4096, seed).reshape(n, 4096)
+    for i in range(n):
+        pg = pages[i]
+        ver = int(rng.choice([0, 1, 2, 2, 2, 3]))
+        pg[8:10] = np.frombuffer((0x1234).to_bytes(2, "little"), np.uint8)  # magic
+        pg[10:12] = np.frombuffer(ver.to_bytes(2, "little"), np.uint8)
+        if ver == 0:
+            pg[8:10] = np.frombuffer((0x0FDB).to_bytes(2, "little"), np.uint8)
+        pg[:16] = np.frombuffer(O.diskqueue_hash(pg, min(ver, 2)), np.uint8)
+        if rng.random() < 0.3:
+            j = int(rng.integers(0, 4096))
+            pg[j] ^= 0x10
+    exp = np.array([O.diskqueue_check_page(pages[i]) for i in range(n)], np.uint8)
+    return pages, exp
+
+
+def test_oracle_diskqueue_roundtrip():
+    pages, exp = make_dq_batch(200, 3)
+    assert 0 < exp.sum() < exp.size
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("page_size", [4096, 8192, 512, 65536])
+def test_gpu_sqlite_verify_mixed(cuda, page_size):
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    n = {4096: 3000, 8192: 800, 512: 4000, 65536: 64}[page_size]
+    first = 7
+    pages, exp = make_sqlite_batch(n, page_size, first, page_size)
+    d = torch.from_numpy(pages.reshape(-1)).to(cuda)
+    status, bad = PC.sqlite_verify_pages(d, page_size, first_pgno=first)
+    got = status.cpu().numpy()
+    assert np.array_equal(got, exp)
+    assert int(bad.cpu().numpy().view(np.uint64)[0]) == int((exp == 0).sum())
+    assert set(np.unique(exp)) >= {0, 1, 2, 3} or page_size == 65536
+
+
+@pytest.mark.gpu
+def test_gpu_sqlite_legacy_page_sequence(cuda):
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    page = legacy_page()
+    bad = page.copy()
+    bad[4088 // 2] ^= 0xFF
+    up = page.copy()
+    up[4088:] = np.frombuffer(O.sqlite_trailer_xxh3(up), np.uint8)
+    d = torch.from_numpy(np.concatenate([page, bad, page, up])).to(cuda)
+    status, nbad = PC.sqlite_verify_pages(d, 4096, first_pgno=2)
+    assert status.cpu().tolist() == [1, 0, 1, 2]
+    assert int(nbad.cpu().numpy().view(np.uint64)[0]) == 1
+
+
+@pytest.mark.gpu
+def test_gpu_diskqueue_check(cuda):
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    pages, exp = make_dq_batch(3000, 11)
+    d = torch.from_numpy(pages.reshape(-1)).to(cuda)
+    ok, bad = PC.diskqueue_check_pages(d)
+    assert np.array_equal(ok.cpu().numpy(), exp)
+    assert int(bad.cpu().numpy().view(np.uint64)[0]) == int((exp == 0).sum())
+
+
+@pytest.mark.gpu
+def test_gpu_pagecheck_all_one_kind_and_empty(cuda):
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    n = 2048
+    pages = sm_bytes(n * 4096, 99).reshape(n, 4096)
+    for i in range(n):
+        pages[i, -8:] = np.frombuffer(O.sqlite_trailer_xxh3(pages[i]), np.uint8)
+    d = torch.from_numpy(pages.reshape(-1)).to(cuda)
+    status, bad = PC.sqlite_verify_pages(d, 4096)
+    assert (status.cpu().numpy() == 2).all() and int(bad.cpu().numpy().view(np.uint64)[0]) == 0
+    s0, b0 = PC.sqlite_verify_pages(d, 4096, count=0)
+    assert s0.numel() == 0 and int(b0.cpu().numpy().view(np.uint64)[0]) == 0
