@@ -11,9 +11,13 @@ n = 1 << 20
 big = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
 F.fill_splitmix64(big, 0x5EED)
 out = torch.empty(n, dtype=torch.uint32, device=dev)
+out64 = torch.empty(n, dtype=torch.uint64, device=dev)
 torch.cuda.synchronize()
 for _ in range(5):
-    if mode == "pages4k":
+    if mode == "xxh3":
+        import foundationdb_amd.xxh3 as X
+        X.batch_fixed(big, 4096, 4088, n, out=out64)
+    elif mode == "pages4k":
         F.batch_fixed(big, 4096, 4096, n, out=out)
     elif mode == "stride0":
         F.batch_fixed(big, 0, 4096, n, out=out)

@@ -55,5 +55,10 @@ def main(mode="pages4k", workload="pages4k", kernel="k_pages4k", algorithmic=(1 
                                           "per_unit")}))
 
 
+PRESETS = {
+    "pages4k": ("pages4k", "pages4k", "k_pages4k", (1 << 20) * 4100, 1 << 20),
+    "xxh3": ("xxh3", "xxh3-pages4k", "k_xxh3_rows", (1 << 20) * (4088 + 8), 1 << 20),
+}
+
 if __name__ == "__main__":
-    main(*sys.argv[1:2])
+    main(*PRESETS[sys.argv[1] if len(sys.argv) > 1 else "pages4k"])
