@@ -153,6 +153,15 @@ __device__ __forceinline__ uint32_t word_step4(const uint32_t* lds, uint32_t x, 
 	return xor3(lds_rd(lds, a3), lds_rd(lds, a2 + 128), lds_rd(lds, a1)) ^ lds_rd(lds, a0 + 128);
 }
 
+// word_step4 with the next message word folded in: returns s' ^ next.
+__device__ __forceinline__ uint32_t word_step4_next(const uint32_t* lds, uint32_t x, uint32_t next, uint32_t c4) {
+	const uint32_t a3 = __builtin_amdgcn_perm(x, c4, 0x0c0c0400u);
+	const uint32_t a2 = __builtin_amdgcn_perm(x, c4, 0x0c0c0500u);
+	const uint32_t a1 = __builtin_amdgcn_perm(x, c4, 0x0c020600u);
+	const uint32_t a0 = __builtin_amdgcn_perm(x, c4, 0x0c020700u);
+	return xor3(xor3(lds_rd(lds, a3), lds_rd(lds + 32, a2), lds_rd(lds, a1)), lds_rd(lds + 32, a0), next);
+}
+
 __device__ __forceinline__ uint32_t feed16_b(const uint32_t* lds, uint32_t s, u32x4 w, uint32_t c4) {
 	s = word_step4(lds, s ^ w.x, c4);
 	s = word_step4(lds, s ^ w.y, c4);
@@ -166,9 +175,11 @@ __device__ __forceinline__ uint32_t feed16_b(const uint32_t* lds, uint32_t s, u3
 __device__ __forceinline__ uint32_t mul_nibbles(const uint32_t* lds, uint32_t s, uint32_t base) {
 	uint32_t r[8];
 #pragma unroll
-	for (int n = 0; n < 8; ++n) {
-		const uint32_t v = (s >> (4 * n)) & 15u;
-		r[n] = lds_rd(lds, ((v << 7) | base) + n * 2048);
+	for (int n = 0; n < 8; ++n) {  // nibble n of s at bits 7..10, table n at bits 11..13 (zero in base)
+		const uint32_t v = n == 0 ? (s << 7) : (4 * n >= 7 ? (s >> (4 * n - 7)) : (s << (7 - 4 * n)));
+		// (v & 0x780) | (base | n << 11) as one v_bitop3 (truth table 0xEA = (S0 & S1) | S2): written
+		// as a plain expression, LLVM turns the OR into an add against hoisted per-n constants
+		r[n] = lds_rd(lds, __builtin_amdgcn_bitop3_b32(v, 0x780u, base | ((uint32_t)n << 11), 0xEA));
 	}
 	return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }

@@ -148,10 +148,14 @@ __device__ __forceinline__ void unit_crc_b(const uint32_t* lds, int lane, uint32
 	uint32_t x[U];
 #pragma unroll
 	for (int j = 0; j < U; ++j) x[j] = (!WINDOW && lane == 0) ? ~s[j] : 0u;
+	// 16 word steps per chain; the next word is folded into the second XOR3
+	// (x' = T3 ^ T2 ^ T1 ^ T0 ^ w': two VALU XORs per word)
 #pragma unroll
-	for (int r = 0; r < 4; ++r)
+	for (int j = 0; j < U; ++j) x[j] ^= u[j].r[0][0];
 #pragma unroll
-		for (int j = 0; j < U; ++j) x[j] = feed16_b(lds, x[j], u[j].r[r], c4);
+	for (int w = 0; w < 16; ++w)
+#pragma unroll
+		for (int j = 0; j < U; ++j) x[j] = word_step4_next(lds, x[j], w < 15 ? u[j].r[(w + 1) >> 2][(w + 1) & 3] : 0u, c4);
 #pragma unroll
 	for (int j = 0; j < U; ++j) {
 		const uint32_t r = wave_xor(mul_nibbles(lds, x[j], c_lane));

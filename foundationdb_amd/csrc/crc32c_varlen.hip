@@ -457,6 +457,7 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 		}
 	};
 
+#if !(FDBCRC_EXP & 8)
 	// ======================= sweep 1: small pieces, four per pass ==========
 	// Load k (k = 0..3) fetches quarter qk = {0,2,1,3}[k] = 16-lane team qk
 	// after unswizzle; team t checksums piece t inside the 1 KiB window ending
@@ -547,6 +548,8 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 		}
 	}
 
+#endif
+#if !(FDBCRC_EXP & 16)
 	// ======================= sweep 2: large pieces, 4 KiB blocks ===========
 	// Blocks aligned to the piece's aligned end, taken two at a time (two
 	// register chains interleave, next two blocks in flight).  Each block's
@@ -643,7 +646,11 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 		uint32_t acc = 0;
 		auto fold = [&](const Blk& d, uint32_t v) {
 			if (!(d.flags & 1u)) return;
+#if FDBCRC_EXP & 2
+			acc = (d.flags & 2u) ? v : acc ^ v;
+#else
 			acc = (d.flags & 2u) ? v : umul(T->block, acc) ^ v;
+#endif
 			if (d.flags & 4u) deposit(d.slot, d.j, acc, 3u);
 			if (d.slot) s1.pending -= 1; else s0.pending -= 1;
 		};
@@ -680,6 +687,7 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 			b[1] = nb[1];
 		}
 	}
+#endif
 }
 
 // ---------------------------------------------------------------------------
