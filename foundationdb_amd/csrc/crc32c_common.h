@@ -15,14 +15,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------------------
 // LDS image (byte offsets).  Lane l always reads bank column l%32.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSliceOff = 0x00000;  // [256 idx][2 tab][32 col]         64 KiB
-constexpr uint32_t kBlockOff = 0x10000;  // [8 nib][16 v][32 col]            16 KiB  x^(8*4096)
-constexpr uint32_t kLaneOff = 0x14000;   // [2 half][8 nib][16 v][32 col]    32 KiB  x^(8*64*(63-l))
-constexpr uint32_t kLdsBytes = 0x1C000;  // 112 KiB -> one 1024-thread workgroup per CU
-constexpr uint32_t kTabT1 = 0;           // slice table: byte followed by one zero byte
-constexpr uint32_t kTabT0 = 128;         // slice table: single byte
-
-// Layout B (4 KiB page kernel only): 4-byte slicing, 160 KiB = all of LDS.
+// 4-byte slicing, 160 KiB = all of LDS:
 //   region 0 [idx][T3,T2][col], region 1 [idx][T1,T0][col], then lane tables.
 constexpr uint32_t kS4Off = 0x00000;     // 2 x 64 KiB
 constexpr uint32_t kS4LaneOff = 0x20000; // [2 half][8 nib][16 v][32 col]    32 KiB  x^(8*64*(63-l))
@@ -36,43 +29,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// Expand the compact tables into the bank-replicated LDS image.  Each thread
-// first issues all of its (independent) global loads, then writes: slice and
-// block-shift values go to all 32 bank columns, lane-combine values to the
-// one column (lane%32) of the lane they belong to.
-__device__ inline void fill_lds(uint32_t* lds, const DevTables* __restrict__ t) {
-	constexpr uint32_t kSlice = 512, kBlock = 128, kLane = 64 * 128;
-	constexpr uint32_t kCompact = kSlice + kBlock + kLane;  // 8832 words
-	constexpr uint32_t kPer = (kCompact + 1023) / 1024;
-	const uint32_t* src = reinterpret_cast<const uint32_t*>(t);
-	uint32_t v[kPer];
-#pragma unroll
-	for (uint32_t i = 0; i < kPer; ++i) {
-		const uint32_t q = threadIdx.x + i * blockDim.x;
-		v[i] = q < kCompact ? src[q] : 0u;
-	}
-#pragma unroll
-	for (uint32_t i = 0; i < kPer; ++i) {
-		const uint32_t q = threadIdx.x + i * blockDim.x;
-		if (q < kSlice) {  // slice[tab][idx] -> [idx][tab][col]
-			const uint32_t tab = q >> 8, idx = q & 255;
-			uint32_t* d = lds + (kSliceOff / 4) + (idx * 2 + tab) * 32;
-#pragma unroll
-			for (int c = 0; c < 32; ++c) d[c] = v[i];
-		} else if (q < kSlice + kBlock) {  // block[nib][v] -> [nib][v][col]
-			uint32_t* d = lds + (kBlockOff / 4) + (q - kSlice) * 32;
-#pragma unroll
-			for (int c = 0; c < 32; ++c) d[c] = v[i];
-		} else if (q < kCompact) {  // lane[l][nib][v] -> [l/32][nib][v][l%32]
-			const uint32_t r = q - kSlice - kBlock;
-			const uint32_t l = r >> 7, nv = r & 127;
-			lds[(kLaneOff / 4) + (l >> 5) * 4096 + nv * 32 + (l & 31)] = v[i];
-		}
-	}
-	__syncthreads();
-}
-
-// Layout B fill: slice4 (1024 words) to all 32 columns, lane tables to their column.
+// LDS fill: slice4 (1024 words) to all 32 columns, lane tables to their column.
 __device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t) {
 	constexpr uint32_t kSlice = 1024, kLane = 64 * 128;
 	constexpr uint32_t kCompact = kSlice + kLane;  // 9216 words
@@ -103,9 +60,6 @@ __device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t
 }
 
 struct LaneCtx {
-	uint32_t c_slice;  // col*4
-	uint32_t c_block;  // kBlockOff | col*4
-	uint32_t c_lane;   // kLaneOff + half*16 KiB | col*4
 	uint32_t ld_off;   // byte offset of this lane's first 16 B load inside a block
 	int lane;
 };
@@ -113,10 +67,6 @@ struct LaneCtx {
 __device__ __forceinline__ LaneCtx make_ctx() {
 	LaneCtx c;
 	c.lane = threadIdx.x & 63;
-	const uint32_t col4 = (c.lane & 31) * 4;
-	c.c_slice = kSliceOff | col4;
-	c.c_block = kBlockOff | col4;
-	c.c_lane = (kLaneOff + (c.lane >> 5) * 0x4000) | col4;
 	// lane m = 32h + 16q + r loads, for load k = 2kb + ka, the 16 bytes at
 	//   2048*ka + 1024*kb + 64r + 32q + 16h
 	// which after the swap network (unswizzle) puts block bytes
@@ -126,24 +76,7 @@ __device__ __forceinline__ LaneCtx make_ctx() {
 	return c;
 }
 
-// Two bytes of register update: x already holds (register ^ data).
-//   x' = (x >> 16) ^ T1[x.b0] ^ T0[x.b1]
-__device__ __forceinline__ uint32_t half_step(const uint32_t* lds, uint32_t x, uint32_t c_slice) {
-	const uint32_t a0 = __builtin_amdgcn_perm(x, c_slice, 0x0c0c0400u);  // (x.b0 << 8) | col*4
-	const uint32_t a1 = __builtin_amdgcn_perm(x, c_slice, 0x0c0c0500u);  // (x.b1 << 8) | col*4
-	return xor3(x >> 16, lds_rd(lds, a0 + kTabT1), lds_rd(lds, a1 + kTabT0));
-}
-
-// Feed 16 bytes into register s.
-__device__ __forceinline__ uint32_t feed16(const uint32_t* lds, uint32_t s, u32x4 w, uint32_t c_slice) {
-	s = half_step(lds, half_step(lds, s ^ w.x, c_slice), c_slice);
-	s = half_step(lds, half_step(lds, s ^ w.y, c_slice), c_slice);
-	s = half_step(lds, half_step(lds, s ^ w.z, c_slice), c_slice);
-	s = half_step(lds, half_step(lds, s ^ w.w, c_slice), c_slice);
-	return s;
-}
-
-// Layout B: four bytes per step, s' = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3]
+// Four bytes per step, s' = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3]
 // with x = s ^ word.  c4 = col*4 | 0x10000 (byte 2 selects region 1).
 __device__ __forceinline__ uint32_t word_step4(const uint32_t* lds, uint32_t x, uint32_t c4) {
 	const uint32_t a3 = __builtin_amdgcn_perm(x, c4, 0x0c0c0400u);  // (x.b0 << 8) | col*4
@@ -160,14 +93,6 @@ __device__ __forceinline__ uint32_t word_step4_next(const uint32_t* lds, uint32_
 	const uint32_t a1 = __builtin_amdgcn_perm(x, c4, 0x0c020600u);
 	const uint32_t a0 = __builtin_amdgcn_perm(x, c4, 0x0c020700u);
 	return xor3(xor3(lds_rd(lds, a3), lds_rd(lds + 32, a2), lds_rd(lds, a1)), lds_rd(lds + 32, a0), next);
-}
-
-__device__ __forceinline__ uint32_t feed16_b(const uint32_t* lds, uint32_t s, u32x4 w, uint32_t c4) {
-	s = word_step4(lds, s ^ w.x, c4);
-	s = word_step4(lds, s ^ w.y, c4);
-	s = word_step4(lds, s ^ w.z, c4);
-	s = word_step4(lds, s ^ w.w, c4);
-	return s;
 }
 
 // Multiply a register by the constant whose nibble tables start at `base`
@@ -314,27 +239,6 @@ __device__ __forceinline__ void unswizzle(Block& b) {
 	swap32(b.r[2], b.r[3]);
 	swap16(b.r[0], b.r[2]);
 	swap16(b.r[1], b.r[3]);
-}
-
-// Register of this lane after its 64 bytes, starting from s.
-__device__ __forceinline__ uint32_t chain64(const uint32_t* lds, uint32_t s, const Block& b, uint32_t c_slice) {
-	s = feed16(lds, s, b.r[0], c_slice);
-	s = feed16(lds, s, b.r[1], c_slice);
-	s = feed16(lds, s, b.r[2], c_slice);
-	s = feed16(lds, s, b.r[3], c_slice);
-	return s;
-}
-
-
-// Byte-serial register update (tiny pieces), wave-uniform.
-__device__ __forceinline__ uint32_t byte_step(const uint32_t* lds, uint32_t s, uint32_t b, uint32_t c_slice) {
-	const uint32_t a = __builtin_amdgcn_perm(s ^ b, c_slice, 0x0c0c0400u);
-	return (s >> 8) ^ lds_rd(lds, a + kTabT0);
-}
-
-__device__ inline uint32_t feed_bytes(const uint32_t* lds, uint32_t s, const uint8_t* p, const uint8_t* e, uint32_t c_slice) {
-	for (; p < e; ++p) s = byte_step(lds, s, ld1(p), c_slice);
-	return s;
 }
 
 }  // namespace fdbcrc

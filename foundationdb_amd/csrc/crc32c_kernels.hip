@@ -13,12 +13,13 @@
 //     two v_permlane32_swap + two v_permlane16_swap rounds (16 VALU per
 //     block) leave lane l holding the 64 CONTIGUOUS bytes [64l, 64l+64) of
 //     the block in registers.
-//   * Each lane runs one CRC register over its 64 bytes (2-byte slicing from
-//     bank-replicated LDS tables: every ds_read_b32 is conflict-free).
+//   * Each lane runs one CRC register over its 64 bytes (4-byte slicing from
+//     bank-replicated LDS tables -- every ds_read_b32 is conflict-free -- the
+//     next message word folded into each step's second XOR3).
 //   * Lane l then multiplies its register by x^(8*64*(63-l)) -- its distance
 //     to the end of the block -- and the 64 registers are xor-reduced across
-//     the wave (DPP row reduction + 4 readlanes).  Consecutive blocks of one
-//     buffer fold Horner-style with x^(8*4096).  This is append_hw's stream
+//     the wave (DPP row reduction + 4 readlanes).  Two blocks of one buffer
+//     combine with x^(8*4096) (8 KiB pages).  This is append_hw's stream
 //     merge (crc32c.cpp:268-269) with GPU-shaped distances.
 //   * Seed: the register at the buffer's first byte is ~seed, as in
 //     append_hw's pre-inversion (crc32c.cpp:197); the result is post-inverted
@@ -31,93 +32,7 @@
 
 namespace fdbcrc {
 
-// ---------------------------------------------------------------------------
-// Fixed-stride pages of NB*4 KiB (16-byte aligned base and stride).
-// Every wave owns a contiguous run of pages and works on UNIT = 2 blocks at a
-// time (two 4 KiB pages, or one 8 KiB page) while the next unit's loads are
-// in flight.  The two blocks' register chains interleave (ILP 2).  Control
-// flow is scalar (readfirstlane'd wave id); seeds arrive as one vector load
-// per 64 pages, checksums leave as one coalesced store per 64 pages.
-// ---------------------------------------------------------------------------
-template <int NB>  // 4 KiB blocks per page: 1 or 2
-__device__ __forceinline__ void unit_crc(const uint32_t* lds, const LaneCtx& c, Block (&u)[2], uint32_t sa,
-                                         uint32_t sb, uint32_t& ca, uint32_t& cb) {
-	unswizzle(u[0]);
-	unswizzle(u[1]);
-	if (NB == 1) {  // two pages
-		const uint32_t x0 = chain64(lds, c.lane == 0 ? ~sa : 0u, u[0], c.c_slice);
-		const uint32_t x1 = chain64(lds, c.lane == 0 ? ~sb : 0u, u[1], c.c_slice);
-		ca = ~wave_xor(mul_nibbles(lds, x0, c.c_lane));
-		cb = ~wave_xor(mul_nibbles(lds, x1, c.c_lane));
-	} else {  // one 8 KiB page
-		const uint32_t x0 = chain64(lds, c.lane == 0 ? ~sa : 0u, u[0], c.c_slice);
-		const uint32_t x1 = chain64(lds, 0u, u[1], c.c_slice);
-		const uint32_t acc = mul_nibbles(lds, x0, c.c_block) ^ x1;
-		ca = ~wave_xor(mul_nibbles(lds, acc, c.c_lane));
-		cb = ca;
-	}
-}
-
-template <int NB>
-__device__ __forceinline__ void load_unit(Block (&u)[2], const uint8_t* p0, const uint8_t* p1, uint32_t ld_off) {
-	if (NB == 1) {
-		load_block(u[0], p0, ld_off);
-		load_block(u[1], p1, ld_off);
-	} else {
-		load_block(u[0], p0, ld_off);
-		load_block(u[1], p0 + 4096, ld_off);
-	}
-}
-
-template <int NB>
-__global__ __launch_bounds__(1024) void k_pages(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
-                                                uint32_t seed, const uint32_t* __restrict__ seeds,
-                                                uint32_t* __restrict__ out, const DevTables* __restrict__ tabs) {
-	__shared__ uint32_t lds[kLdsBytes / 4];
-	constexpr uint64_t PPU = NB == 1 ? 2 : 1;  // pages per unit
-	const LaneCtx c = make_ctx();
-	const uint64_t wpb = blockDim.x >> 6;
-	const uint64_t wave = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
-	const uint64_t waves = (uint64_t)gridDim.x * wpb;
-	uint64_t per = (count + waves - 1) / waves;
-	per = per > 64 ? (per + 63) & ~uint64_t(63) : (per + PPU - 1) / PPU * PPU;
-	const uint64_t begin = wave * per;
-	const uint64_t end = begin + per < count ? begin + per : count;
-	const uint64_t last = end ? end - 1 : 0;
-	// page index -> address, clamped into this wave's run (clamped duplicates
-	// are computed and discarded, so every load is consumed unconditionally)
-	auto page = [&](uint64_t i) { return base + (i < end ? i : (begin < end ? last : 0)) * stride; };
-	Block u0[2], u1[2];
-	load_unit<NB>(u0, page(begin), page(begin + 1), c.ld_off);  // in flight during the LDS fill
-	fill_lds(lds, tabs);
-	if (begin >= end) return;
-	for (uint64_t first = begin; first < end; first += 64) {
-		const uint64_t n = end - first < 64 ? end - first : 64;
-		const uint32_t my_seed = seeds ? seeds[first + ((uint64_t)c.lane < n ? c.lane : 0)] : seed;
-		uint32_t mine = 0;  // lane k keeps the checksum of page first+k
-		for (uint64_t k = 0; k < n; k += 2 * PPU) {
-			uint32_t ca, cb;
-			load_unit<NB>(u1, page(first + k + PPU), page(first + k + PPU + 1), c.ld_off);
-			__builtin_amdgcn_sched_barrier(0);
-			unit_crc<NB>(lds, c, u0, rdlane(my_seed, (int)k),
-			             rdlane(my_seed, (int)(k + 1) & 63), ca, cb);
-			mine = (uint64_t)c.lane == k ? ca : mine;
-			if (PPU == 2) mine = (uint64_t)c.lane == k + 1 ? cb : mine;
-			__builtin_amdgcn_sched_barrier(0);
-			load_unit<NB>(u0, page(first + k + 2 * PPU), page(first + k + 2 * PPU + 1), c.ld_off);
-			__builtin_amdgcn_sched_barrier(0);
-			unit_crc<NB>(lds, c, u1, rdlane(my_seed, (int)(k + PPU) & 63),
-			             rdlane(my_seed, (int)(k + PPU + 1) & 63), ca, cb);
-			mine = (uint64_t)c.lane == k + PPU ? ca : mine;
-			if (PPU == 2) mine = (uint64_t)c.lane == k + PPU + 1 ? cb : mine;
-			__builtin_amdgcn_sched_barrier(0);
-		}
-		if ((uint64_t)c.lane < n) out[first + c.lane] = mine;
-	}
-}
-
-// 4 KiB pages with the layout-B image (4-byte slicing: half the dependent
-// LDS round trips and a third less VALU than layout A).
+// 4 KiB pages (160 KiB LDS image, 4-byte slicing).
 // U pages per unit: U independent register chains interleave (ILP U) while
 // the next unit's U pages are in flight.  Groups of G = 2U*floor(64/2U) pages
 // share one seed vector load and one coalesced checksum store.
@@ -126,7 +41,7 @@ __global__ __launch_bounds__(1024) void k_pages(const uint8_t* __restrict__ base
 // gets the seed register at byte h (lane 32's chunk 16..31 takes the bytes
 // spilling past 16), lane 63's last chunk (4080..4095) is masked from 16 - t;
 // the t zero bytes are removed from the raw register when the group is stored.
-template <int U, bool WINDOW>
+template <int U, bool WINDOW, bool RAW = WINDOW>
 __device__ __forceinline__ void unit_crc_b(const uint32_t* lds, int lane, uint32_t c4, uint32_t c_lane,
                                            Block (&u)[U], const uint32_t (&s)[U], uint32_t (&crc)[U],
                                            uint32_t h, uint32_t t) {
@@ -159,7 +74,7 @@ __device__ __forceinline__ void unit_crc_b(const uint32_t* lds, int lane, uint32
 #pragma unroll
 	for (int j = 0; j < U; ++j) {
 		const uint32_t r = wave_xor(mul_nibbles(lds, x[j], c_lane));
-		crc[j] = WINDOW ? r : ~r;  // WINDOW: raw register, finished at the store
+		crc[j] = RAW ? r : ~r;  // raw register (WINDOW, PAIR): finished at the store
 	}
 }
 
@@ -176,7 +91,11 @@ __device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t
 
 // LIST: page i of the batch is page idx[i] of `base` and the batch size is
 // read from *d_count (device-side compaction output, pagecheck.hip).
-template <int U, bool WINDOW = false, bool LIST = false>
+// PAIR: 8 KiB pages as pairs of 4 KiB blocks (block 2i+h = half h of page
+// i): the seed enters the first half, and at the group store lane 2m
+// combines raw(A)*x^(8*4096) ^ raw(B) with its neighbour (DPP lane swap +
+// one lane-parallel table multiply).
+template <int U, bool WINDOW = false, bool LIST = false, bool PAIR = false>
 __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
                                                   uint32_t seed, const uint32_t* __restrict__ seeds,
                                                   uint32_t* __restrict__ out, const DevTables* __restrict__ tabs,
@@ -187,6 +106,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		count = *d_count;
 		if (count == 0) return;  // the list is empty: idx[] holds nothing to read
 	}
+	if (PAIR) count *= 2;  // blocks
 	constexpr uint64_t G = 2 * U * (64 / (2 * U));  // a whole number of loop iterations
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const LaneCtx c = make_ctx();
@@ -205,6 +125,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 	// are computed and discarded, so every load is consumed unconditionally
 	auto page = [&](uint64_t i) {
 		const uint64_t j = i < end ? i : (begin < end ? last : 0);
+		if (PAIR) return base + (j >> 1) * stride + (j & 1) * 4096;
 		return base + (LIST ? (uint64_t)idx[j] : j) * stride;
 	};
 	auto load_u = [&](Block (&u)[U], uint64_t i0) {
@@ -217,7 +138,11 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 	if (begin >= end) return;
 	for (uint64_t first = begin; first < end; first += G) {
 		const uint64_t n = end - first < G ? end - first : G;
-		const uint32_t my_seed = seeds ? seeds[first + ((uint64_t)c.lane < n ? c.lane : 0)] : seed;
+		// PAIR: block first+k is half k&1 of page (first+k)/2; odd blocks carry no seed (~0 -> 0)
+		const uint64_t sp = PAIR ? (first >> 1) + ((uint64_t)c.lane < n ? (uint64_t)c.lane >> 1 : 0)
+		                         : first + ((uint64_t)c.lane < n ? c.lane : 0);
+		uint32_t my_seed = seeds ? seeds[sp] : seed;
+		if (PAIR && (c.lane & 1)) my_seed = ~0u;
 		uint32_t mine = 0;  // lane k keeps the checksum of page first+k
 		for (uint64_t k = 0; k < n; k += 2 * U) {
 			uint32_t sd[U], crc[U];
@@ -225,7 +150,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 			__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + j) & 63);
-			unit_crc_b<U, WINDOW>(lds, c.lane, c4, c_lane, u0, sd, crc, h, t);
+			unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u0, sd, crc, h, t);
 #pragma unroll
 			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + j ? crc[j] : mine;
 			__builtin_amdgcn_sched_barrier(0);
@@ -233,13 +158,19 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 			__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + U + j) & 63);
-			unit_crc_b<U, WINDOW>(lds, c.lane, c4, c_lane, u1, sd, crc, h, t);
+			unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u1, sd, crc, h, t);
 #pragma unroll
 			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + U + j ? crc[j] : mine;
 			__builtin_amdgcn_sched_barrier(0);
 		}
 		if (WINDOW) mine = ~(t ? vmul_tab(tabs->inv_z[t], mine) : mine);
-		if ((uint64_t)c.lane < n) out[first + c.lane] = mine;
+		if (PAIR) {
+			const uint32_t other = __builtin_amdgcn_update_dpp(0u, mine, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+			mine = ~(vmul_tab(tabs->block, mine) ^ other);
+			if ((uint64_t)c.lane < n && !(c.lane & 1)) out[(first >> 1) + (c.lane >> 1)] = mine;
+		} else if ((uint64_t)c.lane < n) {
+			out[first + c.lane] = mine;
+		}
 	}
 }
 
@@ -255,7 +186,14 @@ int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint
 	if (grid == 0) grid = 1;
 	switch (blocks_per_page) {
 		case 1: k_pages4k<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
-		case 2: k_pages<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
+		case 2: {  // 8 KiB pages as block pairs on the 4 KiB kernel
+			uint64_t g2 = (2 * units + 15) / 16;
+			if (g2 > (uint64_t)num_cus) g2 = num_cus;
+			if (g2 == 0) g2 = 1;
+			k_pages4k<2, false, false, true><<<(unsigned)g2, threads, 0, stream>>>(base, stride, count, seed, seeds, out,
+			                                                                      tabs);
+			break;
+		}
 		default: return -1;
 	}
 	return 0;

@@ -245,13 +245,24 @@ __device__ __forceinline__ u32x4 load_chunk_if(uint64_t ca, const Piece& p) {
 	return ok ? ld16(reinterpret_cast<const uint8_t*>(ca)) : u32x4{0u, 0u, 0u, 0u};
 }
 
-// Register chain over the lane's 64 contiguous bytes (layout B, 4-byte slicing).
+// Register chain over the lane's 64 contiguous bytes (layout B, 4-byte
+// slicing), each step folding in the next word (word_step4_next).
 __device__ __forceinline__ uint32_t chain64_b(const uint32_t* lds, uint32_t s, const Block& b, uint32_t c4) {
-	s = feed16_b(lds, s, b.r[0], c4);
-	s = feed16_b(lds, s, b.r[1], c4);
-	s = feed16_b(lds, s, b.r[2], c4);
-	s = feed16_b(lds, s, b.r[3], c4);
+	s ^= b.r[0][0];
+#pragma unroll
+	for (int w = 0; w < 16; ++w) s = word_step4_next(lds, s, w < 15 ? b.r[(w + 1) >> 2][(w + 1) & 3] : 0u, c4);
 	return s;
+}
+// Two independent chains interleaved (ILP 2).
+__device__ __forceinline__ void chain64_b2(const uint32_t* lds, const Block& b0, const Block& b1, uint32_t c4,
+                                           uint32_t& y0, uint32_t& y1) {
+	y0 = b0.r[0][0];
+	y1 = b1.r[0][0];
+#pragma unroll
+	for (int w = 0; w < 16; ++w) {
+		y0 = word_step4_next(lds, y0, w < 15 ? b0.r[(w + 1) >> 2][(w + 1) & 3] : 0u, c4);
+		y1 = word_step4_next(lds, y1, w < 15 ? b1.r[(w + 1) >> 2][(w + 1) & 3] : 0u, c4);
+	}
 }
 
 // ---------------------------------------------------------------------------
@@ -667,12 +678,8 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 				edges(b[1], cur[1]);
 				unswizzle(b[0]);
 				unswizzle(b[1]);
-				uint32_t y0 = 0u, y1 = 0u;
-#pragma unroll
-				for (int r = 0; r < 4; ++r) {
-					y0 = feed16_b(lds, y0, b[0].r[r], c4);
-					y1 = feed16_b(lds, y1, b[1].r[r], c4);
-				}
+				uint32_t y0, y1;
+				chain64_b2(lds, b[0], b[1], c4, y0, y1);
 				const uint32_t v0 = wave_xor(mul_nibbles(lds, y0, c_lane));
 				const uint32_t v1 = wave_xor(mul_nibbles(lds, y1, c_lane));
 				fold(cur[0], v0);
