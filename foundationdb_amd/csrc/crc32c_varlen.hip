@@ -164,12 +164,17 @@ __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, ui
 // ---------------------------------------------------------------------------
 // Uniform (wave-wide) multiply through nibble tables in global memory: the
 // value is uniform, so these are scalar-cache loads, off the LDS path.
+// The table is read through the constant address space with a uniform
+// index, so these are s_load (lgkmcnt): as vector loads they would share the
+// in-order vmcnt with the data prefetch and every multiply would wait for it.
 __device__ __forceinline__ uint32_t umul(const uint32_t (*tab)[16], uint32_t v) {
+	typedef __attribute__((address_space(4))) const uint32_t c_u32;
+	const c_u32* t = (const c_u32*)reinterpret_cast<uintptr_t>(&tab[0][0]);
 	v = rdfirst(v);
 	uint32_t r = 0;
 #pragma unroll
-	for (int n = 0; n < 8; ++n) r ^= tab[n][(v >> (4 * n)) & 15u];
-	return r;
+	for (int n = 0; n < 8; ++n) r ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
+	return rdfirst(r);
 }
 
 // Uniform value times x^(8d), d >= 0: one table multiply per set bit of d.

@@ -12,9 +12,20 @@ big = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
 F.fill_splitmix64(big, 0x5EED)
 out = torch.empty(n, dtype=torch.uint32, device=dev)
 out64 = torch.empty(n, dtype=torch.uint64, device=dev)
+if mode in ("chunks", "zipf"):
+    import numpy as np
+    import bench_workloads as W
+    lens = (W.chunk_lengths() if mode == "chunks" else W.zipf_lengths()).astype(np.int64)
+    al = 4096 if mode == "chunks" else 256
+    padded = (lens + al - 1) // al * al
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(padded)[:-1]])).to(dev)
+    lt = torch.from_numpy(lens).to(dev)
+    vout = torch.empty(lens.size, dtype=torch.uint32, device=dev)
 torch.cuda.synchronize()
 for _ in range(5):
-    if mode == "xxh3":
+    if mode in ("chunks", "zipf"):
+        F.batch_varlen(big, offs, lt, out=vout)
+    elif mode == "xxh3":
         import foundationdb_amd.xxh3 as X
         X.batch_fixed(big, 4096, 4088, n, out=out64)
     elif mode == "pages4k":
