@@ -75,7 +75,7 @@ class Pages:
 
     def __init__(self, dev, rank, page_bytes=4096, count=1 << 20, seed=0):
         self.dev, self.page_bytes, self.count, self.seed = dev, page_bytes, count, seed
-        self.kernel_name = "fdbcrc::k_pages4k" if page_bytes == 4096 else "fdbcrc::k_pages<2>"
+        self.kernel_name = "fdbcrc::k_pages4k<2>" if page_bytes == 4096 else "fdbcrc::k_pages4k<2, PAIR> (8 KiB pages as block pairs)"
         self.buf = torch.empty(count * page_bytes, dtype=torch.uint8, device=dev)
         F.fill_splitmix64(self.buf, STATE)
         self.out = torch.empty(count, dtype=torch.uint32, device=dev)
@@ -124,7 +124,7 @@ def _spot_check(buf, offsets, lengths, seed, got, n=512):
 
 
 class VarLen:
-    kernel_name = "fdbcrc::k_general"
+    kernel_name = "fdbcrc::k_varlen (+ k_plan, k_scan)"
 
     def __init__(self, dev, rank, lengths, align, desc, seed=0):
         self.dev, self.seed = dev, seed
