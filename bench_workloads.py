@@ -239,6 +239,51 @@ class HostChunks:
                          offsets=self.h_offsets[:k].copy(), lengths=self.h_lengths[:k].copy(), seed=self.seed)
 
 
+class HostPages(HostChunks):
+    """configs[1] shape, host-to-host: 1 Mi x 4 KiB pages in pinned host memory
+    (pages as read from disk), checksummed through the pinned H2D -> page kernel
+    -> D2H pipeline (4 streams, 64 MiB segments).  PCIe-bound by design; the
+    device-resident rate of the same batch is the `pages4k` workload."""
+    kernel_name = "host pipeline (H2D + fdbcrc::k_pages4k + D2H)"
+
+    def __init__(self, dev, rank, count=1 << 20, seed=0):
+        self.count, self.seed = count, seed
+        self.buf = torch.empty(count * 4096, dtype=torch.uint8).pin_memory()
+        dbuf = torch.empty(count * 4096, dtype=torch.uint8, device=dev)
+        F.fill_splitmix64(dbuf, STATE)
+        self.buf.copy_(dbuf)
+        del dbuf
+        self.out = torch.empty(count, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
+        self.pipe = F.Pipeline(segment_bytes=64 << 20, nstreams=4)
+        self.bytes_per_step = count * 4096
+        self.algorithmic_bytes_per_step = count * 4100
+        self.data_desc = (f"synthetic: splitmix64 stream (state 0x{STATE:X}) in PINNED HOST memory; "
+                          f"{count} x 4096 B pages, host-to-host")
+        self.config = {"workload": f"{count} x 4 KiB pages, host-resident, pinned H2D/D2H overlapped "
+                                   "(4 streams x 64 MiB segments)", "buffers": count,
+                       "total_bytes": self.bytes_per_step, "seed": seed}
+
+    def step(self, stream):
+        self.pipe.fixed(self.buf, 4096, 4096, self.count, seed=self.seed, out=self.out)
+
+    def verify(self):
+        got = self.out
+        if self.count == 1 << 20:
+            d = [d for d in _golden()["pages_full"]["digests"] if d["seed"] == self.seed][0]
+            return int(np.bitwise_xor.reduce(got)) == d["xor"] and int(got.astype(np.uint64).sum()) == d["sum"]
+        host = self.buf.numpy()
+        rng = np.random.default_rng(0)
+        return all(F.crc32c_append(self.seed, host[i * 4096:(i + 1) * 4096]) == int(got[i])
+                   for i in rng.choice(self.count, size=256, replace=False))
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        n = 65536
+        buf = self.buf.numpy()[:n * 4096]
+        return CpuSample(f"first {n} x 4096 B pages of the same batch", n * 4096, buf, stride=4096, length=4096,
+                         count=n, seed=self.seed)
+
+
 class DryCpuPages:
     """--dry-cpu: exercises bench.py's multi-rank harness on CPU with the
     library's host crc32c_append over a small page batch.  Not a measurement."""
@@ -311,5 +356,6 @@ WORKLOADS = {
     "chunks": lambda dev, rank: VarLen(dev, rank, chunk_lengths(), 4096,
                                        "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch"),
     "chunks-host": lambda dev, rank: HostChunks(dev, rank),
+    "pages4k-host": lambda dev, rank: HostPages(dev, rank),
     "xxh3-pages4k": lambda dev, rank: Xxh3Pages(dev, rank),
 }

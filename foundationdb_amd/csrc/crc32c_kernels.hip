@@ -30,6 +30,13 @@
 
 #include "crc32c_common.h"
 
+#ifndef FDBCRC_PDEPTH
+#define FDBCRC_PDEPTH 2  // pages in flight per wave, in units of U (development experiments)
+#endif
+#ifndef FDBCRC_PU
+#define FDBCRC_PU 2  // pages per unit (register chains interleaved per wave)
+#endif
+
 namespace fdbcrc {
 
 // 4 KiB pages (160 KiB LDS image, 4-byte slicing).
@@ -132,6 +139,38 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 #pragma unroll
 		for (int j = 0; j < U; ++j) load_block(u[j], page(i0 + j), c.ld_off);
 	};
+if constexpr (FDBCRC_PDEPTH == 3 && !WINDOW && !LIST && !PAIR) {
+	Block u0[U], u1[U], u2[U];
+	load_u(u0, begin);  // in flight during the LDS fill
+	load_u(u1, begin + U);
+	fill_lds_b(lds, tabs);
+	if (begin >= end) return;
+	constexpr uint64_t G3 = 3 * U * (63 / (3 * U));
+	for (uint64_t first = begin; first < end; first += G3) {
+		const uint64_t n = end - first < G3 ? end - first : G3;
+		const uint64_t sp = first + ((uint64_t)c.lane < n ? c.lane : 0);
+		const uint32_t my_seed = seeds ? seeds[sp] : seed;
+		uint32_t mine = 0;
+		auto phase = [&](Block (&cu)[U], Block (&ld)[U], uint64_t kc, uint64_t kl) {
+			uint32_t sd[U], crc[U];
+			load_u(ld, first + kl);
+			__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(kc + j) & 63);
+			unit_crc_b<U, false, false>(lds, c.lane, c4, c_lane, cu, sd, crc, h, t);
+#pragma unroll
+			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == kc + j ? crc[j] : mine;
+			__builtin_amdgcn_sched_barrier(0);
+		};
+		for (uint64_t k = 0; k < n; k += 3 * U) {
+			phase(u0, u2, k, k + 2 * U);
+			phase(u1, u0, k + U, k + 3 * U);
+			phase(u2, u1, k + 2 * U, k + 4 * U);
+		}
+		if ((uint64_t)c.lane < n) out[first + c.lane] = mine;
+	}
+	return;
+	}
 	Block u0[U], u1[U];
 	load_u(u0, begin);  // in flight during the LDS fill
 	fill_lds_b(lds, tabs);
@@ -185,7 +224,7 @@ int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint
 	if (grid > (uint64_t)num_cus) grid = num_cus;
 	if (grid == 0) grid = 1;
 	switch (blocks_per_page) {
-		case 1: k_pages4k<2><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
+		case 1: k_pages4k<FDBCRC_PU><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
 		case 2: {  // 8 KiB pages as block pairs on the 4 KiB kernel
 			uint64_t g2 = (2 * units + 15) / 16;
 			if (g2 > (uint64_t)num_cus) g2 = num_cus;

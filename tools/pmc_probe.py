@@ -12,18 +12,20 @@ big = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
 F.fill_splitmix64(big, 0x5EED)
 out = torch.empty(n, dtype=torch.uint32, device=dev)
 out64 = torch.empty(n, dtype=torch.uint64, device=dev)
-if mode in ("chunks", "zipf"):
+VARLEN = ("chunks", "zipf", "v4096", "v1024")
+if mode in VARLEN:
     import numpy as np
     import bench_workloads as W
-    lens = (W.chunk_lengths() if mode == "chunks" else W.zipf_lengths()).astype(np.int64)
-    al = 4096 if mode == "chunks" else 256
+    lens = {"chunks": W.chunk_lengths, "zipf": W.zipf_lengths, "v4096": lambda: np.full(1 << 18, 4096),
+            "v1024": lambda: np.full(1 << 20, 1024)}[mode]().astype(np.int64)
+    al = {"chunks": 4096, "zipf": 256, "v4096": 4096, "v1024": 1024}[mode]
     padded = (lens + al - 1) // al * al
     offs = torch.from_numpy(np.concatenate([[0], np.cumsum(padded)[:-1]])).to(dev)
     lt = torch.from_numpy(lens).to(dev)
     vout = torch.empty(lens.size, dtype=torch.uint32, device=dev)
 torch.cuda.synchronize()
 for _ in range(5):
-    if mode in ("chunks", "zipf"):
+    if mode in VARLEN:
         F.batch_varlen(big, offs, lt, out=vout)
     elif mode == "xxh3":
         import foundationdb_amd.xxh3 as X
