@@ -14,6 +14,11 @@ struct DevTables {
 	uint32_t inv_z[16][8][16];  // nibble tables of x^(-8z), z = 0..15: drop z trailing zero bytes
 	uint32_t pow2[64][8][16];   // nibble tables of x^(8*2^m): shift by arbitrary byte counts
 	uint32_t corr[4][16][8][16];  // x^(-8(z + 1024(3-t))): quarter t's team value -> piece register, minus z zeros
+	// varlen v7 (1 KiB window slots, 64 slots per table)
+	uint32_t x4pow[16][8][16];       // x^(8*4096*i): slot sums of pass i -> weight x^(8*1024*(63-slot))
+	uint32_t table_shift[8][16];     // x^(8*65536): a piece's register carried across a 64-slot table
+	uint32_t normk[64][16][8][16];   // x^(-8*(1024*(63-k) + z)): piece ending at slot k, z trailing zeros
+	uint32_t chunkpow[256][8][16];   // x^(8*16*(255-c)): 16-byte chunk c of a pass block to the block's end
 };
 
 // Build the tables on the host (crc32c_tables.cpp).
@@ -35,6 +40,11 @@ int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
                          const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus,
                          hipStream_t stream);
+// v7 workspace and launch (ws: varlen7_workspace_bytes(count, nwave), 16-byte aligned)
+uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave);
+int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
+                   uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
+                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream);
 int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out, hipStream_t stream);
 
 }  // namespace fdbcrc

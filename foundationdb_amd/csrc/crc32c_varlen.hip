@@ -33,6 +33,9 @@
 
 #include "crc32c_common.h"
 
+#ifndef FDBCRC_V7
+#define FDBCRC_V7 1  // varlen batches: 1 = v7 (prep + window-slot streaming), 0 = v4 (two sweeps)
+#endif
 #ifndef FDBCRC_EXP
 #define FDBCRC_EXP 0  // development timing experiments only (wrong results when set)
 #endif
@@ -77,9 +80,11 @@ __global__ __launch_bounds__(256) void k_plan(const uint64_t* __restrict__ lengt
 }
 
 // Single workgroup.  ntile tiles, nwave waves in the main grid.
+// quantum: ceil(total / nwave), at least qmin, rounded up to a multiple of qalign
 __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, uint64_t ntile,
                                                uint32_t* __restrict__ wave_tile, uint64_t nwave,
-                                               uint64_t* __restrict__ hdr) {
+                                               uint64_t* __restrict__ hdr, uint64_t qmin = 4096,
+                                               uint64_t qalign = 64) {
 	constexpr uint32_t C = 8192;  // tiles per LDS chunk
 	__shared__ uint64_t buf[C];
 	__shared__ uint64_t wsum[16];
@@ -94,7 +99,7 @@ __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, ui
 	uint64_t total = 0;
 	for (int k = 0; k < 16; ++k) total += wsum[k];
 	uint64_t q = (total + nwave - 1) / nwave;
-	q = q < 4096 ? 4096 : (q + 63) & ~uint64_t(63);
+	q = q < qmin ? qmin : (q + qalign - 1) / qalign * qalign;
 	__syncthreads();
 	if (t == 0) carry_s = 0;
 	__syncthreads();
@@ -308,6 +313,10 @@ __device__ __forceinline__ uint64_t scan64(uint64_t v, int lane) {
 __device__ __forceinline__ uint32_t gld32(const uint32_t* p) {
 	typedef __attribute__((address_space(1))) const uint32_t g_u32;
 	return *((g_u32*)reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ uint64_t gld64(const uint64_t* p) {
+	typedef __attribute__((address_space(1))) const uint64_t g_u64;
+	return *((g_u64*)reinterpret_cast<uintptr_t>(p));
 }
 
 // Lane-parallel multiply by the per-lane constant whose nibble tables start
@@ -703,16 +712,538 @@ __global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables
 }
 
 // ---------------------------------------------------------------------------
+// v7: window slots, prepared per buffer, streamed per wave
+// ---------------------------------------------------------------------------
+// Every buffer of >= 16 bytes is cut into W = ceil((E - A) / 1024) windows of
+// 1 KiB ALIGNED TO ITS END E = ceil16(P1) (A = P0 & ~15): window m covers
+// [E - 1024(W-m), E - 1024(W-m-1)); window 0 starts lo = 1024W - (E - A)
+// bytes before A, and those leading bytes are not loaded (leading zeros are
+// free).  The windows of all buffers, in index order, are the batch's SLOTS
+// (global slot g_i + m for window m of buffer i).  Shorter buffers are
+// finished byte-serially by the prep kernel.
+//
+//  k_v7prep   per tile of 256 buffers: W and the tile's slot prefix (single-pass
+//             decoupled look-back over the tiles), then per buffer g_i, the lead
+//             and tail EDGE TERMS (below), short buffers finished; zeroes out[]
+//             of windowed buffers; the last tile writes the total and the
+//             per-wave quantum (whole passes)
+//  k_varlen7  wave w checksums slots [w*Qs, (w+1)*Qs): slot k of a pass is
+//             window k%4 of 4 (one 16-lane team each, page-kernel layout), so a
+//             pass always carries four windows whatever the buffer sizes.
+//
+// Edge terms (CRC linearity: the chain of a XOR b is chain(a) ^ chain(b)):
+// the pass checksums the garbage bytes [A, P0) before the buffer and
+// [P1, E) after it, and no seed.  The lead term is the register of the lead
+// lane's 64-byte span fed with only those garbage bytes, with the register
+// ~seed injected at P0 (crc32c.cpp:197) -- XORed in, it cancels the garbage
+// and adds the seed; the tail term cancels the trailing garbage.  Both are
+// stored as TEAM-SUM terms (already multiplied by their lane's constant), so
+// the streaming kernel only XORs them into the slot sums.
+//
+// Combining, per table of 64 slots (16 passes) of a wave, lane-parallel: the
+// 64-lane constant tables give slot sum S_k = Rw_k * x^(8*1024*(3 - k%4));
+// weighted by x^(8*4096*(15 - k/4)) it becomes Rw_k * x^(8*1024*(63-k)); a
+// prefix XOR over the lanes then yields every buffer's total at its last slot
+// kl, normalised by x^(-8*(1024*(63-kl) + zt)) (zt = E - P1 trailing zeros).
+// A buffer open at a table's end carries into the next table as one uniform
+// register times x^(8*65536); a buffer cut by the wave range is finished as a
+// part shifted to its end and XOR-merged (atomicXor) with its other parts.
+constexpr uint32_t kTileW = 256;
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
+	return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+	return ((uint64_t)shfl32((uint32_t)(v >> 32), src) << 32) | shfl32((uint32_t)v, src);
+}
+// Inclusive prefix XOR over the wave.
+__device__ __forceinline__ uint32_t scanx(uint32_t v, int lane) {
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint32_t y = shup(v, d);
+		if (lane >= d) v ^= y;
+	}
+	return v;
+}
+// Byte mask of a 16-byte chunk keeping bytes < k1 (1..15).
+__device__ __forceinline__ void keep_below7(uint32_t k1, uint32_t (&tm)[4]) {
+	const uint64_t ones = ~uint64_t(0);
+	const uint64_t lo = k1 >= 8 ? ones : ones >> (64 - 8 * k1);
+	const uint64_t hi = k1 <= 8 ? 0 : ones >> (128 - 8 * k1);
+	tm[0] = (uint32_t)lo; tm[1] = (uint32_t)(lo >> 32); tm[2] = (uint32_t)hi; tm[3] = (uint32_t)(hi >> 32);
+}
+struct Geo7 {
+	uint64_t A;    // P0 & ~15
+	uint32_t W;    // windows (0: shorter than 16 bytes)
+	uint32_t lo;   // bytes of window 0 before A (multiple of 16, < 1024)
+	uint32_t k0;   // P0 % 16
+	uint32_t zt;   // E - P1
+};
+__device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len) {
+	Geo7 g;
+	const uint64_t P1 = P0 + len;
+	const uint64_t E = (P1 + 15) & ~uint64_t(15);
+	g.A = P0 & ~uint64_t(15);
+	const uint64_t span = E - g.A;
+	g.W = len >= 16 ? (uint32_t)((span + 1023) >> 10) : 0u;
+	g.lo = (uint32_t)(1024 * (uint64_t)g.W - span) & 1023u;
+	g.k0 = (uint32_t)(P0 & 15);
+	g.zt = (uint32_t)(E - P1);
+	return g;
+}
+struct V7Params {
+	const uint8_t* base;
+	const uint64_t* offsets;   // nullptr: fixed stride
+	const uint64_t* lengths;   // nullptr: fixed length
+	uint64_t stride, length, count;
+	uint32_t seed;
+	const uint32_t* seeds;
+	uint32_t* out;
+	uint64_t* hdr;             // [0] total slots, [1] slots per wave
+	uint64_t* tsum;            // per tile: windows of its buffers (exclusive prefix after k_scan)
+	uint64_t* incl;            // per tile: inclusive slot prefix
+	uint64_t ntile, nwave;
+	bool scanned;              // tsum already holds exclusive prefixes (large batches: k_scan ran)
+	uint32_t* gs;              // first slot of each buffer
+	uint32_t* cl;              // lead edge term (team-sum form)
+	uint32_t* ct;              // tail edge term (team-sum form)
+	const DevTables* tabs;
+};
+__device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_t& off, uint64_t& len) {
+	off = P.offsets ? P.offsets[i] : i * P.stride;
+	len = P.lengths ? P.lengths[i] : P.length;
+}
+__global__ __launch_bounds__(256) void k_v7count(V7Params P) {
+	__shared__ uint64_t part[4];
+	const uint64_t i = (uint64_t)blockIdx.x * kTileW + threadIdx.x;
+	uint64_t W = 0;
+	if (i < P.count) {
+		uint64_t off, len;
+		v7_buffer(P, i, off, len);
+		W = geo7(reinterpret_cast<uint64_t>(P.base) + off, len).W;
+	}
+	for (int o = 32; o > 0; o >>= 1) W += __shfl_xor(W, o);
+	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = W;
+	__syncthreads();
+	if (threadIdx.x == 0) P.tsum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+__global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
+	__shared__ uint32_t s4[4][256];  // slice4 tables (no bank replication: this kernel is not LDS-bound)
+	__shared__ uint32_t wsum[4];
+	__shared__ uint64_t s_pre[4];
+	const DevTables* T = P.tabs;
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = T->slice4[k][threadIdx.x];
+	const uint32_t tile = blockIdx.x;
+	// exclusive slot prefix of this tile: the sum of all earlier tile sums,
+	// read in parallel by the whole block (no inter-block waiting)
+	uint64_t pre = 0;
+	if (P.scanned) {
+		pre = threadIdx.x == 0 ? P.tsum[tile] : 0;
+	} else {
+		for (uint32_t k = threadIdx.x; k < tile; k += blockDim.x) pre += P.tsum[k];
+	}
+	for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+	if (lane == 0) s_pre[wv] = pre;
+	const uint64_t i = (uint64_t)tile * kTileW + threadIdx.x;
+	const bool ok = i < P.count;
+	uint64_t off = 0, len = 0;
+	if (ok) v7_buffer(P, i, off, len);
+	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
+	const Geo7 g = geo7(P0, len);
+	const uint32_t W = ok ? g.W : 0u;
+	uint32_t incl = W;
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+		if (lane >= d) incl += y;
+	}
+	if (lane == 63) wsum[wv] = incl;
+	__syncthreads();
+	uint32_t inwave = 0, agg = 0;
+	for (int k = 0; k < 4; ++k) {
+		inwave += k < wv ? wsum[k] : 0u;
+		agg += wsum[k];
+	}
+	const uint32_t excl = (uint32_t)(s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3]);
+	if (threadIdx.x == 0) {
+		P.incl[tile] = (uint64_t)excl + agg;
+		if (tile + 1 == P.ntile) {
+			const uint64_t total = (uint64_t)excl + agg;
+			uint64_t q = (total + P.nwave - 1) / P.nwave;
+			q = q < 4 ? 4 : (q + 3) & ~uint64_t(3);
+			P.hdr[0] = total;
+			P.hdr[1] = q;
+		}
+	}
+	if (!ok) return;
+	const uint32_t gi = excl + inwave + incl - W;
+	P.gs[i] = gi;
+	const uint32_t s0 = ~(P.seeds ? P.seeds[i] : P.seed);
+	if (!W) {  // shorter than 16 bytes: byte-serial
+		uint32_t r = s0;
+		for (uint64_t q = 0; q < len; ++q) r = (r >> 8) ^ s4[3][(r ^ ld1(P.base + off + q)) & 255u];
+		P.out[i] = ~r;
+		return;
+	}
+	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
+	// lead term: the lead chunk's bytes below k0 with the register ~seed
+	// injected at k0, carried to the end of the pass block (chunkpow)
+	{
+		const u32x4 ch = ld16(reinterpret_cast<const uint8_t*>(g.A));
+		uint32_t x = 0;
+#pragma unroll
+		for (uint32_t b = 0; b < 16; ++b) {
+			if (b == g.k0) x ^= s0;
+			const uint32_t byte = b < g.k0 ? (ch[b >> 2] >> (8 * (b & 3))) & 255u : 0u;
+			x = (x >> 8) ^ s4[3][(x ^ byte) & 255u];
+		}
+		P.cl[i] = vmul(&T->chunkpow[64u * (gi & 3u) + (g.lo >> 4)][0][0], x);
+	}
+	// tail term: the garbage bytes after P1 in the last chunk (chunk 63 of the
+	// last window)
+	uint32_t tv = 0;
+	if (g.zt) {
+		const u32x4 ch = ld16(reinterpret_cast<const uint8_t*>((P0 + len) & ~uint64_t(15)));
+		uint32_t km[4];
+		keep_below7(16u - g.zt, km);
+		uint32_t x = 0;
+#pragma unroll
+		for (int d = 0; d < 4; ++d) {
+			x ^= ch[d] & ~km[d];
+			x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
+		}
+		tv = vmul(&T->chunkpow[64u * ((gi + W - 1) & 3u) + 63u][0][0], x);
+	}
+	P.ct[i] = tv;
+}
+
+// Streaming kernel.  Tables of 64 slots (wave-relative), passes of 4 slots.
+constexpr uint32_t k7_LO = 0x7FFu;          // bytes of the window not loaded at its start (1024: empty slot)
+constexpr uint32_t k7_ZT = 11;              // trailing zeros of the last window (4 bits)
+constexpr uint32_t k7_LAST = 1u << 15;      // last window of the buffer
+constexpr uint32_t k7_PEND = 1u << 16;      // the wave's last slot, buffer continues in the next wave
+constexpr uint32_t k7_SPLIT = 1u << 17;     // buffer shared with another wave: XOR-merge the part
+constexpr uint32_t k7_INV = 1u << 18;       // this part holds window 0 (applies the final inversion)
+constexpr uint32_t k7_CONT = 1u << 19;      // buffer began before this table
+constexpr uint32_t k7_KF = 20;              // first slot of the buffer inside the table (6 bits)
+// s_waitcnt vmcnt(6) (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15, vmcnt[5:4] at [15:14])
+__device__ __forceinline__ void kWaitVm6() { __builtin_amdgcn_s_waitcnt(0x0F76); }
+struct Tab7 {
+	uint64_t wa;   // window address
+	uint32_t f;
+	uint32_t oi;   // output index relative to the wave's first tile
+	uint32_t S;    // team sum of the slot, XORed onto the slot's edge terms (team-sum form)
+};
+
+__global__ __launch_bounds__(1024) void k_varlen7(V7Params P) {
+	__shared__ uint32_t lds[kLdsBytesB / 4];
+	const DevTables* __restrict__ T = P.tabs;
+	const LaneCtx c = make_ctx();
+	const int lane = c.lane;
+	const uint32_t col4 = (lane & 31) * 4;
+	const uint32_t c4 = col4 | 0x10000u;
+	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
+	fill_lds_b(lds, T);
+	const uint64_t wpb = blockDim.x >> 6;
+	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
+	const uint64_t w = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
+	typedef __attribute__((address_space(1))) const uint64_t g_u64;
+	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
+	const uint64_t total = rdfirst64(hp[0]), Qs = rdfirst64(hp[1]);
+	const uint64_t lo_s64 = w * Qs;
+	if (lo_s64 >= total) return;
+	const uint32_t lo_s = (uint32_t)lo_s64;
+	const uint32_t hi_s = (uint32_t)(lo_s64 + Qs < total ? lo_s64 + Qs : total);
+	// the tile holding slot lo_s: the number of tiles whose inclusive prefix is
+	// <= lo_s, narrowed 64 segments at a time
+	uint64_t t_lo = 0, t_n = P.ntile;
+	while (t_n > 64) {
+		const uint64_t stp = (t_n + 63) >> 6;
+		const uint64_t k = (uint64_t)lane * stp;
+		bool le = false;
+		if (k < t_n) {
+			const uint64_t idx = t_lo + (k + stp - 1 < t_n ? k + stp - 1 : t_n - 1);
+			le = gld64(&P.incl[idx]) <= lo_s;
+		}
+		const uint64_t cnt = __builtin_popcountll(__ballot(le));
+		t_lo += cnt * stp;
+		t_n = cnt * stp + stp <= t_n ? stp : t_n - cnt * stp;
+	}
+	const bool le = (uint64_t)lane < t_n && gld64(&P.incl[t_lo + lane]) <= lo_s;
+	const uint64_t bi_w = (t_lo + __builtin_popcountll(__ballot(le))) * kTileW;  // output indices are relative to this
+
+	// ---- batch: 64 buffers, lane j <-> buffer bi0 + j ---------------------
+	uint64_t nb_bi0 = bi_w;
+	bool more = true;
+	uint64_t B_bi0 = 0;
+	uint64_t B_wb;          // window 0 address
+	uint32_t B_g, B_W, B_f; // first slot, windows, lo | zt << 11
+	uint32_t B_cl, B_ct;
+	uint32_t Gb1 = 0;       // wave-relative end of the batch's slots
+	uint64_t p_shift = 0;   // bytes from the end of the wave's last window to its buffer's end
+	auto build = [&]() {
+		const uint64_t bi0 = nb_bi0;
+		const uint64_t j = bi0 + lane;
+		const bool ok = j < P.count;
+		uint64_t off = 0, len = 0;
+		uint32_t g = 0xFFFFFFFFu, cl = 0, ct = 0;
+		if (ok) {
+			v7_buffer(P, j, off, len);
+			g = P.gs[j];
+			cl = P.cl[j];
+			ct = P.ct[j];
+		}
+		const Geo7 ge = geo7(reinterpret_cast<uint64_t>(P.base) + off, len);
+		const uint32_t W = ok ? ge.W : 0u;
+		B_bi0 = bi0;
+		B_wb = ge.A - ge.lo;
+		B_g = g;
+		B_W = W;
+		B_f = ge.lo | (ge.zt << k7_ZT);
+		B_cl = cl;
+		B_ct = ct;
+		nb_bi0 = bi0 + 64;
+		// end of the slots of this batch (pieces are in order; W = 0 pieces add nothing)
+		const uint32_t e = ok ? g + W : 0u;
+		uint32_t emax = e;
+#pragma unroll
+		for (int d = 32; d > 0; d >>= 1) {
+			const uint32_t y = (uint32_t)__shfl_xor((int)emax, d);
+			emax = y > emax ? y : emax;
+		}
+		emax = rdfirst(emax);
+		Gb1 = (emax > hi_s ? hi_s : emax) - lo_s;
+		if (emax < lo_s) Gb1 = 0;
+		more = nb_bi0 < P.count && emax < hi_s;
+	};
+	// slots [sb + k_lo, min(Gb1, sb + 64)) of the current batch into table lanes
+	auto expand = [&](Tab7& X, uint32_t sb, uint32_t k_lo) -> uint32_t {
+		const uint32_t k_hi = Gb1 - sb < 64u ? Gb1 - sb : 64u;
+		const uint32_t ts = lo_s + sb;  // global slot of table lane 0
+		// buffer start inside the table, clamped (non-decreasing in j); the
+		// owner of lane k is the largest j with st_j <= k
+		const uint32_t st = B_g == 0xFFFFFFFFu ? 64u : (B_g <= ts ? 0u : (B_g - ts < 64u ? B_g - ts : 64u));
+		uint32_t jj = 0;
+#pragma unroll
+		for (uint32_t step = 32; step; step >>= 1)
+			if (shfl32(st, jj + step) <= (uint32_t)lane) jj += step;
+		const uint64_t wb = shfl64(B_wb, jj);
+		const uint32_t g = shfl32(B_g, jj), W = shfl32(B_W, jj), bf = shfl32(B_f, jj);
+		const uint32_t cl = shfl32(B_cl, jj), ct = shfl32(B_ct, jj);
+		const uint32_t slot = ts + (uint32_t)lane;
+		const uint32_t m = slot - g;
+		const bool lead = m == 0, last = m + 1 == W;
+		const bool pend = slot + 1 == hi_s && !last;
+		const bool split = g < lo_s || g + W > hi_s;
+		const bool cont = g < ts;
+		const uint32_t f = (lead ? (bf & 1023u) : 0u) | (last ? (bf & (15u << k7_ZT)) : 0u) | (last ? k7_LAST : 0u) |
+		                   (pend ? k7_PEND : 0u) | (split ? k7_SPLIT : 0u) | (g >= lo_s ? k7_INV : 0u) |
+		                   (cont ? k7_CONT : 0u) | ((cont ? 0u : g - ts) << k7_KF);
+		if ((uint32_t)lane >= k_lo && (uint32_t)lane < k_hi) {
+			X.wa = wb + 1024 * (uint64_t)m;
+			X.f = f;
+			X.S = (lead ? cl : 0u) ^ (last ? ct : 0u);
+			X.oi = (uint32_t)(B_bi0 - bi_w) + jj;
+		}
+		// bytes from the end of the wave's last window to the buffer's end
+		const uint64_t pm = __ballot(pend && (uint32_t)lane >= k_lo && (uint32_t)lane < k_hi);
+		if (pm) {
+			const int k = __builtin_ctzll(pm);
+			p_shift = 1024 * (uint64_t)(rdlane(W, k) - 1 - rdlane(m, k)) - ((rdlane(bf, k) >> k7_ZT) & 15u);
+		}
+		return k_hi;
+	};
+	auto build_table = [&](Tab7& X, uint32_t sb) -> uint32_t {
+		X.wa = 0;
+		X.f = 1024u;
+		X.oi = 0;
+		X.S = 0;
+		uint32_t filled = 0;
+		for (;;) {
+			if (Gb1 > sb + filled) filled = expand(X, sb, filled);
+			if (filled == 64 || !more) break;
+			build();
+		}
+		if (filled && filled < 64) {  // empty slots re-read a chunk of slot 0 (never used)
+			const uint64_t w0 = rdlane64(X.wa, 0);
+			if ((uint32_t)lane >= filled) X.wa = w0;
+		}
+		return filled;
+	};
+	// load k of a pass fetches team {0,2,1,3}[k]'s window.  Every load is
+	// issued unconditionally (a branch around a load defeats the compiler's
+	// wait counting): chunks of window 0 before the buffer's first chunk, and
+	// empty slots, re-read the lead chunk (empty slots: slot 0's last chunk)
+	// and are zeroed at compute time.
+	auto load = [&](Block& nb, const Tab7& X, uint32_t p) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint32_t s = 4 * p + (((k & 1) << 1) | (k >> 1));
+			const uint64_t wa = rdlane64(X.wa, (int)s);
+			const uint32_t lo = rdlane(X.f, (int)s) & k7_LO;
+			const uint32_t lc = lo < 1008u ? lo : 1008u;
+			nb.r[k] = ld16(reinterpret_cast<const uint8_t*>(wa + (c.ld_off > lc ? c.ld_off : lc)));
+		}
+	};
+	auto compute = [&](Block& b, Tab7& X, uint32_t p) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint32_t lo = rdlane(X.f, (int)(4 * p + (((k & 1) << 1) | (k >> 1)))) & k7_LO;
+			if (lo) {
+				const bool z = c.ld_off < lo;
+#pragma unroll
+				for (int d = 0; d < 4; ++d) b.r[k][d] = z ? 0u : b.r[k][d];
+			}
+		}
+		unswizzle(b);
+		const uint32_t R = row_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
+		const uint32_t v = shfl32(R, ((uint32_t)lane & 3u) * 16u);
+		X.S ^= ((uint32_t)lane >> 2) == p ? v : 0u;
+	};
+	uint32_t carry = 0;  // register of the buffer open across the table boundary
+	auto combine = [&](Tab7& X, uint32_t filled) {
+#if FDBCRC_EXP & 64
+		const uint32_t D = X.S;
+#else
+		const uint32_t D = vmul(&T->x4pow[15 - ((uint32_t)lane >> 2)][0][0], X.S);
+#endif
+		const uint32_t Pp = scanx(D, lane);
+		const uint32_t f = X.f;
+		const uint32_t kf = (f >> k7_KF) & 63u;
+		const bool cont = f & k7_CONT;
+		const uint32_t pk = shfl32(Pp, kf ? kf - 1 : 0u);
+		uint32_t v = Pp ^ ((!cont && kf) ? pk : 0u);
+		const uint32_t cc = carry ? umul(T->table_shift, carry) : 0u;
+		v ^= cont ? cc : 0u;
+		carry = (filled == 64 && !(rdlane(f, 63) & (k7_LAST | k7_PEND))) ? rdlane(v, 63) : 0u;
+		const bool fin = (f & (k7_LAST | k7_PEND)) && (uint32_t)lane < filled;
+		const uint32_t zt = (f & k7_LAST) ? (f >> k7_ZT) & 15u : 0u;
+#if !(FDBCRC_EXP & 64)
+		v = vmul(&T->normk[lane][zt][0][0], v);
+#endif
+		const uint64_t pm = __ballot(fin && (f & k7_PEND));
+		if (pm) {  // the wave's last buffer continues in the next wave: shift its part to the buffer's end
+			const int k = __builtin_ctzll(pm);
+			const uint32_t vv = mul_xpow(T, rdlane(v, k), p_shift);
+			v = lane == k ? vv : v;
+		}
+		if (fin) {
+			uint32_t* o = P.out + bi_w + X.oi;
+			if (f & k7_SPLIT) atomicXor(o, (f & k7_INV) ? ~v : v);
+			else *o = ~v;
+		}
+	};
+	// Two blocks in ping-pong (a register copy would wait for the loads in
+	// flight): pass p computes from one while pass p + 1 loads into the other.
+	// Full tables have 16 passes, so the next table's pass 0 lands in ba.
+	Block ba, bb;
+	// all passes of table X (its pass 0 already issued into ba); builds Y and
+	// issues its pass 0 before the last pass of X
+	auto run_table = [&](Tab7& X, Tab7& Y, uint32_t sbX, uint32_t fX) -> uint32_t {
+		const uint32_t npass = (fX + 3) >> 2;
+		uint32_t fY = 0;
+		uint32_t p = 0;
+		// steady state: only the data loads touch vector memory.  The explicit
+		// waits (no-ops at run time: at most the 4 loads of ba plus 2 stores are
+		// outstanding there) pin the loop's entry state for the compiler's
+		// wait-count pass, which otherwise merges the paths into the loop
+		// pessimistically and waits for the loads in flight.
+		kWaitVm6();
+		for (; p + 2 < npass; p += 2) {
+			load(bb, X, p + 1);
+			__builtin_amdgcn_sched_barrier(0);
+			compute(ba, X, p);
+			__builtin_amdgcn_sched_barrier(0);
+			load(ba, X, p + 2);
+			__builtin_amdgcn_sched_barrier(0);
+			compute(bb, X, p + 1);
+			__builtin_amdgcn_sched_barrier(0);
+			kWaitVm6();
+		}
+		if (p + 1 < npass) {  // last pair: the next table's pass 0 goes to ba
+			load(bb, X, p + 1);
+			__builtin_amdgcn_sched_barrier(0);
+			compute(ba, X, p);
+			__builtin_amdgcn_sched_barrier(0);
+			fY = fX == 64 ? build_table(Y, sbX + 64) : 0u;
+			if (fY) load(ba, Y, 0);
+			__builtin_amdgcn_sched_barrier(0);
+			compute(bb, X, p + 1);
+			__builtin_amdgcn_sched_barrier(0);
+		} else {  // a single pass left (odd pass count: the wave's last table)
+			compute(ba, X, p);
+			__builtin_amdgcn_sched_barrier(0);
+		}
+		combine(X, fX);
+		return fY;
+	};
+
+	Tab7 t0, t1;
+	build();
+	uint32_t sb = 0;
+	uint32_t f0 = build_table(t0, 0);
+	if (f0) load(ba, t0, 0);
+	while (f0) {
+		const uint32_t f1 = run_table(t0, t1, sb, f0);
+		sb += 64;
+		if (!f1) break;
+		f0 = run_table(t1, t0, sb, f1);
+		sb += 64;
+	}
+}
+
+uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
+	const uint64_t ntile = (count + kTileW - 1) / kTileW;
+	return 16 + 16 * (ntile + 1) + 4 * nwave + 12 * count + 64;
+}
+
+int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
+                   uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
+                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream) {
+	const uint64_t grid = (uint64_t)num_cus;
+	const uint64_t nwave = grid * 16;
+	const uint64_t ntile = (count + kTileW - 1) / kTileW;
+	uint8_t* wp = static_cast<uint8_t*>(ws);
+	V7Params P{};
+	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
+	P.seed = seed; P.seeds = seeds; P.out = out; P.tabs = tabs;
+	P.ntile = ntile; P.nwave = nwave;
+	P.hdr = reinterpret_cast<uint64_t*>(wp);
+	P.tsum = reinterpret_cast<uint64_t*>(wp + 16);
+	P.incl = P.tsum + ntile + 1;
+	uint32_t* wave_tile = reinterpret_cast<uint32_t*>(P.incl + ntile + 1);  // k_scan output (unused here)
+	P.gs = wave_tile + nwave;
+	P.cl = P.gs + count;
+	P.ct = P.cl + count;
+	// tile prefixes: each prep block sums its predecessors (up to 8192 tiles);
+	// larger batches scan the tile sums first
+	P.scanned = ntile > 8192;
+	k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	if (P.scanned) k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4);
+	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	k_varlen7<<<(unsigned)grid, 1024, 0, stream>>>(P);
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) {
+#if FDBCRC_V7
+	return varlen7_workspace_bytes(count, nwave);
+#else
 	const uint64_t ntile = (count + kTile - 1) / kTile;
 	return 16 + 8 * (ntile + 1) + 4 * nwave + 64;
+#endif
 }
 
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                   hipStream_t stream) {
+#if FDBCRC_V7
+	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream);
+#endif
 	const uint64_t grid = (uint64_t)num_cus;
 	const uint64_t nwave = grid * 16;
 	const uint64_t ntile = (count + kTile - 1) / kTile;
