@@ -15,9 +15,11 @@ struct DevTables {
 	uint32_t pow2[64][8][16];   // nibble tables of x^(8*2^m): shift by arbitrary byte counts
 	uint32_t corr[4][16][8][16];  // x^(-8(z + 1024(3-t))): quarter t's team value -> piece register, minus z zeros
 	// varlen v7 (1 KiB window slots, 64 slots per table)
-	uint32_t x4pow[16][8][16];       // x^(8*4096*i): slot sums of pass i -> weight x^(8*1024*(63-slot))
 	uint32_t table_shift[8][16];     // x^(8*65536): a piece's register carried across a 64-slot table
-	uint32_t normk[64][16][8][16];   // x^(-8*(1024*(63-k) + z)): piece ending at slot k, z trailing zeros
+	uint32_t slotw[64][16][8][16];   // x^(8*(1024*(d-3) - z)): slot sum of pass p -> its buffer's end
+	                                 // (d = last slot - 4p, z trailing zeros)
+	uint32_t carryw[64][16][8][16];  // x^(8*(1024*(k+1) - z)): a register carried into a table -> its
+	                                 // buffer's end at slot k
 	uint32_t chunkpow[256][8][16];   // x^(8*16*(255-c)): 16-byte chunk c of a pass block to the block's end
 };
 

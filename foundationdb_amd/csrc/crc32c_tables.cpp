@@ -26,10 +26,13 @@ void build_dev_tables(DevTables* t) {
 	for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(z), t->inv_z[z]);
 	for (int q = 0; q < 4; ++q)
 		for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(z + 1024u * (3 - q)), t->corr[q][z]);
-	for (int i = 0; i < 16; ++i) mul_tables_nibble(xpow8(4096u * i), t->x4pow[i]);
 	mul_tables_nibble(xpow8(65536), t->table_shift);
-	for (int k = 0; k < 64; ++k)
-		for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(1024u * (63 - k) + z), t->normk[k][z]);
+	for (int d = 0; d < 64; ++d)
+		for (int z = 0; z < 16; ++z) {
+			const int64_t e = 1024 * (int64_t)(d - 3) - z;
+			mul_tables_nibble(e >= 0 ? xpow8((uint64_t)e) : xpow8_inv((uint64_t)-e), t->slotw[d][z]);
+			mul_tables_nibble(xpow8(1024u * (d + 1) - z), t->carryw[d][z]);
+		}
 	for (int c = 0; c < 256; ++c) mul_tables_nibble(xpow8(16u * (255 - c)), t->chunkpow[c]);
 	for (int m = 0; m < 64; ++m) {
 		// x^(8*2^m) by repeated squaring of x^8

@@ -806,6 +806,7 @@ struct V7Params {
 	uint32_t* gs;              // first slot of each buffer
 	uint32_t* cl;              // lead edge term (team-sum form)
 	uint32_t* ct;              // tail edge term (team-sum form)
+	uint32_t* dummy;           // 64 words per wave: target of the no-op XORs
 	const DevTables* tabs;
 };
 __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_t& off, uint64_t& len) {
@@ -920,13 +921,14 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 
 // Streaming kernel.  Tables of 64 slots (wave-relative), passes of 4 slots.
 constexpr uint32_t k7_LO = 0x7FFu;          // bytes of the window not loaded at its start (1024: empty slot)
-constexpr uint32_t k7_ZT = 11;              // trailing zeros of the last window (4 bits)
-constexpr uint32_t k7_LAST = 1u << 15;      // last window of the buffer
-constexpr uint32_t k7_PEND = 1u << 16;      // the wave's last slot, buffer continues in the next wave
+constexpr uint32_t k7_ZT = 11;              // trailing zeros of the buffer, when it ends in this table (4 bits)
+constexpr uint32_t k7_FIN = 1u << 15;       // the buffer's last slot in this wave
+constexpr uint32_t k7_PEND = 1u << 16;      // ... because the wave ends there: the buffer continues
 constexpr uint32_t k7_SPLIT = 1u << 17;     // buffer shared with another wave: XOR-merge the part
 constexpr uint32_t k7_INV = 1u << 18;       // this part holds window 0 (applies the final inversion)
 constexpr uint32_t k7_CONT = 1u << 19;      // buffer began before this table
 constexpr uint32_t k7_KF = 20;              // first slot of the buffer inside the table (6 bits)
+constexpr uint32_t k7_KL = 26;              // last slot of the buffer's part in the table, 63 if open (6 bits)
 // s_waitcnt vmcnt(6) (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15, vmcnt[5:4] at [15:14])
 __device__ __forceinline__ void kWaitVm6() { __builtin_amdgcn_s_waitcnt(0x0F76); }
 struct Tab7 {
@@ -936,7 +938,10 @@ struct Tab7 {
 	uint32_t S;    // team sum of the slot, XORed onto the slot's edge terms (team-sum form)
 };
 
-__global__ __launch_bounds__(1024) void k_varlen7(V7Params P) {
+#ifndef FDBCRC_V7_THREADS
+#define FDBCRC_V7_THREADS 768  // 12 waves per CU: 168 VGPRs per lane, no spills
+#endif
+__global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const DevTables* __restrict__ T = P.tabs;
 	const LaneCtx c = make_ctx();
@@ -1033,13 +1038,17 @@ __global__ __launch_bounds__(1024) void k_varlen7(V7Params P) {
 		const uint32_t cl = shfl32(B_cl, jj), ct = shfl32(B_ct, jj);
 		const uint32_t slot = ts + (uint32_t)lane;
 		const uint32_t m = slot - g;
+		const uint32_t gend = g + W - 1;                          // the buffer's last slot
+		const uint32_t wend = gend < hi_s - 1 ? gend : hi_s - 1;  // ... in this wave
 		const bool lead = m == 0, last = m + 1 == W;
-		const bool pend = slot + 1 == hi_s && !last;
+		const bool fin = slot == wend, pend = fin && wend != gend;
 		const bool split = g < lo_s || g + W > hi_s;
 		const bool cont = g < ts;
-		const uint32_t f = (lead ? (bf & 1023u) : 0u) | (last ? (bf & (15u << k7_ZT)) : 0u) | (last ? k7_LAST : 0u) |
-		                   (pend ? k7_PEND : 0u) | (split ? k7_SPLIT : 0u) | (g >= lo_s ? k7_INV : 0u) |
-		                   (cont ? k7_CONT : 0u) | ((cont ? 0u : g - ts) << k7_KF);
+		const bool ends = wend - ts < 64u;  // the part ends inside this table
+		const uint32_t f = (lead ? (bf & 1023u) : 0u) | ((ends && wend == gend) ? (bf & (15u << k7_ZT)) : 0u) |
+		                   (fin ? k7_FIN : 0u) | (pend ? k7_PEND : 0u) | (split ? k7_SPLIT : 0u) |
+		                   (g >= lo_s ? k7_INV : 0u) | (cont ? k7_CONT : 0u) | ((cont ? 0u : g - ts) << k7_KF) |
+		                   ((ends ? wend - ts : 63u) << k7_KL);
 		if ((uint32_t)lane >= k_lo && (uint32_t)lane < k_hi) {
 			X.wa = wb + 1024 * (uint64_t)m;
 			X.f = f;
@@ -1101,54 +1110,84 @@ __global__ __launch_bounds__(1024) void k_varlen7(V7Params P) {
 		const uint32_t v = shfl32(R, ((uint32_t)lane & 3u) * 16u);
 		X.S ^= ((uint32_t)lane >> 2) == p ? v : 0u;
 	};
-	uint32_t carry = 0;  // register of the buffer open across the table boundary
-	auto combine = [&](Tab7& X, uint32_t filled) {
-#if FDBCRC_EXP & 64
-		const uint32_t D = X.S;
-#else
-		const uint32_t D = vmul(&T->x4pow[15 - ((uint32_t)lane >> 2)][0][0], X.S);
-#endif
+	// Combining a table: one round of table lookups weights every slot sum
+	// straight to its buffer's end (slotw[kl - 4p][zt]), so a prefix XOR over
+	// the lanes leaves each buffer's final register at its last slot.  The
+	// lookups (global gathers, which share the in-order vmcnt with the data
+	// loads) are issued after the table's last pass (phase 1) and consumed in
+	// the next table's first pass, right after its next loads (phase 2): the
+	// wait then coincides with one the pipeline does anyway.  Every vector
+	// memory operation here is unconditional (lanes with nothing to finish XOR
+	// 0 into a dummy word): a load or store skipped by a branch would make the
+	// compiler wait for all loads in flight.
+	uint32_t carry = 0;     // register of the buffer open across the table boundary (relative to the table end)
+	uint32_t pend_filled = 0;
+	uint32_t gv[8];         // nibble-table words in flight (never live across a pass's compute)
+	auto phase1 = [&](Tab7& X, uint32_t filled) {
+		const uint32_t f = X.f;
+		const uint32_t d = (((f >> k7_KL) & 63u) - ((uint32_t)lane >> 2) * 4u) & 63u;
+		const uint32_t(*tab)[16] = T->slotw[d][(f >> k7_ZT) & 15u];
+		const uint32_t v = X.S;
+#pragma unroll
+		for (int n = 0; n < 8; ++n) gv[n] = gld32(&tab[n][(v >> (4 * n)) & 15u]);
+		pend_filled = filled;
+	};
+	auto phase2 = [&](Tab7& X) {
+		const uint32_t D = xor3(xor3(gv[0], gv[1], gv[2]), xor3(gv[3], gv[4], gv[5]), gv[6] ^ gv[7]);
 		const uint32_t Pp = scanx(D, lane);
 		const uint32_t f = X.f;
 		const uint32_t kf = (f >> k7_KF) & 63u;
 		const bool cont = f & k7_CONT;
 		const uint32_t pk = shfl32(Pp, kf ? kf - 1 : 0u);
 		uint32_t v = Pp ^ ((!cont && kf) ? pk : 0u);
-		const uint32_t cc = carry ? umul(T->table_shift, carry) : 0u;
-		v ^= cont ? cc : 0u;
-		carry = (filled == 64 && !(rdlane(f, 63) & (k7_LAST | k7_PEND))) ? rdlane(v, 63) : 0u;
-		const bool fin = (f & (k7_LAST | k7_PEND)) && (uint32_t)lane < filled;
-		const uint32_t zt = (f & k7_LAST) ? (f >> k7_ZT) & 15u : 0u;
-#if !(FDBCRC_EXP & 64)
-		v = vmul(&T->normk[lane][zt][0][0], v);
-#endif
+		// the register carried in from the previous table belongs to the buffer
+		// holding slot 0 (CONT): to its finishing slot, or across this table
+		const uint32_t f0 = rdlane(f, 0);
+		const uint32_t kl0 = (f0 >> k7_KL) & 63u;
+		const bool fin0 = (f0 & k7_CONT) && (rdlane(f, (int)kl0) & k7_FIN);
+		uint32_t cc = 0;
+		if (carry) cc = umul(fin0 ? T->carryw[kl0][(f0 >> k7_ZT) & 15u] : T->table_shift, carry);
+		const bool fin = (f & k7_FIN) && (uint32_t)lane < pend_filled;
+		v ^= (cont && (fin || lane == 63)) ? cc : 0u;
+		carry = (pend_filled == 64 && !(rdlane(f, 63) & k7_FIN)) ? rdlane(v, 63) : 0u;
 		const uint64_t pm = __ballot(fin && (f & k7_PEND));
 		if (pm) {  // the wave's last buffer continues in the next wave: shift its part to the buffer's end
 			const int k = __builtin_ctzll(pm);
 			const uint32_t vv = mul_xpow(T, rdlane(v, k), p_shift);
 			v = lane == k ? vv : v;
 		}
-		if (fin) {
-			uint32_t* o = P.out + bi_w + X.oi;
-			if (f & k7_SPLIT) atomicXor(o, (f & k7_INV) ? ~v : v);
-			else *o = ~v;
-		}
+		// windowed buffers' out[] words are zeroed by the prep kernel; the part
+		// holding window 0 carries the final inversion
+		atomicXor(fin ? P.out + bi_w + X.oi : P.dummy + w * 64 + lane, fin ? ((f & k7_INV) ? ~v : v) : 0u);
 	};
 	// Two blocks in ping-pong (a register copy would wait for the loads in
 	// flight): pass p computes from one while pass p + 1 loads into the other.
 	// Full tables have 16 passes, so the next table's pass 0 lands in ba.
 	Block ba, bb;
-	// all passes of table X (its pass 0 already issued into ba); builds Y and
-	// issues its pass 0 before the last pass of X
-	auto run_table = [&](Tab7& X, Tab7& Y, uint32_t sbX, uint32_t fX) -> uint32_t {
+	// all passes of table X (its pass 0 already issued into ba); V holds the
+	// previous table (phase 1 done) and is rebuilt as the next table
+	auto run_table = [&](Tab7& X, Tab7& V, uint32_t sbX, uint32_t fX) -> uint32_t {
 		const uint32_t npass = (fX + 3) >> 2;
 		uint32_t fY = 0;
 		uint32_t p = 0;
+		if (npass >= 3) {  // first pair: the previous table's phase 2
+			load(bb, X, 1);
+			__builtin_amdgcn_sched_barrier(0);
+			phase2(V);
+			__builtin_amdgcn_sched_barrier(0);
+			compute(ba, X, 0);
+			__builtin_amdgcn_sched_barrier(0);
+			load(ba, X, 2);
+			__builtin_amdgcn_sched_barrier(0);
+			compute(bb, X, 1);
+			__builtin_amdgcn_sched_barrier(0);
+			p = 2;
+		} else {
+			phase2(V);
+		}
 		// steady state: only the data loads touch vector memory.  The explicit
-		// waits (no-ops at run time: at most the 4 loads of ba plus 2 stores are
-		// outstanding there) pin the loop's entry state for the compiler's
-		// wait-count pass, which otherwise merges the paths into the loop
-		// pessimistically and waits for the loads in flight.
+		// wait (a no-op at run time) pins the loop's entry state for the
+		// compiler's wait-count pass.
 		kWaitVm6();
 		for (; p + 2 < npass; p += 2) {
 			load(bb, X, p + 1);
@@ -1166,8 +1205,8 @@ __global__ __launch_bounds__(1024) void k_varlen7(V7Params P) {
 			__builtin_amdgcn_sched_barrier(0);
 			compute(ba, X, p);
 			__builtin_amdgcn_sched_barrier(0);
-			fY = fX == 64 ? build_table(Y, sbX + 64) : 0u;
-			if (fY) load(ba, Y, 0);
+			fY = fX == 64 ? build_table(V, sbX + 64) : 0u;
+			if (fY) load(ba, V, 0);
 			__builtin_amdgcn_sched_barrier(0);
 			compute(bb, X, p + 1);
 			__builtin_amdgcn_sched_barrier(0);
@@ -1175,11 +1214,16 @@ __global__ __launch_bounds__(1024) void k_varlen7(V7Params P) {
 			compute(ba, X, p);
 			__builtin_amdgcn_sched_barrier(0);
 		}
-		combine(X, fX);
+		phase1(X, fX);
 		return fY;
 	};
 
 	Tab7 t0, t1;
+	t1.wa = 0;
+	t1.f = 1024u;  // empty: the first table's "previous table" finishes nothing
+	t1.oi = 0;
+	t1.S = 0;
+	phase1(t1, 0);
 	build();
 	uint32_t sb = 0;
 	uint32_t f0 = build_table(t0, 0);
@@ -1187,22 +1231,27 @@ __global__ __launch_bounds__(1024) void k_varlen7(V7Params P) {
 	while (f0) {
 		const uint32_t f1 = run_table(t0, t1, sb, f0);
 		sb += 64;
-		if (!f1) break;
+		if (!f1) {
+			phase2(t0);
+			break;
+		}
 		f0 = run_table(t1, t0, sb, f1);
 		sb += 64;
+		if (!f0) phase2(t1);
 	}
 }
 
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
+	nwave = nwave > 16 * 1024 ? nwave : 16 * 1024;  // covers any launch geometry up to 1024 CUs
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
-	return 16 + 16 * (ntile + 1) + 4 * nwave + 12 * count + 64;
+	return 16 + 16 * (ntile + 1) + 4 * nwave + 12 * count + 256 * nwave + 64;
 }
 
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                    const DevTables* tabs, int num_cus, void* ws, hipStream_t stream) {
 	const uint64_t grid = (uint64_t)num_cus;
-	const uint64_t nwave = grid * 16;
+	const uint64_t nwave = grid * (FDBCRC_V7_THREADS / 64);
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
 	uint8_t* wp = static_cast<uint8_t*>(ws);
 	V7Params P{};
@@ -1216,13 +1265,14 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.gs = wave_tile + nwave;
 	P.cl = P.gs + count;
 	P.ct = P.cl + count;
+	P.dummy = P.ct + count;
 	// tile prefixes: each prep block sums its predecessors (up to 8192 tiles);
 	// larger batches scan the tile sums first
 	P.scanned = ntile > 8192;
 	k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.scanned) k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4);
 	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
-	k_varlen7<<<(unsigned)grid, 1024, 0, stream>>>(P);
+	k_varlen7<<<(unsigned)grid, FDBCRC_V7_THREADS, 0, stream>>>(P);
 	return 0;
 }
 
