@@ -805,7 +805,6 @@ struct V7Params {
 	bool scanned;              // tsum already holds exclusive prefixes (large batches: k_scan ran)
 	uint32_t* gs;              // first slot of each buffer
 	uint32_t* cl;              // lead edge term (team-sum form)
-	uint32_t* ct;              // tail edge term (team-sum form)
 	uint32_t* dummy;           // 64 words per wave: target of the no-op XORs
 	const DevTables* tabs;
 };
@@ -843,7 +842,9 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	if (P.scanned) {
 		pre = threadIdx.x == 0 ? P.tsum[tile] : 0;
 	} else {
+#if !(FDBCRC_EXP & 256)
 		for (uint32_t k = threadIdx.x; k < tile; k += blockDim.x) pre += P.tsum[k];
+#endif
 	}
 	for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
 	if (lane == 0) s_pre[wv] = pre;
@@ -888,35 +889,23 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		return;
 	}
 	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
-	// lead term: the lead chunk's bytes below k0 with the register ~seed
-	// injected at k0, carried to the end of the pass block (chunkpow)
-	{
-		const u32x4 ch = ld16(reinterpret_cast<const uint8_t*>(g.A));
-		uint32_t x = 0;
+#if FDBCRC_EXP & 128
+	P.cl[i] = 0; return;
+#endif
+	// lead term: the lead chunk's bytes below k0 (read only when the buffer
+	// starts inside its chunk) with the register ~seed injected at k0, carried
+	// to the end of the pass block (chunkpow).  The garbage after the buffer's
+	// end is masked by the streaming kernel (it always sits in lane 63).
+	u32x4 ch = u32x4{0u, 0u, 0u, 0u};
+	if (g.k0) ch = ld16(reinterpret_cast<const uint8_t*>(g.A));
+	uint32_t x = 0;
 #pragma unroll
-		for (uint32_t b = 0; b < 16; ++b) {
-			if (b == g.k0) x ^= s0;
-			const uint32_t byte = b < g.k0 ? (ch[b >> 2] >> (8 * (b & 3))) & 255u : 0u;
-			x = (x >> 8) ^ s4[3][(x ^ byte) & 255u];
-		}
-		P.cl[i] = vmul(&T->chunkpow[64u * (gi & 3u) + (g.lo >> 4)][0][0], x);
+	for (uint32_t b = 0; b < 16; ++b) {
+		if (b == g.k0) x ^= s0;
+		const uint32_t byte = b < g.k0 ? (ch[b >> 2] >> (8 * (b & 3))) & 255u : 0u;
+		x = (x >> 8) ^ s4[3][(x ^ byte) & 255u];
 	}
-	// tail term: the garbage bytes after P1 in the last chunk (chunk 63 of the
-	// last window)
-	uint32_t tv = 0;
-	if (g.zt) {
-		const u32x4 ch = ld16(reinterpret_cast<const uint8_t*>((P0 + len) & ~uint64_t(15)));
-		uint32_t km[4];
-		keep_below7(16u - g.zt, km);
-		uint32_t x = 0;
-#pragma unroll
-		for (int d = 0; d < 4; ++d) {
-			x ^= ch[d] & ~km[d];
-			x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
-		}
-		tv = vmul(&T->chunkpow[64u * ((gi + W - 1) & 3u) + 63u][0][0], x);
-	}
-	P.ct[i] = tv;
+	P.cl[i] = vmul(&T->chunkpow[64u * (gi & 3u) + (g.lo >> 4)][0][0], x);
 }
 
 // Streaming kernel.  Tables of 64 slots (wave-relative), passes of 4 slots.
@@ -984,7 +973,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	uint64_t B_bi0 = 0;
 	uint64_t B_wb;          // window 0 address
 	uint32_t B_g, B_W, B_f; // first slot, windows, lo | zt << 11
-	uint32_t B_cl, B_ct;
+	uint32_t B_cl;
 	uint32_t Gb1 = 0;       // wave-relative end of the batch's slots
 	uint64_t p_shift = 0;   // bytes from the end of the wave's last window to its buffer's end
 	auto build = [&]() {
@@ -992,12 +981,11 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		const uint64_t j = bi0 + lane;
 		const bool ok = j < P.count;
 		uint64_t off = 0, len = 0;
-		uint32_t g = 0xFFFFFFFFu, cl = 0, ct = 0;
+		uint32_t g = 0xFFFFFFFFu, cl = 0;
 		if (ok) {
 			v7_buffer(P, j, off, len);
 			g = P.gs[j];
 			cl = P.cl[j];
-			ct = P.ct[j];
 		}
 		const Geo7 ge = geo7(reinterpret_cast<uint64_t>(P.base) + off, len);
 		const uint32_t W = ok ? ge.W : 0u;
@@ -1007,7 +995,6 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		B_W = W;
 		B_f = ge.lo | (ge.zt << k7_ZT);
 		B_cl = cl;
-		B_ct = ct;
 		nb_bi0 = bi0 + 64;
 		// end of the slots of this batch (pieces are in order; W = 0 pieces add nothing)
 		const uint32_t e = ok ? g + W : 0u;
@@ -1035,7 +1022,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			if (shfl32(st, jj + step) <= (uint32_t)lane) jj += step;
 		const uint64_t wb = shfl64(B_wb, jj);
 		const uint32_t g = shfl32(B_g, jj), W = shfl32(B_W, jj), bf = shfl32(B_f, jj);
-		const uint32_t cl = shfl32(B_cl, jj), ct = shfl32(B_ct, jj);
+		const uint32_t cl = shfl32(B_cl, jj);
 		const uint32_t slot = ts + (uint32_t)lane;
 		const uint32_t m = slot - g;
 		const uint32_t gend = g + W - 1;                          // the buffer's last slot
@@ -1052,7 +1039,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		if ((uint32_t)lane >= k_lo && (uint32_t)lane < k_hi) {
 			X.wa = wb + 1024 * (uint64_t)m;
 			X.f = f;
-			X.S = (lead ? cl : 0u) ^ (last ? ct : 0u);
+			X.S = lead ? cl : 0u;
 			X.oi = (uint32_t)(B_bi0 - bi_w) + jj;
 		}
 		// bytes from the end of the wave's last window to the buffer's end
@@ -1098,11 +1085,19 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	auto compute = [&](Block& b, Tab7& X, uint32_t p) {
 #pragma unroll
 		for (int k = 0; k < 4; ++k) {
-			const uint32_t lo = rdlane(X.f, (int)(4 * p + (((k & 1) << 1) | (k >> 1)))) & k7_LO;
-			if (lo) {
+			const uint32_t f = rdlane(X.f, (int)(4 * p + (((k & 1) << 1) | (k >> 1))));
+			const uint32_t lo = f & k7_LO;
+			if (lo) {  // window 0: chunks before the buffer's first chunk
 				const bool z = c.ld_off < lo;
 #pragma unroll
 				for (int d = 0; d < 4; ++d) b.r[k][d] = z ? 0u : b.r[k][d];
+			}
+			const uint32_t zt = (f >> k7_ZT) & 15u;
+			if ((f & (k7_FIN | k7_PEND)) == k7_FIN && zt) {  // last window: bytes after P1 (lane 63's chunk)
+				uint32_t km[4];
+				keep_below7(16u - zt, km);
+#pragma unroll
+				for (int d = 0; d < 4; ++d) b.r[k][d] &= lane == 63 ? km[d] : ~0u;
 			}
 		}
 		unswizzle(b);
@@ -1244,7 +1239,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 	nwave = nwave > 16 * 1024 ? nwave : 16 * 1024;  // covers any launch geometry up to 1024 CUs
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
-	return 16 + 16 * (ntile + 1) + 4 * nwave + 12 * count + 256 * nwave + 64;
+	return 16 + 16 * (ntile + 1) + 4 * nwave + 8 * count + 256 * nwave + 64;
 }
 
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
@@ -1264,8 +1259,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	uint32_t* wave_tile = reinterpret_cast<uint32_t*>(P.incl + ntile + 1);  // k_scan output (unused here)
 	P.gs = wave_tile + nwave;
 	P.cl = P.gs + count;
-	P.ct = P.cl + count;
-	P.dummy = P.ct + count;
+	P.dummy = P.cl + count;
 	// tile prefixes: each prep block sums its predecessors (up to 8192 tiles);
 	// larger batches scan the tile sums first
 	P.scanned = ntile > 8192;
