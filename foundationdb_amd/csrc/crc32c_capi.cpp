@@ -190,7 +190,11 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
 #ifdef FDBCRC_DEBUG
 		crc32c_debug_bounds((uint64_t)base, (uint64_t)base + (count - 1) * stride + length);
 #endif
-		rc = launch_fixed_general(base, stride, length, count, seed, d_seeds, d_out, st->tables, st->num_cus, s);
+		void* ws = nullptr;
+		uint64_t have = 0;
+		if (int wrc = stream_workspace(st, s, varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have))
+			return wrc;
+		rc = launch_fixed_general(base, stride, length, count, seed, d_seeds, d_out, st->tables, st->num_cus, ws, s);
 #ifdef FDBCRC_DEBUG
 		(void)hipDeviceSynchronize();
 		debug_report("batch_fixed(general)");

@@ -39,8 +39,9 @@ uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                   hipStream_t stream);
+// Fixed stride, any length/alignment (same engine, same workspace size as varlen).
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
-                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus,
+                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                          hipStream_t stream);
 // v7 workspace and launch (ws: varlen7_workspace_bytes(count, nwave), 16-byte aligned)
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave);

@@ -1,85 +1,21 @@
 // Variable-length / unaligned batched CRC-32C (gfx950).
 //
 // Serves every batch the 4 KiB page kernel does not: any alignment, any
-// length (0 .. 2^64), offsets in any order (overlaps allowed), per-buffer
-// seeds.  Reference semantics: crc32c_append (contrib/crc32/crc32c.cpp:346-356)
-// per buffer; the chained/streaming callers (fdbrpc/FileTransfer.cpp:29-37)
-// reduce to the same thing through crc32c_combine.
-//
-// Work decomposition -- balanced by BYTES, not by buffers:
-//   k_plan   one workgroup per tile of 256 buffers: tile byte sums; zeroes out[]
-//   k_scan   one workgroup: exclusive prefix over tiles, total bytes, quantum
-//            Q = ceil(total / waves), and for each wave the tile holding its
-//            first byte (w*Q)
-//   k_varlen every wave owns the byte range [w*Q, (w+1)*Q) of the buffers laid
-//            end to end in index order.  It walks the 4 KiB blocks of the
-//            buffer pieces inside its range as ONE stream, with the next
-//            block's loads always in flight (also across buffer boundaries),
-//            and the per-buffer metadata fetched 64 buffers at a time.
-// A buffer cut by a range boundary is checksummed in pieces: each piece's raw
-// register is multiplied by x^(8*(bytes after the piece)) and XORed into
-// out[] with atomicXor (linearity of CRC, the same identity as
-// crc32c_combine); whole buffers are stored directly.
-//
-// Inside a piece [P0, P1): the 16-byte aligned chunks covering it are read as
-// blocks aligned to the piece's aligned END (front padding of the first block
-// reads as zero and costs nothing, see crc32c_kernels.hip); bytes outside
-// [P0, P1) in the boundary chunks are masked to zero.  The seed enters as the
-// register value at P0 -- XORed into the four message bytes at P0 -- and the
-// z = (16 - P1 % 16) % 16 zero bytes masked after P1 are removed by a final
-// multiply with x^(-8z).
+// length, offsets in any order (overlaps allowed), per-buffer seeds, and
+// fixed-stride batches of odd lengths.  Reference semantics: crc32c_append
+// (contrib/crc32/crc32c.cpp:346-356) per buffer; the chained/streaming callers
+// (fdbrpc/FileTransfer.cpp:29-37) reduce to the same thing through
+// crc32c_combine.  The design (v7) is described where its kernels start below.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "crc32c_common.h"
 
-#ifndef FDBCRC_V7
-#define FDBCRC_V7 1  // varlen batches: 1 = v7 (prep + window-slot streaming), 0 = v4 (two sweeps)
-#endif
-#ifndef FDBCRC_EXP
-#define FDBCRC_EXP 0  // development timing experiments only (wrong results when set)
-#endif
-
 namespace fdbcrc {
 
-constexpr uint32_t kTile = 256;               // buffers per planning tile
-constexpr uint64_t kSmall = 1024;             // pieces whose aligned span fits one 1 KiB quarter
-
-struct VarlenParams {
-	const uint8_t* base;
-	const uint64_t* offsets;   // nullptr: fixed mode, buffer i at base + i*stride
-	const uint64_t* lengths;   // nullptr: fixed mode, every buffer `length` bytes
-	uint64_t stride, length, count;
-	uint32_t seed;
-	const uint32_t* seeds;
-	uint32_t* out;
-	const uint64_t* prefix;      // varlen: exclusive tile prefix [T+1]
-	const uint32_t* wave_tile;   // varlen: tile of each wave's first byte
-	const uint64_t* hdr;         // varlen: [0] total bytes, [1] quantum
-	uint64_t total, quantum;     // fixed mode (host-computed)
-	const DevTables* tabs;
-};
-
 // ---------------------------------------------------------------------------
-// planning
+// tile scan (batches of more than 8192 tiles)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_plan(const uint64_t* __restrict__ lengths, uint64_t count,
-                                              uint64_t* __restrict__ tile_sum, uint32_t* __restrict__ out) {
-	__shared__ uint64_t part[4];
-	const uint64_t i = (uint64_t)blockIdx.x * kTile + threadIdx.x;
-	uint64_t v = 0;
-	if (i < count) {
-		v = lengths[i];
-		out[i] = 0u;  // split buffers accumulate with atomicXor
-	}
-	// wave reduction (64 lanes) then across the 4 waves
-	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
-	__syncthreads();
-	if (threadIdx.x == 0) tile_sum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
-}
-
-// Single workgroup.  ntile tiles, nwave waves in the main grid.
 // quantum: ceil(total / nwave), at least qmin, rounded up to a multiple of qalign
 __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, uint64_t ntile,
                                                uint32_t* __restrict__ wave_tile, uint64_t nwave,
@@ -165,7 +101,7 @@ __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, ui
 }
 
 // ---------------------------------------------------------------------------
-// main kernel helpers
+// helpers
 // ---------------------------------------------------------------------------
 // Uniform (wave-wide) multiply through nibble tables in global memory: the
 // value is uniform, so these are scalar-cache loads, off the LDS path.
@@ -189,72 +125,6 @@ __device__ uint32_t mul_xpow(const DevTables* __restrict__ t, uint32_t v, uint64
 	return v;
 }
 
-// One piece of one buffer: bytes [P0, P1) of buffer `buf`.
-struct Piece {
-	uint64_t buf;
-	uint64_t P0, P1;
-	uint64_t after;     // bytes of the buffer after P1
-	uint32_t seed;
-	uint32_t flags;     // bit0: piece starts the buffer, bit1: buffer is split
-};
-
-__device__ __forceinline__ uint64_t span_aligned(const Piece& p) {
-	return ((p.P1 + 15) & ~uint64_t(15)) - (p.P0 & ~uint64_t(15));
-}
-
-// Edge fix-ups of a piece, precomputed once (uniform):
-//   lead chunk  (P0 & ~15): keep bytes >= P0%16, XOR the register value ~seed
-//                           into the four message bytes at P0 (first piece)
-//   spill chunk (lead+16):  the seed bytes that cross into the next chunk
-//   tail chunk ((P1-1)&~15): keep bytes < P1 - tail
-struct Edges {
-	uint64_t lead, tail;
-	uint32_t lm[4], inj[4], tm[4], spill;
-	bool any_lead, any_tail, any_spill;
-};
-
-__device__ __forceinline__ Edges make_edges(const Piece& p) {
-	Edges e;
-	const uint32_t k0 = (uint32_t)(p.P0 & 15);
-	const uint32_t k1 = (uint32_t)((p.P1 - 1) & 15) + 1;
-	const uint32_t s0 = (p.flags & 1) ? ~p.seed : 0u;
-	const Masks m = edge_masks(rdfirst(k0), rdfirst(k1), rdfirst(s0));
-	e.lead = p.P0 & ~uint64_t(15);
-	e.tail = (p.P1 - 1) & ~uint64_t(15);
-#pragma unroll
-	for (int d = 0; d < 4; ++d) {
-		e.lm[d] = m.lm[d];
-		e.tm[d] = m.tm[d];
-		e.inj[d] = m.inj[d];
-	}
-	e.spill = m.spill;
-	e.any_lead = k0 != 0 || (p.flags & 1);
-	e.any_tail = k1 != 16;
-	e.any_spill = e.spill != 0;
-	return e;
-}
-
-// Apply the edge fix-ups to the chunk this lane loaded at `ca` for one load
-// whose 1 KiB window starts at `w` (uniform early-out when the window has no edge).
-__device__ __forceinline__ void fix_edges(u32x4& r, uint64_t w, uint64_t ca, const Edges& e) {
-	const bool wl = e.any_lead && e.lead >= w && e.lead < w + 1024;
-	const bool wt = e.any_tail && e.tail >= w && e.tail < w + 1024;
-	const bool ws = e.any_spill && e.lead + 16 >= w && e.lead + 16 < w + 1024;
-	if (!(wl || wt || ws)) return;
-	const bool il = ca == e.lead, it = ca == e.tail, is = ca == e.lead + 16;
-#pragma unroll
-	for (int d = 0; d < 4; ++d) {
-		uint32_t m = (il ? e.lm[d] : ~0u) & (it ? e.tm[d] : ~0u);
-		uint32_t inj = il ? e.inj[d] : ((is && d == 0) ? e.spill : 0u);
-		r[d] = (r[d] & m) ^ inj;
-	}
-}
-
-__device__ __forceinline__ u32x4 load_chunk_if(uint64_t ca, const Piece& p) {
-	const bool ok = ca + 16 > p.P0 && ca < p.P1;
-	return ok ? ld16(reinterpret_cast<const uint8_t*>(ca)) : u32x4{0u, 0u, 0u, 0u};
-}
-
 // Register chain over the lane's 64 contiguous bytes (layout B, 4-byte
 // slicing), each step folding in the next word (word_step4_next).
 __device__ __forceinline__ uint32_t chain64_b(const uint32_t* lds, uint32_t s, const Block& b, uint32_t c4) {
@@ -263,41 +133,6 @@ __device__ __forceinline__ uint32_t chain64_b(const uint32_t* lds, uint32_t s, c
 	for (int w = 0; w < 16; ++w) s = word_step4_next(lds, s, w < 15 ? b.r[(w + 1) >> 2][(w + 1) & 3] : 0u, c4);
 	return s;
 }
-// Two independent chains interleaved (ILP 2).
-__device__ __forceinline__ void chain64_b2(const uint32_t* lds, const Block& b0, const Block& b1, uint32_t c4,
-                                           uint32_t& y0, uint32_t& y1) {
-	y0 = b0.r[0][0];
-	y1 = b1.r[0][0];
-#pragma unroll
-	for (int w = 0; w < 16; ++w) {
-		y0 = word_step4_next(lds, y0, w < 15 ? b0.r[(w + 1) >> 2][(w + 1) & 3] : 0u, c4);
-		y1 = word_step4_next(lds, y1, w < 15 ? b1.r[(w + 1) >> 2][(w + 1) & 3] : 0u, c4);
-	}
-}
-
-// ---------------------------------------------------------------------------
-// main kernel
-// ---------------------------------------------------------------------------
-// Per-lane metadata of one BATCH of 64 consecutive buffers: lane j describes
-// the piece of buffer bi0 + j that lies in this wave's byte range.
-constexpr uint32_t kNone = 0, kDirect = 1, kSmallC = 2, kLargeC = 3;  // info bits 0-1
-constexpr uint32_t kFirst = 4, kSplit = 8;                              // info bits 2, 3
-struct Meta {
-	uint64_t P0, P1;   // piece [P0, P1), device addresses
-	uint64_t after;    // bytes of the buffer after P1
-	uint32_t s0;       // register value entering at P0: ~seed for a buffer's first piece, else 0
-	uint32_t info;
-	uint32_t geo;      // k0 = P0%16 | k1 = (P1-1)%16+1 << 8 | lead chunk offset << 16, inside the
-	                   // piece's first 1 KiB window (small) or 4 KiB block (large)
-};
-// Uniform state of one ring slot (a built batch).
-struct Slot {
-	uint64_t bi0;
-	uint64_t mask;      // pieces of the current sweep's class not yet taken
-	uint32_t pending;   // taken work items not yet computed
-	bool valid;
-};
-
 __device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d); }
 
 // Inclusive prefix sum of a 64-bit value over the wave.
@@ -326,389 +161,6 @@ __device__ __forceinline__ uint32_t vmul(const uint32_t* tab, uint32_t v) {
 #pragma unroll
 	for (int n = 0; n < 8; ++n) r ^= gld32(tab + n * 16 + ((v >> (4 * n)) & 15u));
 	return r;
-}
-
-__global__ __launch_bounds__(1024) void k_varlen(VarlenParams P, const DevTables* __restrict__ T) {
-	__shared__ uint32_t lds[kLdsBytesB / 4];
-	const LaneCtx c = make_ctx();
-	const int lane = c.lane;
-	const uint32_t col4 = (lane & 31) * 4;
-	const uint32_t c4 = col4 | 0x10000u;
-	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
-	fill_lds_b(lds, T);
-	const uint64_t wpb = blockDim.x >> 6;
-	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
-	const uint64_t w = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
-	const bool fixed = P.offsets == nullptr;
-	uint64_t total = P.total, Q = P.quantum;
-	if (!fixed) {  // planner output (global address space)
-		typedef __attribute__((address_space(1))) const uint64_t g_u64;
-		const g_u64* h = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
-		total = rdfirst64(h[0]);
-		Q = rdfirst64(h[1]);
-	}
-	const uint64_t lo = w * Q;
-	const uint64_t hi = w + 1 == nwave ? ~uint64_t(0) : lo + Q;
-	if (lo > total || P.count == 0) return;
-
-	// first batch of the range: the planning tile holding byte lo (buffers
-	// before lo are classified kNone by build())
-	uint64_t first_bi0, first_start;
-	if (fixed) {
-		first_bi0 = P.length ? lo / P.length : 0;
-		if (P.length == 0) first_bi0 = 0;
-		first_start = first_bi0 * P.length;
-	} else {
-		const uint64_t t = P.wave_tile[w];
-		first_bi0 = t * kTile;
-		first_start = P.prefix[t];
-	}
-
-	// ---- batch builder (lane-parallel) ----------------------------------
-	uint64_t nb_bi0 = first_bi0, nb_start = first_start;
-	bool more = true;
-	auto build = [&](Meta& m, Slot& s, uint32_t want) {
-		const uint64_t bi0 = nb_bi0;
-		const uint64_t j = bi0 + lane;
-		const bool ok = j < P.count;
-		uint64_t off = 0, len = 0, st;
-		uint32_t sd = P.seed;
-		if (fixed) {
-			off = j * P.stride;
-			len = ok ? P.length : 0;
-			st = j * P.length;
-			nb_start = (bi0 + 64) * P.length;
-		} else {
-			if (ok) {
-				off = P.offsets[j];
-				len = P.lengths[j];
-			}
-			const uint64_t incl = scan64(len, lane);
-			st = nb_start + incl - len;
-			nb_start += rdlane64(incl, 63);
-		}
-		if (P.seeds && ok) sd = P.seeds[j];
-		nb_bi0 = bi0 + 64;
-		more = nb_bi0 < P.count && nb_start < hi;
-		const bool in = ok && st < hi && (st + len > lo || (len == 0 && st >= lo));
-		const uint64_t a = lo > st ? lo - st : 0;
-		const uint64_t b = in ? (hi - st < len ? hi - st : len) : 0;
-		const uint64_t q = reinterpret_cast<uint64_t>(P.base) + off;
-		m.P0 = q + a;
-		m.P1 = q + b;
-		m.after = in ? len - b : 0;
-		m.s0 = a == 0 ? ~sd : 0u;
-		uint32_t cls = kNone;
-		const uint64_t span = ((m.P1 + 15) & ~uint64_t(15)) - (m.P0 & ~uint64_t(15));
-		if (in) cls = b - a < 16 ? kDirect : (span <= kSmall ? kSmallC : kLargeC);
-		m.geo = (uint32_t)(m.P0 & 15) | (((uint32_t)((m.P1 - 1) & 15) + 1) << 8) |
-		        (((uint32_t)(-span) & (cls == kSmallC ? 1023u : 4095u)) << 16);
-		m.info = cls | (a == 0 ? kFirst : 0u) | ((a != 0 || b != len) ? kSplit : 0u);
-		s.bi0 = bi0;
-		s.mask = __ballot(cls == want);
-		s.pending = 0;
-		s.valid = true;
-	};
-	// Finish the pieces of class `want` (kSmallC also finishes kDirect) of a
-	// batch: remove the team offset and the z zero bytes (corr tables), shift
-	// split pieces by the bytes after them, store or XOR-merge.
-	auto finalize = [&](const Meta& m, uint64_t bi0, uint32_t x, uint32_t t, uint32_t want) {
-		const uint32_t cls = m.info & 3;
-		const bool mine = cls == want || (want == kSmallC && cls == kDirect);
-		uint32_t r = x;
-		if (mine && cls == kDirect) {  // < 16 bytes or empty: byte-serial per lane
-			r = m.s0;
-			for (uint64_t p = m.P0; p < m.P1; ++p) {
-				const uint32_t y = r ^ ld1(reinterpret_cast<const uint8_t*>(p));
-				r = (r >> 8) ^ lds_rd(lds, __builtin_amdgcn_perm(y, c4, 0x0c020400u) + 128);
-			}
-		} else if (mine) {
-			r = vmul(&T->corr[t][(uint32_t)(-m.P1 & 15)][0][0], x);
-		}
-		uint64_t am = __ballot(mine && m.after != 0);
-		while (am) {  // split pieces ending before their buffer does: at most one per wave
-			const int k = __builtin_ctzll(am);
-			am &= am - 1;
-			const uint32_t v = mul_xpow(T, rdlane(r, k), rdlane64(m.after, k));
-			r = lane == k ? v : r;
-		}
-		if (mine) {
-			uint32_t* o = P.out + bi0 + lane;
-			if (m.info & kSplit) atomicXor(o, (m.info & kFirst) ? ~r : r);
-			else *o = ~r;
-		}
-	};
-
-	Meta m0, m1;
-	Slot s0, s1;
-	uint32_t x0 = 0, x1 = 0, t0 = 0, t1 = 0;  // per-lane results awaiting finalize
-	auto reset = [&](uint32_t want) {
-		nb_bi0 = first_bi0;
-		nb_start = first_start;
-		more = true;
-		build(m0, s0, want);
-		s1.valid = false;
-		s1.mask = 0;
-		s1.pending = 0;
-		if (more) build(m1, s1, want);
-	};
-	// slot with work left, older batch first (-1: none)
-	auto pick = [&]() -> int {
-		const bool a = s0.valid && s0.mask, b = s1.valid && s1.mask;
-		if (a && b) return s0.bi0 < s1.bi0 ? 0 : 1;
-		return a ? 0 : (b ? 1 : -1);
-	};
-	auto deposit = [&](int slot, int j, uint32_t v, uint32_t t) {
-		if (slot) {
-			x1 = lane == j ? v : x1;
-			t1 = lane == j ? t : t1;
-		} else {
-			x0 = lane == j ? v : x0;
-			t0 = lane == j ? t : t0;
-		}
-	};
-	// finalize + rebuild every slot whose work is done; `busy` = slot of a
-	// large piece that still has blocks to take (-1: none)
-	auto retire = [&](uint32_t want, int busy) {
-		if (s0.valid && !s0.mask && !s0.pending && busy != 0) {
-			finalize(m0, s0.bi0, x0, t0, want);
-			s0.valid = false;
-			if (more) build(m0, s0, want);
-		}
-		if (s1.valid && !s1.mask && !s1.pending && busy != 1) {
-			finalize(m1, s1.bi0, x1, t1, want);
-			s1.valid = false;
-			if (more) build(m1, s1, want);
-		}
-	};
-
-#if !(FDBCRC_EXP & 8)
-	// ======================= sweep 1: small pieces, four per pass ==========
-	// Load k (k = 0..3) fetches quarter qk = {0,2,1,3}[k] = 16-lane team qk
-	// after unswizzle; team t checksums piece t inside the 1 KiB window ending
-	// at its aligned end.  Lane tables multiply lane l by x^(8*64*(63-l)), so
-	// team t's row sum carries an extra x^(8*1024*(3-t)), removed together
-	// with the z trailing zeros by the corr tables in finalize().
-	{
-		struct Item {
-			int slot, n;
-			int j[4];
-		};
-		auto take = [&](Item& it) {
-			it.n = 0;
-			const int s = pick();
-			if (s < 0) return;
-			Slot& S = s ? s1 : s0;
-			it.slot = s;
-			uint64_t mk = S.mask;
-#pragma unroll
-			for (int t = 0; t < 4; ++t) {
-				if (mk) {
-					it.j[t] = __builtin_ctzll(mk);
-					mk &= mk - 1;
-					it.n = t + 1;
-				}
-			}
-			S.mask = mk;
-			S.pending += 1;
-		};
-		auto win = [](uint64_t P1) -> uint64_t { return ((P1 + 15) & ~uint64_t(15)) - 1024; };
-		const int quarter[4] = {0, 2, 1, 3};
-		// the window ends at the piece's aligned end, so chunk ld_off belongs
-		// to the piece iff ld_off >= the lead chunk's offset
-		auto load_item = [&](Block& b, const Item& it) {
-#pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const int t = quarter[k];
-				b.r[k] = u32x4{0u, 0u, 0u, 0u};
-				if (t < it.n) {
-					const Meta& m = it.slot ? m1 : m0;
-					const uint64_t w0 = win(rdlane64(m.P1, it.j[t]));
-					const uint32_t lead_rel = rdlane(m.geo, it.j[t]) >> 16;
-					if (c.ld_off >= lead_rel) b.r[k] = ld16(reinterpret_cast<const uint8_t*>(w0 + c.ld_off));
-				}
-			}
-		};
-		// lead chunk: mask + seed; next chunk: seed spill; lane 63 holds the
-		// window's last chunk = the tail chunk
-		auto fix_item = [&](u32x4& r, int slot, int j) {
-			const Meta& m = slot ? m1 : m0;
-			const uint32_t geo = rdlane(m.geo, j);
-			const Masks mk = edge_masks(geo & 15u, (geo >> 8) & 31u, rdlane(m.s0, j));
-			const uint32_t lead_rel = geo >> 16;
-			const bool il = c.ld_off == lead_rel, is = c.ld_off == lead_rel + 16, it = lane == 63;
-#pragma unroll
-			for (int d = 0; d < 4; ++d) {
-				const uint32_t mm = il ? mk.lm[d] : (it ? mk.tm[d] : ~0u);
-				const uint32_t x = il ? mk.inj[d] : ((d == 0 && is) ? mk.spill : 0u);
-				r[d] = (r[d] & mm) ^ x;
-			}
-		};
-		reset(kSmallC);
-		Item cur, nxt;
-		cur.n = 0;
-		Block b, nb;
-		for (;;) {
-			take(nxt);
-			if (nxt.n) load_item(nb, nxt);
-			__builtin_amdgcn_sched_barrier(0);
-			if (cur.n) {
-#pragma unroll
-				for (int k = 0; k < 4; ++k) {
-					const int t = quarter[k];
-					if (t < cur.n) fix_item(b.r[k], cur.slot, cur.j[t]);
-				}
-				unswizzle(b);
-				const uint32_t x = row_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
-#pragma unroll
-				for (int t = 0; t < 4; ++t)
-					if (t < cur.n) deposit(cur.slot, cur.j[t], rdlane(x, 16 * t), (uint32_t)t);
-				if (cur.slot) s1.pending -= 1; else s0.pending -= 1;
-			}
-			__builtin_amdgcn_sched_barrier(0);
-			retire(kSmallC, -1);
-			if (!nxt.n && !cur.n && !s0.valid && !s1.valid) break;
-			cur = nxt;
-			b = nb;
-		}
-	}
-
-#endif
-#if !(FDBCRC_EXP & 16)
-	// ======================= sweep 2: large pieces, 4 KiB blocks ===========
-	// Blocks aligned to the piece's aligned end, taken two at a time (two
-	// register chains interleave, next two blocks in flight).  Each block's
-	// register sum is reduced to a uniform value and folded Horner-style with
-	// x^(8*4096); the piece total goes to its batch lane for finalize().
-	{
-		struct Blk {
-			uint64_t bb;       // block address (aligned to the piece's aligned end)
-			int slot, j;
-			uint32_t flags;    // bit0 valid, bit1 first block, bit2 last block, bit3 holds an edge,
-			                   // bit4 block 1 holding the seed spill
-		};
-		// active piece (uniform)
-		bool act = false;
-		int a_slot = 0, a_j = 0;
-		uint64_t a_blk = 0, a_nblk = 0, a_vbase = 0, a_P0 = 0, a_P1 = 0;
-		uint32_t a_geo = 0;
-		const uint32_t koff[4] = {0, 2048, 1024, 3072};
-		// take the next block of the stream and issue its loads
-		auto take = [&](Blk& d, Block& b) {
-			d.flags = 0;
-			if (!act) {
-				const int s = pick();
-				if (s < 0) {
-#pragma unroll
-					for (int k = 0; k < 4; ++k) b.r[k] = u32x4{0u, 0u, 0u, 0u};
-					return;
-				}
-				Slot& S = s ? s1 : s0;
-				const Meta& m = s ? m1 : m0;
-				a_slot = s;
-				a_j = __builtin_ctzll(S.mask);
-				S.mask &= S.mask - 1;
-				a_P0 = rdlane64(m.P0, a_j);
-				a_P1 = rdlane64(m.P1, a_j);
-				a_geo = rdlane(m.geo, a_j);
-				const uint64_t end = (a_P1 + 15) & ~uint64_t(15);
-				a_nblk = (end - (a_P0 & ~uint64_t(15)) + 4095) >> 12;
-				a_vbase = end - 4096 * a_nblk;
-				a_blk = 0;
-				act = true;
-			}
-			const uint64_t bb = a_vbase + 4096 * a_blk;
-			d.bb = bb;
-			d.slot = a_slot;
-			d.j = a_j;
-			// edges: lead chunk (+ seed) in block 0, seed spill in block 0 or 1
-			// when k0 > 12, tail chunk (k1 < 16) at offset 4080 of the last block
-			const uint32_t k0 = a_geo & 15u, k1 = (a_geo >> 8) & 31u, o = a_geo >> 16;
-			const bool spill1 = k0 > 12 && o == 4080;
-			d.flags = 1u | (a_blk == 0 ? 2u : 0u) | (a_blk + 1 == a_nblk ? 4u : 0u) |
-			          ((a_blk == 0 || (a_blk == 1 && spill1) || (a_blk + 1 == a_nblk && k1 != 16)) ? 8u : 0u) |
-			          (a_blk == 1 && spill1 ? 16u : 0u);
-			if (a_slot) s1.pending += 1; else s0.pending += 1;
-			if (++a_blk == a_nblk) act = false;
-			if (bb >= a_P0 && bb + 4096 <= a_P1) {
-				load_block(b, reinterpret_cast<const uint8_t*>(bb), c.ld_off);
-			} else {
-				Piece p;
-				p.P0 = a_P0;
-				p.P1 = a_P1;
-#pragma unroll
-				for (int k = 0; k < 4; ++k) b.r[k] = load_chunk_if(bb + koff[k] + c.ld_off, p);
-			}
-		};
-		// edge fix-ups: the lead chunk is in block 0, its seed spill in block 0
-		// or 1, the tail chunk in the last block
-		auto edges = [&](Block& b, const Blk& d) {
-			if (!(d.flags & 8u)) return;
-			const Meta& m = d.slot ? m1 : m0;
-			const uint32_t geo = rdlane(m.geo, d.j);
-			const uint32_t k0 = geo & 15u, k1 = (geo >> 8) & 31u, o = geo >> 16;
-			const Masks mk = edge_masks(k0, k1, rdlane(m.s0, d.j));
-			const bool first = d.flags & 2u, last = d.flags & 4u;
-			// block offsets of the edge chunks (0xFFFF: none in this block)
-			const uint32_t ol = first ? o : 0xFFFFu;
-			const uint32_t os = (d.flags & 16u) ? 0u : ((first && k0 > 12 && o + 16 < 4096) ? o + 16 : 0xFFFFu);
-			const uint32_t ot = (last && k1 != 16) ? 4080u : 0xFFFFu;
-#pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const uint32_t w = koff[k];
-				const bool any = (ol - w < 1024u) || (os - w < 1024u) || (ot - w < 1024u);
-				if (!any) continue;
-				const uint32_t off = w + c.ld_off;
-				const bool il = off == ol, is = off == os, it = off == ot;
-#pragma unroll
-				for (int dd = 0; dd < 4; ++dd) {
-					const uint32_t mm = (il ? mk.lm[dd] : ~0u) & (it ? mk.tm[dd] : ~0u);
-					const uint32_t x = il ? mk.inj[dd] : ((dd == 0 && is) ? mk.spill : 0u);
-					b.r[k][dd] = (b.r[k][dd] & mm) ^ x;
-				}
-			}
-		};
-		uint32_t acc = 0;
-		auto fold = [&](const Blk& d, uint32_t v) {
-			if (!(d.flags & 1u)) return;
-#if FDBCRC_EXP & 2
-			acc = (d.flags & 2u) ? v : acc ^ v;
-#else
-			acc = (d.flags & 2u) ? v : umul(T->block, acc) ^ v;
-#endif
-			if (d.flags & 4u) deposit(d.slot, d.j, acc, 3u);
-			if (d.slot) s1.pending -= 1; else s0.pending -= 1;
-		};
-		reset(kLargeC);
-		Blk cur[2], nxt[2];
-		cur[0].flags = cur[1].flags = 0;
-		Block b[2], nb[2];
-		for (;;) {
-			take(nxt[0], nb[0]);
-			take(nxt[1], nb[1]);
-			__builtin_amdgcn_sched_barrier(0);
-			if (cur[0].flags) {
-				edges(b[0], cur[0]);
-				edges(b[1], cur[1]);
-				unswizzle(b[0]);
-				unswizzle(b[1]);
-				uint32_t y0, y1;
-				chain64_b2(lds, b[0], b[1], c4, y0, y1);
-				const uint32_t v0 = wave_xor(mul_nibbles(lds, y0, c_lane));
-				const uint32_t v1 = wave_xor(mul_nibbles(lds, y1, c_lane));
-				fold(cur[0], v0);
-				fold(cur[1], v1);
-			}
-			__builtin_amdgcn_sched_barrier(0);
-			retire(kLargeC, act ? a_slot : -1);
-			if (!nxt[0].flags && !cur[0].flags && !s0.valid && !s1.valid) break;
-			cur[0] = nxt[0];
-			cur[1] = nxt[1];
-			b[0] = nb[0];
-			b[1] = nb[1];
-		}
-	}
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -842,9 +294,7 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	if (P.scanned) {
 		pre = threadIdx.x == 0 ? P.tsum[tile] : 0;
 	} else {
-#if !(FDBCRC_EXP & 256)
 		for (uint32_t k = threadIdx.x; k < tile; k += blockDim.x) pre += P.tsum[k];
-#endif
 	}
 	for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
 	if (lane == 0) s_pre[wv] = pre;
@@ -889,9 +339,6 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		return;
 	}
 	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
-#if FDBCRC_EXP & 128
-	P.cl[i] = 0; return;
-#endif
 	// lead term: the lead chunk's bytes below k0 (read only when the buffer
 	// starts inside its chunk) with the register ~seed injected at k0, carried
 	// to the end of the pass block (chunkpow).  The garbage after the buffer's
@@ -940,7 +387,6 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
 	fill_lds_b(lds, T);
 	const uint64_t wpb = blockDim.x >> 6;
-	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
 	const uint64_t w = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
 	typedef __attribute__((address_space(1))) const uint64_t g_u64;
 	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
@@ -1027,7 +473,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		const uint32_t m = slot - g;
 		const uint32_t gend = g + W - 1;                          // the buffer's last slot
 		const uint32_t wend = gend < hi_s - 1 ? gend : hi_s - 1;  // ... in this wave
-		const bool lead = m == 0, last = m + 1 == W;
+		const bool lead = m == 0;
 		const bool fin = slot == wend, pend = fin && wend != gend;
 		const bool split = g < lo_s || g + W > hi_s;
 		const bool cont = g < ts;
@@ -1273,58 +719,20 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) {
-#if FDBCRC_V7
-	return varlen7_workspace_bytes(count, nwave);
-#else
-	const uint64_t ntile = (count + kTile - 1) / kTile;
-	return 16 + 8 * (ntile + 1) + 4 * nwave + 64;
-#endif
-}
+uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) { return varlen7_workspace_bytes(count, nwave); }
 
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                   hipStream_t stream) {
-#if FDBCRC_V7
 	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream);
-#endif
-	const uint64_t grid = (uint64_t)num_cus;
-	const uint64_t nwave = grid * 16;
-	const uint64_t ntile = (count + kTile - 1) / kTile;
-	uint8_t* w = static_cast<uint8_t*>(ws);
-	uint64_t* hdr = reinterpret_cast<uint64_t*>(w);
-	uint64_t* prefix = reinterpret_cast<uint64_t*>(w + 16);
-	uint32_t* wave_tile = reinterpret_cast<uint32_t*>(w + 16 + 8 * (ntile + 1));
-	k_plan<<<(unsigned)ntile, 256, 0, stream>>>(lengths, count, prefix, out);
-	k_scan<<<1, 1024, 0, stream>>>(prefix, ntile, wave_tile, nwave, hdr);
-	VarlenParams P{};
-	P.base = base; P.offsets = offsets; P.lengths = lengths; P.count = count;
-	P.seed = seed; P.seeds = seeds; P.out = out;
-	P.prefix = prefix; P.wave_tile = wave_tile; P.hdr = hdr; P.tabs = tabs;
-	k_varlen<<<(unsigned)grid, 1024, 0, stream>>>(P, tabs);
-	return 0;
 }
 
+// Fixed stride, any length and alignment: the same engine with metadata
+// computed on the fly.
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
-                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus,
+                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                          hipStream_t stream) {
-	const uint64_t grid = (uint64_t)num_cus;
-	const uint64_t nwave = grid * 16;
-	VarlenParams P{};
-	P.base = base; P.stride = stride; P.length = length; P.count = count;
-	P.seed = seed; P.seeds = seeds; P.out = out; P.tabs = tabs;
-	P.total = count * length;
-	const uint64_t per = (P.total + nwave - 1) / nwave;
-	if (length <= per) {
-		// whole buffers per wave: no piece ever straddles two waves
-		P.quantum = (per + length - 1) / length * length;
-	} else {
-		// long buffers: cut into 4 KiB-multiple pieces merged with atomicXor
-		P.quantum = per < 4096 ? 4096 : (per + 4095) & ~uint64_t(4095);
-		if (hipMemsetAsync(out, 0, 4 * count, stream) != hipSuccess) return -1;
-	}
-	k_varlen<<<(unsigned)grid, 1024, 0, stream>>>(P, tabs);
-	return 0;
+	return launch_varlen7(base, nullptr, nullptr, stride, length, count, seed, seeds, out, tabs, num_cus, ws, stream);
 }
 
 #ifdef FDBCRC_DEBUG

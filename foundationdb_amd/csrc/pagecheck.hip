@@ -218,14 +218,16 @@ __global__ void k_dq_final(const uint8_t* __restrict__ pages, uint64_t count, ui
 // Launchers
 // ---------------------------------------------------------------------------
 uint64_t workspace_bytes(uint64_t count) {
-	// counters, two u32 lists, u32 CRC results, u64 XXH3 results
-	return 64 + 4 * count + 4 * count + 4 * count + 8 * count + 64;
+	// counters, two u32 lists, u32 CRC results, u64 XXH3 results, and the
+	// general engine's workspace (page sizes other than 4 KiB)
+	return 64 + 4 * count + 4 * count + 4 * count + 8 * count + 64 + fdbcrc::varlen7_workspace_bytes(count, 0) + 16;
 }
 
 struct Ws {
 	unsigned long long* ctr;
 	uint32_t *list_a, *list_b, *crc_out;
 	uint64_t* xxh_out;
+	void* eng;
 };
 static Ws carve(void* ws, uint64_t count) {
 	uint8_t* p = static_cast<uint8_t*>(ws);
@@ -239,6 +241,8 @@ static Ws carve(void* ws, uint64_t count) {
 	w.list_b = reinterpret_cast<uint32_t*>(p);
 	p += 4 * count;
 	w.crc_out = reinterpret_cast<uint32_t*>(p);
+	p += 4 * count;
+	w.eng = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
 	return w;
 }
 
@@ -257,7 +261,7 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 		k_sq_after_crc<<<blocks(count), 256, 0, s>>>(pages, ps, w.list_a, w.ctr, w.crc_out, status);
 	} else {
 		// other page sizes: every page through the general fixed-stride engine
-		fdbcrc::launch_fixed_general(pages, ps, ps - 8, count, 0xFDBEEFDBu, nullptr, w.crc_out, tabs, num_cus, s);
+		fdbcrc::launch_fixed_general(pages, ps, ps - 8, count, 0xFDBEEFDBu, nullptr, w.crc_out, tabs, num_cus, w.eng, s);
 		k_sq_after_crc_all<<<blocks(count), 256, 0, s>>>(pages, ps, count, w.crc_out, status);
 	}
 	k_sq_xxh_classify<<<blocks(count), 256, 0, s>>>(pages, ps, count, status, w.list_b, w.ctr);
