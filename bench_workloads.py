@@ -124,7 +124,7 @@ def _spot_check(buf, offsets, lengths, seed, got, n=512):
 
 
 class VarLen:
-    kernel_name = "fdbcrc::k_varlen (+ k_plan, k_scan)"
+    kernel_name = "fdbcrc::k_varlen7 (+ k_v7count, k_v7prep)"
 
     def __init__(self, dev, rank, lengths, align, desc, seed=0):
         self.dev, self.seed = dev, seed
@@ -192,7 +192,7 @@ class HostChunks:
     """configs[4], host-to-host: backup chunks in pinned host memory, checksummed
     through the pinned H2D -> kernel -> D2H pipeline (4 streams, 64 MiB segments).
     The rate includes both PCIe copies; it is PCIe-bound by design."""
-    kernel_name = "host pipeline (H2D + fdbcrc::k_varlen + D2H)"
+    kernel_name = "host pipeline (H2D + fdbcrc::k_varlen7 + D2H)"
     host_timed = True
     pcie_peak_gbs = 63.0  # PCIe Gen5 x16 per direction, MI355X_MICROARCH.md
 

@@ -12,7 +12,7 @@ timeout -k 10 400 python -m pytest tests -m gpu -q > $R/pytest_gpu.txt 2>&1 || {
 tail -1 $R/pytest_gpu.txt
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $R/smoke.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $R/bench_pages4k.json 2> $R/bench_pages4k.err || exit 1
-for w in pages8k zipf chunks chunks-host xxh3-pages4k; do
+for w in pages8k zipf chunks chunks-host pages4k-host xxh3-pages4k; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --cpu-seconds 5 > $R/bench_$w.json 2> $R/bench_$w.err || exit 1
 done
 echo benches done
