@@ -1,7 +1,7 @@
 """Tabulate gpurun_out/pmcsq/<mode>/*_counter_collection.csv per kernel (development)."""
 import collections, csv, glob, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-UNITS = {"pages4k": 1 << 20, "v4096": 1 << 18, "v1024": 1 << 20, "zipf": 406147, "chunks": 5773}
+UNITS = {"pages4k": 1 << 20, "v4096": 1 << 18, "v1024": 1 << 20, "zipf": 406147, "chunks": 5773}  # buffers
 for mode in sys.argv[1:] or ["pages4k", "v4096", "v1024", "zipf"]:
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
@@ -13,7 +13,7 @@ for mode in sys.argv[1:] or ["pages4k", "v4096", "v1024", "zipf"]:
     for k, c in agg.items():
         if "splitmix" in k:
             continue
-        ms = sum(dur[k]) / len(dur[k]) / 2
+        ms = sum(dur[k]) / len(dur[k])
         m = {n: sum(v) / len(v) for n, v in c.items()}
         u = UNITS[mode]
         print(f"{mode:8s} {k:40s} {ms:.4f} ms  clk {m.get('GRBM_GUI_ACTIVE', 0) / 8 / ms / 1e6:.2f} GHz")
