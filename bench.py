@@ -45,7 +45,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=30, help="untimed steps (the clock settles within ~30 launches)")
     p.add_argument("--workload", default="pages4k", choices=sorted(W.WORKLOADS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
     p.add_argument("--no-verify", action="store_true")
