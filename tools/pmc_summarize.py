@@ -13,29 +13,36 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def load(mode, kernel_substr):
+def load(mode, kernel_substrs):
+    """Per counter: the sum over the step's kernels (every kernel whose name
+    holds one of kernel_substrs) of that kernel's mean value per launch."""
     agg = collections.defaultdict(list)
-    durs = []
+    durs = collections.defaultdict(list)
     for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "pmc", mode, "*_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if kernel_substr in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if any(k in r["Kernel_Name"] for k in kernel_substrs):
+                agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
         for t in csv.DictReader(open(f.replace("counter_collection", "kernel_trace"))):
-            if kernel_substr in t["Kernel_Name"]:
-                durs.append((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) * 1e-9)
-    return agg, durs
+            if any(k in t["Kernel_Name"] for k in kernel_substrs):
+                durs[t["Kernel_Name"]].append((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) * 1e-9)
+    mean = collections.defaultdict(float)
+    for (_, counter), v in agg.items():
+        mean[counter] += sum(v) / len(v)
+    dur = sum(sum(v) / len(v) for v in durs.values())
+    launches = max(len(v) for v in durs.values())
+    return dict(mean), dur, launches
 
 
-def main(mode="pages4k", workload="pages4k", kernel="k_pages4k", algorithmic=(1 << 20) * 4100, units=1 << 20):
-    agg, durs = load(mode, kernel)
-    mean = {k: sum(v) / len(v) for k, v in agg.items()}
+def main(mode="pages4k", workload="pages4k", kernel=("k_pages4k",), algorithmic=(1 << 20) * 4100, units=1 << 20):
+    if callable(algorithmic):
+        algorithmic, units = algorithmic()
+    mean, dur, launches = load(mode, kernel)
     fetch = mean["FETCH_SIZE"] * 1024 * 2
     write = mean["WRITE_SIZE"] * 1024
-    dur = sum(durs) / len(durs)
     out = {
         "workload": workload,
-        "kernel": kernel,
-        "source": f"rocprofv3 --pmc <counters> --kernel-trace, separate passes, {len(durs)} launches",
+        "kernel": " + ".join(kernel),
+        "source": f"rocprofv3 --pmc <counters> --kernel-trace, separate passes, {launches} launches per pass",
         "correction": "FETCH_SIZE(KiB)*1024*2 (gfx950 reports half of wide streaming reads) + WRITE_SIZE(KiB)*1024",
         "hbm_bytes_per_launch": round(fetch + write),
         "fetch_bytes_per_launch": round(fetch),
@@ -55,9 +62,22 @@ def main(mode="pages4k", workload="pages4k", kernel="k_pages4k", algorithmic=(1 
                                           "per_unit")}))
 
 
+def _varlen(fn):
+    """Algorithmic bytes of a bench_workloads varlen batch: data + 20 B per buffer."""
+    def f():
+        sys.path.insert(0, ROOT)
+        import bench_workloads as W
+        lens = getattr(W, fn)()
+        return int(lens.sum()) + 20 * lens.size, lens.size
+    return f
+
+
+VARLEN_KERNELS = ("k_v7count", "k_v7prep", "k_scan", "k_varlen7")
 PRESETS = {
-    "pages4k": ("pages4k", "pages4k", "k_pages4k", (1 << 20) * 4100, 1 << 20),
-    "xxh3": ("xxh3", "xxh3-pages4k", "k_xxh3_rows", (1 << 20) * (4088 + 8), 1 << 20),
+    "pages4k": ("pages4k", "pages4k", ("k_pages4k",), (1 << 20) * 4100, 1 << 20),
+    "xxh3": ("xxh3", "xxh3-pages4k", ("k_xxh3_rows",), (1 << 20) * (4088 + 8), 1 << 20),
+    "zipf": ("zipf", "zipf", VARLEN_KERNELS, _varlen("zipf_lengths"), None),
+    "chunks": ("chunks", "chunks", VARLEN_KERNELS, _varlen("chunk_lengths"), None),
 }
 
 if __name__ == "__main__":

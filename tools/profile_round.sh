@@ -23,7 +23,7 @@ done
 echo rocprof done
 P=gpurun_out/pmc
 mkdir -p $P
-for MODE in pages4k xxh3; do
+for MODE in pages4k xxh3 zipf chunks; do
   for spec in "fetch FETCH_SIZE" "write WRITE_SIZE" "sq GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD"; do
     set -- $spec; name=$1; shift
     timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $P/$MODE -o ${name}_$MODE -- python tools/pmc_probe.py $MODE > $P/$MODE.log 2>&1 || exit 1
