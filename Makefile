@@ -22,6 +22,11 @@ CXXFLAGS := -O3 -fPIC -std=c++17 -Wall -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
 all: $(LIB) oracle
 
+# the page kernels' grab requests must stay single-lane atomics whose return is
+# awaited only where it is used (the atomic optimizer's wave reduction reads it
+# back at once, which stalls on every data load in flight)
+$(OBJ)/crc32c_kernels.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+
 $(OBJ)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

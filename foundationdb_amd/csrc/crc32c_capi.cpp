@@ -24,6 +24,7 @@ struct DeviceState {
 	int num_cus = 0;
 	bool ready = false;
 	std::map<hipStream_t, std::pair<void*, uint64_t>> ws;  // varlen planning workspace per stream
+	std::map<hipStream_t, uint32_t*> ctr;                  // page-kernel grab counters per stream
 };
 
 std::mutex g_mu;
@@ -101,6 +102,29 @@ int check_launch(const char* what) {
 }
 
 }  // namespace
+
+// Grab counters of the page kernels for `stream` on the current device:
+// zeroed once here, left at zero by every page launch.
+int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr) {
+	DeviceState* st;
+	if (int rc = device_state(&st)) return rc;
+	std::lock_guard<std::mutex> lock(g_mu);
+	uint32_t*& p = st->ctr[stream];
+	if (!p) {
+		const size_t bytes = (size_t)(num_cus > st->num_cus ? num_cus : st->num_cus) * kPageCtrWords * 4;
+		uint32_t* q = nullptr;
+		hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), bytes);
+		if (e != hipSuccess) return fail(FDB_CRC32C_ENOMEM, "hipMalloc(page counters)", e);
+		e = hipMemset(q, 0, bytes);
+		if (e != hipSuccess) {
+			(void)hipFree(q);
+			return fail(FDB_CRC32C_EHIP, "hipMemset(page counters)", e);
+		}
+		p = q;
+	}
+	*ctr = p;
+	return 0;
+}
 
 // used by the host pipeline (crc32c_pipeline.cpp)
 int device_tables(const DevTables** tabs, int* num_cus) {

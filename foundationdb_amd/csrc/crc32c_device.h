@@ -26,6 +26,12 @@ struct DevTables {
 // Build the tables on the host (crc32c_tables.cpp).
 void build_dev_tables(DevTables* t);
 
+// Grab counters of the page kernels (crc32c_kernels.hip): kPageCtrWords words
+// per workgroup, owned by the launch stream (page kernels on one stream run in
+// order), zero between launches.  Allocated on a stream's first page launch.
+constexpr uint32_t kPageCtrWords = 32;
+int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr);  // crc32c_capi.cpp
+
 int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream);
 // Bytes [h, 4096 - t) of 4 KiB pages (h, t < 16); `pages` 16-byte aligned.

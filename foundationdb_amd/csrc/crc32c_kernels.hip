@@ -30,9 +30,6 @@
 
 #include "crc32c_common.h"
 
-#ifndef FDBCRC_PDEPTH
-#define FDBCRC_PDEPTH 2  // pages in flight per wave, in units of U (development experiments)
-#endif
 #ifndef FDBCRC_PU
 #define FDBCRC_PU 2  // pages per unit (register chains interleaved per wave)
 #endif
@@ -41,8 +38,7 @@ namespace fdbcrc {
 
 // 4 KiB pages (160 KiB LDS image, 4-byte slicing).
 // U pages per unit: U independent register chains interleave (ILP U) while
-// the next unit's U pages are in flight.  Groups of G = 2U*floor(64/2U) pages
-// share one seed vector load and one coalesced checksum store.
+// the next unit's U pages are in flight.
 // WINDOW: checksum bytes [h, 4096 - t) of every page (h, t < 16): before the
 // unswizzle, lane 0's first chunk (page bytes 0..15) is masked below h and
 // gets the seed register at byte h (lane 32's chunk 16..31 takes the bytes
@@ -96,6 +92,21 @@ __device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t
 	return r;
 }
 
+// Load balance.  The SIMD's issue arbitration favours some waves: with an
+// equal static share per wave, the waves of one launch finish between 50 %
+// and 100 % of the kernel time.  So each workgroup owns a contiguous range of
+// GRABS (one unit pair, 2U pages, each) and its waves take them from a
+// per-workgroup counter: the first two grabs of a wave are static, the next
+// one is requested one grab ahead, so the atomic's return travels in the
+// shadow of the data loads issued before it.  The counters (kPageCtrWords
+// apart, one cache line each) belong to the launch stream and are zero
+// between launches: each workgroup puts its counter back to zero once all its
+// waves are done.
+//
+// The checksums of F = 64 / 2U consecutive grabs of a wave collect in its
+// lanes (lane 2U*f + j: page j of the group's f-th grab) and leave together;
+// the WINDOW / PAIR finishing multiplies run once per group.
+//
 // LIST: page i of the batch is page idx[i] of `base` and the batch size is
 // read from *d_count (device-side compaction output, pagecheck.hip).
 // PAIR: 8 KiB pages as pairs of 4 KiB blocks (block 2i+h = half h of page
@@ -106,32 +117,34 @@ template <int U, bool WINDOW = false, bool LIST = false, bool PAIR = false>
 __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
                                                   uint32_t seed, const uint32_t* __restrict__ seeds,
                                                   uint32_t* __restrict__ out, const DevTables* __restrict__ tabs,
-                                                  uint32_t h = 0, uint32_t t = 0,
+                                                  uint32_t* __restrict__ ctr, uint32_t h = 0, uint32_t t = 0,
                                                   const uint32_t* __restrict__ idx = nullptr,
                                                   const uint64_t* __restrict__ d_count = nullptr) {
 	if (LIST) {
 		count = *d_count;
-		if (count == 0) return;  // the list is empty: idx[] holds nothing to read
+		if (count == 0) return;  // the list is empty: every wave leaves before touching the counters
 	}
 	if (PAIR) count *= 2;  // blocks
-	constexpr uint64_t G = 2 * U * (64 / (2 * U));  // a whole number of loop iterations
+	constexpr uint32_t C = 2 * U;   // pages per grab
+	constexpr uint32_t F = 64 / C;  // grabs per store group
+	static_assert(64 % C == 0, "a store group fills the wave's lanes");
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const LaneCtx c = make_ctx();
 	const uint32_t col4 = (c.lane & 31) * 4;
 	const uint32_t c4 = col4 | 0x10000u;
 	const uint32_t c_lane = (kS4LaneOff + (c.lane >> 5) * 0x4000) | col4;
-	const uint64_t wpb = blockDim.x >> 6;
-	const uint64_t wave = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
-	const uint64_t waves = (uint64_t)gridDim.x * wpb;
-	uint64_t per = (count + waves - 1) / waves;
-	per = per > G ? (per + G - 1) / G * G : (per + U - 1) / U * U;
-	const uint64_t begin = wave * per;
-	const uint64_t end = begin + per < count ? begin + per : count;
-	const uint64_t last = end ? end - 1 : 0;
-	// page index -> address, clamped into this wave's run: clamped duplicates
-	// are computed and discarded, so every load is consumed unconditionally
+	const uint32_t wpb = blockDim.x >> 6;
+	const uint32_t wi = rdfirst(threadIdx.x >> 6);
+	const uint64_t ngrab = (count + C - 1) / C;
+	const uint64_t per = (ngrab + gridDim.x - 1) / gridDim.x;
+	const uint64_t g0 = (uint64_t)blockIdx.x * per;
+	const uint64_t g1 = g0 + per < ngrab ? g0 + per : ngrab;
+	uint32_t* const my_ctr = ctr + kPageCtrWords * blockIdx.x;
+	const uint64_t last = count - 1;
+	// page index -> address, clamped into the batch: clamped duplicates are
+	// computed and discarded, so every load is consumed unconditionally
 	auto page = [&](uint64_t i) {
-		const uint64_t j = i < end ? i : (begin < end ? last : 0);
+		const uint64_t j = i < count ? i : last;
 		if (PAIR) return base + (j >> 1) * stride + (j & 1) * 4096;
 		return base + (LIST ? (uint64_t)idx[j] : j) * stride;
 	};
@@ -139,100 +152,105 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 #pragma unroll
 		for (int j = 0; j < U; ++j) load_block(u[j], page(i0 + j), c.ld_off);
 	};
-if constexpr (FDBCRC_PDEPTH == 3 && !WINDOW && !LIST && !PAIR) {
-	Block u0[U], u1[U], u2[U];
-	load_u(u0, begin);  // in flight during the LDS fill
-	load_u(u1, begin + U);
-	fill_lds_b(lds, tabs);
-	if (begin >= end) return;
-	constexpr uint64_t G3 = 3 * U * (63 / (3 * U));
-	for (uint64_t first = begin; first < end; first += G3) {
-		const uint64_t n = end - first < G3 ? end - first : G3;
-		const uint64_t sp = first + ((uint64_t)c.lane < n ? c.lane : 0);
-		const uint32_t my_seed = seeds ? seeds[sp] : seed;
-		uint32_t mine = 0;
-		auto phase = [&](Block (&cu)[U], Block (&ld)[U], uint64_t kc, uint64_t kl) {
-			uint32_t sd[U], crc[U];
-			load_u(ld, first + kl);
-			__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(kc + j) & 63);
-			unit_crc_b<U, false, false>(lds, c.lane, c4, c_lane, cu, sd, crc, h, t);
-#pragma unroll
-			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == kc + j ? crc[j] : mine;
-			__builtin_amdgcn_sched_barrier(0);
-		};
-		for (uint64_t k = 0; k < n; k += 3 * U) {
-			phase(u0, u2, k, k + 2 * U);
-			phase(u1, u0, k + U, k + 3 * U);
-			phase(u2, u1, k + 2 * U, k + 4 * U);
-		}
-		if ((uint64_t)c.lane < n) out[first + c.lane] = mine;
-	}
-	return;
-	}
+	auto clampg = [&](uint64_t g) { return g < g1 ? g : ngrab; };  // ngrab: nothing left
+	auto request = [&]() -> uint32_t {
+		uint32_t r = 0;
+		if (c.lane == 0) r = atomicAdd(my_ctr, 1u);
+		return r;
+	};
+	// lane j < C: seed of page j of grab g (an unconditional load: a branch
+	// around vector memory would make the compiler wait for the loads in flight)
+	auto seed_of = [&](uint64_t g) -> uint32_t {
+		const uint64_t i = g * C + (uint64_t)(c.lane & (C - 1));
+		const uint64_t j = i < count ? i : last;
+		const uint32_t v = *(seeds ? seeds + (PAIR ? j >> 1 : j) : &tabs->slice4[0][0]);
+		const uint32_t sd = seeds ? v : seed;
+		return (PAIR && (c.lane & 1)) ? ~0u : sd;  // second halves carry no seed (~0 -> 0)
+	};
+	uint64_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
+	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
+	uint32_t sdA = seed_of(gA), sdB = seed_of(gB);
 	Block u0[U], u1[U];
-	load_u(u0, begin);  // in flight during the LDS fill
+	load_u(u0, gA * C);  // in flight during the LDS fill
 	fill_lds_b(lds, tabs);
-	if (begin >= end) return;
-	for (uint64_t first = begin; first < end; first += G) {
-		const uint64_t n = end - first < G ? end - first : G;
-		// PAIR: block first+k is half k&1 of page (first+k)/2; odd blocks carry no seed (~0 -> 0)
-		const uint64_t sp = PAIR ? (first >> 1) + ((uint64_t)c.lane < n ? (uint64_t)c.lane >> 1 : 0)
-		                         : first + ((uint64_t)c.lane < n ? c.lane : 0);
-		uint32_t my_seed = seeds ? seeds[sp] : seed;
-		if (PAIR && (c.lane & 1)) my_seed = ~0u;
-		uint32_t mine = 0;  // lane k keeps the checksum of page first+k
-		for (uint64_t k = 0; k < n; k += 2 * U) {
-			uint32_t sd[U], crc[U];
-			load_u(u1, first + k + U);
-			__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + j) & 63);
-			unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u0, sd, crc, h, t);
-#pragma unroll
-			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + j ? crc[j] : mine;
-			__builtin_amdgcn_sched_barrier(0);
-			load_u(u0, first + k + 2 * U);
-			__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-			for (int j = 0; j < U; ++j) sd[j] = rdlane(my_seed, (int)(k + U + j) & 63);
-			unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u1, sd, crc, h, t);
-#pragma unroll
-			for (int j = 0; j < U; ++j) mine = (uint64_t)c.lane == k + U + j ? crc[j] : mine;
-			__builtin_amdgcn_sched_barrier(0);
-		}
+	uint32_t mine = 0;     // lane 2U*f + j: checksum of page j of the group's f-th grab
+	uint64_t myi = ~0ull;  // ... and its index in the batch (~0: none)
+	uint32_t f = 0;        // grabs in the current store group
+	auto store = [&]() {
 		if (WINDOW) mine = ~(t ? vmul_tab(tabs->inv_z[t], mine) : mine);
 		if (PAIR) {
 			const uint32_t other = __builtin_amdgcn_update_dpp(0u, mine, 0xB1, 0xF, 0xF, false);  // lane ^ 1
 			mine = ~(vmul_tab(tabs->block, mine) ^ other);
-			if ((uint64_t)c.lane < n && !(c.lane & 1)) out[(first >> 1) + (c.lane >> 1)] = mine;
-		} else if ((uint64_t)c.lane < n) {
-			out[first + c.lane] = mine;
+			if (myi < count && !(c.lane & 1)) out[myi >> 1] = mine;
+		} else if (myi < count) {
+			out[myi] = mine;
+		}
+		myi = ~0ull;
+	};
+	while (gA < ngrab) {
+		const uint64_t first = gA * C;
+		const uint32_t l0 = f * C;
+		uint32_t sd[U], crc[U];
+		load_u(u1, first + U);
+		__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+		for (int j = 0; j < U; ++j) sd[j] = rdlane(sdA, j);
+		unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u0, sd, crc, h, t);
+#pragma unroll
+		for (int j = 0; j < U; ++j) mine = (uint32_t)c.lane == l0 + j ? crc[j] : mine;
+		__builtin_amdgcn_sched_barrier(0);
+		load_u(u0, gB * C);  // the next grab's first unit
+		__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+		for (int j = 0; j < U; ++j) sd[j] = rdlane(sdA, U + j);
+		unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u1, sd, crc, h, t);
+#pragma unroll
+		for (int j = 0; j < U; ++j) mine = (uint32_t)c.lane == l0 + U + j ? crc[j] : mine;
+		__builtin_amdgcn_sched_barrier(0);
+		const uint32_t k = (uint32_t)c.lane - l0;
+		myi = k < C ? first + k : myi;
+		gA = gB;
+		sdA = sdB;
+		gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
+		req = request();
+		sdB = seed_of(gB);
+		if (++f == F) {
+			store();
+			f = 0;
 		}
 	}
+	if (f) store();
+	// every request of every wave has returned: the counter goes back to zero
+	// for the next launch on this stream
+	__builtin_amdgcn_s_waitcnt(0);
+	__syncthreads();
+	if (threadIdx.x == 0) *my_ctr = 0;
 }
 
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+// At most one workgroup per CU, and at least one grab per wave.
+static unsigned page_grid(uint64_t pages, int num_cus) {
+	const uint64_t grabs = (pages + 2 * FDBCRC_PU - 1) / (2 * FDBCRC_PU);
+	uint64_t grid = (grabs + 15) / 16;
+	if (grid > (uint64_t)num_cus) grid = num_cus;
+	return grid ? (unsigned)grid : 1u;
+}
+
 int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream) {
-	const int threads = 1024;
-	const uint64_t units = (count + 63) / 64;
-	uint64_t grid = (units + 15) / 16;
-	if (grid > (uint64_t)num_cus) grid = num_cus;
-	if (grid == 0) grid = 1;
+	uint32_t* ctr;
+	if (page_counters(stream, num_cus, &ctr)) return -1;
 	switch (blocks_per_page) {
-		case 1: k_pages4k<FDBCRC_PU><<<(unsigned)grid, threads, 0, stream>>>(base, stride, count, seed, seeds, out, tabs); break;
-		case 2: {  // 8 KiB pages as block pairs on the 4 KiB kernel
-			uint64_t g2 = (2 * units + 15) / 16;
-			if (g2 > (uint64_t)num_cus) g2 = num_cus;
-			if (g2 == 0) g2 = 1;
-			k_pages4k<2, false, false, true><<<(unsigned)g2, threads, 0, stream>>>(base, stride, count, seed, seeds, out,
-			                                                                      tabs);
+		case 1:
+			k_pages4k<FDBCRC_PU><<<page_grid(count, num_cus), 1024, 0, stream>>>(base, stride, count, seed, seeds, out,
+			                                                                      tabs, ctr);
 			break;
-		}
+		case 2:  // 8 KiB pages as block pairs on the 4 KiB kernel
+			k_pages4k<FDBCRC_PU, false, false, true><<<page_grid(2 * count, num_cus), 1024, 0, stream>>>(
+			    base, stride, count, seed, seeds, out, tabs, ctr);
+			break;
 		default: return -1;
 	}
 	return 0;
@@ -242,11 +260,10 @@ int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint
 // start, h bytes before the caller's window).
 int launch_pages_window(const uint8_t* pages, uint64_t stride, uint64_t count, uint32_t h, uint32_t t, uint32_t seed,
                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream) {
-	const uint64_t units = (count + 63) / 64;
-	uint64_t grid = (units + 15) / 16;
-	if (grid > (uint64_t)num_cus) grid = num_cus;
-	if (grid == 0) grid = 1;
-	k_pages4k<2, true><<<(unsigned)grid, 1024, 0, stream>>>(pages, stride, count, seed, seeds, out, tabs, h, t);
+	uint32_t* ctr;
+	if (page_counters(stream, num_cus, &ctr)) return -1;
+	k_pages4k<FDBCRC_PU, true><<<page_grid(count, num_cus), 1024, 0, stream>>>(pages, stride, count, seed, seeds, out,
+	                                                                          tabs, ctr, h, t);
 	return 0;
 }
 
@@ -255,12 +272,10 @@ int launch_pages_window(const uint8_t* pages, uint64_t stride, uint64_t count, u
 int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32_t* idx, const uint64_t* d_count,
                              uint64_t max_count, uint32_t h, uint32_t t, uint32_t seed, uint32_t* out,
                              const DevTables* tabs, int num_cus, hipStream_t stream) {
-	const uint64_t units = (max_count + 63) / 64;
-	uint64_t grid = (units + 15) / 16;
-	if (grid > (uint64_t)num_cus) grid = num_cus;
-	if (grid == 0) grid = 1;
-	k_pages4k<2, true, true><<<(unsigned)grid, 1024, 0, stream>>>(pages, stride, max_count, seed, nullptr, out, tabs,
-	                                                              h, t, idx, d_count);
+	uint32_t* ctr;
+	if (page_counters(stream, num_cus, &ctr)) return -1;
+	k_pages4k<FDBCRC_PU, true, true><<<page_grid(max_count, num_cus), 1024, 0, stream>>>(
+	    pages, stride, max_count, seed, nullptr, out, tabs, ctr, h, t, idx, d_count);
 	return 0;
 }
 

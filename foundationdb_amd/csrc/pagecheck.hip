@@ -256,8 +256,9 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 	const uint64_t* n_crc = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
 	const uint64_t* n_xxh = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
 	if (ps == 4096) {
-		fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n_crc, count, 0, 8, 0xFDBEEFDBu, w.crc_out, tabs,
-		                                 num_cus, s);
+		if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n_crc, count, 0, 8, 0xFDBEEFDBu, w.crc_out, tabs,
+		                                     num_cus, s))
+			return -1;
 		k_sq_after_crc<<<blocks(count), 256, 0, s>>>(pages, ps, w.list_a, w.ctr, w.crc_out, status);
 	} else {
 		// other page sizes: every page through the general fixed-stride engine
@@ -288,7 +289,8 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
 	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
 	// V1: crc32c(0xfdbeefdb, bytes [4, 4096))
-	fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n1, count, 4, 0, 0xFDBEEFDBu, w.crc_out, tabs, num_cus, s);
+	if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n1, count, 4, 0, 0xFDBEEFDBu, w.crc_out, tabs, num_cus, s))
+		return -1;
 	// V2: XXH3_64bits(bytes [8, 4096))
 	fdbxxh::XxhParams P{};
 	P.base = pages + 8;

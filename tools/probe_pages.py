@@ -11,7 +11,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     F.gpu_init()
     n = 1 << 20
     length = int(os.environ.get("PLEN", "4096"))
-    count = n * 4096 // length
+    count = int(os.environ.get("PCOUNT", n * 4096 // length))
     big = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
     F.fill_splitmix64(big, 0x5EED)
     out = torch.empty(count, dtype=torch.uint32, device=dev)
@@ -38,5 +38,5 @@ for rnd in range(2):
         if r.returncode:
             print(L, "FAILED", r.stderr[-500:]); sys.exit(1)
         d = json.loads(r.stdout.strip().splitlines()[-1])
-        gb = (1 << 32) / d["ms"] / 1e6
-        print(f"{L or 'base':12s} {d['ms']:.4f} ms  {gb:7.1f} GB/s  {4000 / d['ms']:7.1f} GiB/s  sum={d['xor']:#x}  {['%.4f' % x for x in d['all']]}", flush=True)
+        gb = int(os.environ.get("PCOUNT", 1 << 20)) * 4096 / d["ms"] / 1e6
+        print(f"{L or 'base':12s} {d['ms']:.4f} ms  {gb:7.1f} GB/s  {gb * 1e9 / 2**30 / 1e3:7.1f} GiB/s  sum={d['xor']:#x}  {['%.4f' % x for x in d['all']]}", flush=True)
