@@ -65,7 +65,11 @@ uint32_t crc32c_append_zeros(uint32_t crc, uint64_t nzeros);
 
 /* Prepare the current device (upload operator tables).  Optional: every
  * device entry point does it on first use, but calling it up front keeps the
- * one synchronous upload out of a stream capture.  Thread-safe. */
+ * one synchronous upload out of a stream capture.  Thread-safe.
+ * The page kernels (4 KiB / 8 KiB pages, the page verifiers) also keep a
+ * small per-stream array of load-balancing counters (32 words per CU,
+ * allocated and zeroed on the stream's first page batch, left at zero by
+ * every launch): run one page batch on a stream before capturing it. */
 int crc32c_gpu_init(void);
 
 /* Buffer i (0 <= i < count) is the `length` bytes at d_base + i*stride.
