@@ -197,7 +197,7 @@ def main():
         }
         if dry:
             rec["data"] = "DRY RUN on CPU (harness test, not a measurement)"
-        elif args.cpu_seconds > 0:
+        elif args.cpu_seconds > 0 and world == 1:  # reported at N=1 only
             rec["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:

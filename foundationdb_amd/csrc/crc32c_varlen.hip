@@ -372,7 +372,12 @@ struct Tab7 {
 	uint32_t f;
 	uint32_t oi;   // output index relative to the wave's first tile
 	uint32_t S;    // team sum of the slot, XORed onto the slot's edge terms (team-sum form)
+	uint64_t em;   // (uniform) slots that need masking: window 0 (lo != 0), tail bytes, empty slots
 };
+// A slot whose chunks all hold its buffer's own bytes needs no masking.
+__device__ __forceinline__ bool slot_edge(uint32_t f) {
+	return (f & k7_LO) || ((f & (k7_FIN | k7_PEND)) == k7_FIN && ((f >> k7_ZT) & 15u));
+}
 
 #ifndef FDBCRC_V7_THREADS
 #define FDBCRC_V7_THREADS 768  // 12 waves per CU: 168 VGPRs per lane, no spills
@@ -511,6 +516,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			const uint64_t w0 = rdlane64(X.wa, 0);
 			if ((uint32_t)lane >= filled) X.wa = w0;
 		}
+		X.em = __ballot(slot_edge(X.f));
 		return filled;
 	};
 	// load k of a pass fetches team {0,2,1,3}[k]'s window.  Every load is
@@ -519,16 +525,22 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	// empty slots, re-read the lead chunk (empty slots: slot 0's last chunk)
 	// and are zeroed at compute time.
 	auto load = [&](Block& nb, const Tab7& X, uint32_t p) {
+		const bool edge = (X.em >> (4 * p)) & 15u;  // uniform: plain passes skip the lead clamp
 #pragma unroll
 		for (int k = 0; k < 4; ++k) {
 			const uint32_t s = 4 * p + (((k & 1) << 1) | (k >> 1));
 			const uint64_t wa = rdlane64(X.wa, (int)s);
-			const uint32_t lo = rdlane(X.f, (int)s) & k7_LO;
-			const uint32_t lc = lo < 1008u ? lo : 1008u;
-			nb.r[k] = ld16(reinterpret_cast<const uint8_t*>(wa + (c.ld_off > lc ? c.ld_off : lc)));
+			uint32_t off = c.ld_off;
+			if (edge) {
+				const uint32_t lo = rdlane(X.f, (int)s) & k7_LO;
+				const uint32_t lc = lo < 1008u ? lo : 1008u;
+				off = off > lc ? off : lc;
+			}
+			nb.r[k] = ld16(reinterpret_cast<const uint8_t*>(wa + off));
 		}
 	};
 	auto compute = [&](Block& b, Tab7& X, uint32_t p) {
+		if ((X.em >> (4 * p)) & 15u) {  // a slot of this pass holds an edge, or nothing
 #pragma unroll
 		for (int k = 0; k < 4; ++k) {
 			const uint32_t f = rdlane(X.f, (int)(4 * p + (((k & 1) << 1) | (k >> 1))));
@@ -545,6 +557,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 #pragma unroll
 				for (int d = 0; d < 4; ++d) b.r[k][d] &= lane == 63 ? km[d] : ~0u;
 			}
+		}
 		}
 		unswizzle(b);
 		const uint32_t R = row_xor(mul_nibbles(lds, chain64_b(lds, 0u, b, c4), c_lane));
@@ -664,6 +677,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	t1.f = 1024u;  // empty: the first table's "previous table" finishes nothing
 	t1.oi = 0;
 	t1.S = 0;
+	t1.em = ~0ull;
 	phase1(t1, 0);
 	build();
 	uint32_t sb = 0;
