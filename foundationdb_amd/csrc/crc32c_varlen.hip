@@ -201,6 +201,13 @@ __device__ __forceinline__ uint32_t vmul(const uint32_t* tab, uint32_t v) {
 // register times x^(8*65536); a buffer cut by the wave range is finished as a
 // part shifted to its end and XOR-merged (atomicXor) with its other parts.
 constexpr uint32_t kTileW = 256;
+#ifndef FDBCRC_SMALL_SPAN
+#define FDBCRC_SMALL_SPAN 128
+#endif
+// Buffers whose 16-byte chunks span at most kSmallSpan bytes get no window
+// slots: the prep kernel finishes them, one lane each (a 1 KiB window would
+// mostly checksum lanes of zeros for them).
+constexpr uint32_t kSmallSpan = FDBCRC_SMALL_SPAN;
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
 	return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
@@ -236,7 +243,7 @@ __device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len) {
 	const uint64_t E = (P1 + 15) & ~uint64_t(15);
 	g.A = P0 & ~uint64_t(15);
 	const uint64_t span = E - g.A;
-	g.W = len >= 16 ? (uint32_t)((span + 1023) >> 10) : 0u;
+	g.W = (len >= 16 && span > kSmallSpan) ? (uint32_t)((span + 1023) >> 10) : 0u;
 	g.lo = (uint32_t)(1024 * (uint64_t)g.W - span) & 1023u;
 	g.k0 = (uint32_t)(P0 & 15);
 	g.zt = (uint32_t)(E - P1);
@@ -332,10 +339,40 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	const uint32_t gi = excl + inwave + incl - W;
 	P.gs[i] = gi;
 	const uint32_t s0 = ~(P.seeds ? P.seeds[i] : P.seed);
-	if (!W) {  // shorter than 16 bytes: byte-serial
-		uint32_t r = s0;
-		for (uint64_t q = 0; q < len; ++q) r = (r >> 8) ^ s4[3][(r ^ ld1(P.base + off + q)) & 255u];
-		P.out[i] = ~r;
+	if (!W) {
+		if (len < 16) {  // byte-serial
+			uint32_t r = s0;
+			for (uint64_t q = 0; q < len; ++q) r = (r >> 8) ^ s4[3][(r ^ ld1(P.base + off + q)) & 255u];
+			P.out[i] = ~r;
+			return;
+		}
+		// small buffer: its chunks [A, E) as 4-byte words from a zero register,
+		// the bytes before P0 zeroed and ~seed injected at P0 (crc32c.cpp:197),
+		// the zt bytes after P1 zeroed and then divided out (x^(-8 zt)).  All
+		// chunk loads are issued first (clamped to the last chunk): one latency.
+		constexpr uint32_t NC = kSmallSpan / 16;
+		const uint32_t nch = (uint32_t)(((P0 + len + 15) & ~uint64_t(15)) - g.A) >> 4;
+		u32x4 ch[NC];
+#pragma unroll
+		for (uint32_t j = 0; j < NC; ++j)
+			ch[j] = ld16(reinterpret_cast<const uint8_t*>(g.A + 16 * (j < nch ? j : nch - 1)));
+		const Masks mk = edge_masks(g.k0, 16u - g.zt, s0);
+		uint32_t x = 0;
+#pragma unroll
+		for (uint32_t j = 0; j < NC; ++j) {
+			if (j < nch) {
+#pragma unroll
+				for (int d = 0; d < 4; ++d) {
+					uint32_t w = ch[j][d];
+					if (j == 0) w = (w & mk.lm[d]) ^ mk.inj[d];
+					if (j == 1 && d == 0) w ^= mk.spill;
+					if (j == nch - 1) w &= mk.tm[d];
+					x ^= w;
+					x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
+				}
+			}
+		}
+		P.out[i] = ~(g.zt ? vmul(&T->inv_z[g.zt][0][0], x) : x);
 		return;
 	}
 	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
