@@ -1,7 +1,7 @@
 """CPU checks of the variable-length engine's work decomposition (no GPU):
-every byte of every buffer is assigned to exactly one wavefront piece, every
-zero-length buffer is visited once, and no lane ever loads a 16-byte chunk
-outside the piece it is checksumming.  Mirrors crc32c_varlen.hip via
+every slot belongs to exactly one wavefront, the chunks a buffer's windows
+checksum tile its 16-byte span exactly once, and no lane ever loads a 16-byte
+chunk that does not overlap its buffer.  Mirrors crc32c_varlen.hip (v7) via
 tests/varlen_model.py."""
 import numpy as np
 import pytest
@@ -9,7 +9,7 @@ import pytest
 import varlen_model as M
 
 
-@pytest.mark.parametrize("nwave", [1, 7, 64, 4096])
+@pytest.mark.parametrize("nwave", [1, 7, 64, 3072])
 def test_random_batches_cover_exactly_once(nwave):
     rng = np.random.default_rng(nwave)
     n = 3000
@@ -34,19 +34,29 @@ def test_zipf_like_small_packets():
 def test_fixed_mode_cover_exactly_once(length, stride, count):
     offsets = np.arange(count, dtype=np.uint64) * stride + 3
     lengths = np.full(count, length, dtype=np.uint64)
-    _, errors = M.check_decomposition(lengths, offsets, 4096, fixed=length, check_loads=False)
+    _, errors = M.check_decomposition(lengths, offsets, 3072, check_loads=False)
     assert not errors, errors[:5]
 
 
 def test_all_empty_and_single_byte():
     lengths = np.array([0] * 100 + [1] * 50 + [0] * 10)
     offsets = np.arange(lengths.size) * 7
-    _, errors = M.check_decomposition(lengths, offsets, 4096)
+    _, errors = M.check_decomposition(lengths, offsets, 3072)
     assert not errors, errors[:5]
 
 
-def test_window_loads_stay_inside_piece():
-    for P0, P1 in [(16, 32), (1, 17), (15, 1039), (4096, 4096 + 1024), (100, 100 + 4095), (7, 7 + 70_000),
-                   (4096 * 3 + 5, 4096 * 9 - 3)]:
-        for ca in M.loads_for_piece(P0, P1):
-            assert ca % 16 == 0 and ca + 16 > P0 and ca < P1
+def test_every_alignment_and_threshold_length():
+    """All 16 start alignments x lengths around the small-buffer span, the
+    1 KiB window and 4 KiB pass geometry."""
+    lens = [16, 17, 100, 112, 113, 127, 128, 129, 1007, 1008, 1009, 1023, 1024, 1025, 2047, 4095, 4096, 4097, 12289]
+    offs, lengths = [], []
+    for a in range(16):
+        for n in lens:
+            offs.append(1 << 20 | a)
+            lengths.append(n)
+    cover, errors = M.check_decomposition(lengths, offs, 64)
+    assert not errors, errors[:5]
+    # buffers spanning more than SMALL_SPAN bytes are windowed, the rest finish in prep
+    for i, (o, n) in enumerate(zip(offs, lengths)):
+        A, E, W, _, _, _ = M.geo7(o, n)
+        assert (W > 0) == (E - A > M.SMALL_SPAN), (o, n)

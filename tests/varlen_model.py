@@ -1,16 +1,24 @@
-"""Scalar model of the variable-length engine's work decomposition
-(foundationdb_amd/csrc/crc32c_varlen.hip: k_plan / k_scan / k_varlen).
+"""Scalar model of the variable-length engine's work decomposition (v7,
+foundationdb_amd/csrc/crc32c_varlen.hip: geo7 / k_v7count / k_v7prep /
+k_varlen7).  Keep it in lockstep with the kernel.
 
-It replays, on the CPU, exactly which pieces each wavefront cuts, which 1 KiB
-windows / 4 KiB blocks it reads and which 16-byte chunk addresses every lane
-loads, so tests can check -- without a GPU -- that (a) every byte of every
-buffer is covered exactly once and (b) no lane ever loads outside the piece
-it is working on.  Keep it in lockstep with the kernel.
+It replays, on the CPU, how a batch is cut: every buffer of at least 16 bytes
+whose 16-byte chunks span more than SMALL_SPAN bytes is cut into W windows of
+1 KiB aligned to its end E = ceil16(P1) (window 0 starts `lo` bytes before
+A = P0 & ~15); the windows of all buffers, in index order, are the batch's
+slots; wave w streams slots [w*Qs, (w+1)*Qs).  Lane m of a load reads the 16
+bytes at window + max(ld_off(m), min(lo, 1008)) for window 0 (the chunks
+before the buffer are re-reads of its lead chunk, zeroed at compute time) and
+window + ld_off(m) otherwise.  Shorter buffers are finished by the prep
+kernel: byte-serially below 16 bytes, else one lane loading its chunks
+[A, E) (clamped to the last one).  Tests check -- without a GPU -- that
+(a) every slot belongs to exactly one wave, (b) the chunks a buffer's windows
+checksum tile [A, E) exactly once, and (c) no lane ever loads a 16-byte chunk
+that does not overlap its buffer.
 """
 import numpy as np
 
-TILE = 256
-SMALL = 1024
+SMALL_SPAN = 128  # FDBCRC_SMALL_SPAN
 
 
 def lane_ld_off(lane):
@@ -19,142 +27,101 @@ def lane_ld_off(lane):
 
 
 LD_OFF = np.array([lane_ld_off(l) for l in range(64)], dtype=np.int64)
-KOFF = [0, 2048, 1024, 3072]
 
 
-def plan(lengths, nwave):
-    lengths = np.asarray(lengths, dtype=np.uint64)
-    n = lengths.size
-    ntile = (n + TILE - 1) // TILE
-    tile_sum = [int(lengths[t * TILE:(t + 1) * TILE].sum()) for t in range(ntile)]
-    total = sum(tile_sum)
-    q = (total + nwave - 1) // nwave
-    q = 4096 if q < 4096 else (q + 63) & ~63
-    prefix = [0] * (ntile + 1)
+def geo7(P0, length):
+    """(A, E, W, lo, k0, zt) exactly as the kernel's geo7()."""
+    P1 = P0 + length
+    E = (P1 + 15) & ~15
+    A = P0 & ~15
+    span = E - A
+    W = (span + 1023) >> 10 if (length >= 16 and span > SMALL_SPAN) else 0
+    lo = (1024 * W - span) & 1023
+    return A, E, W, lo, P0 & 15, E - P1
+
+
+def slots(lengths, offsets):
+    """First slot g_i and window count W_i of every buffer; total slots."""
+    g, Ws = [], []
     acc = 0
-    for t in range(ntile):
-        prefix[t] = acc
-        acc += tile_sum[t]
-    prefix[ntile] = total
-    wave_tile = []
-    for w in range(nwave):
-        lo = w * q
-        # last t in [0, ntile) with prefix[t] <= lo
-        t = max(k for k in range(ntile) if prefix[k] <= lo) if ntile else 0
-        wave_tile.append(t)
-    return total, q, prefix, wave_tile
+    for off, ln in zip(offsets, lengths):
+        W = geo7(int(off), int(ln))[2]
+        g.append(acc)
+        Ws.append(W)
+        acc += W
+    return g, Ws, acc
 
 
-def pieces_of_wave(w, nwave, lengths, offsets, total, q, prefix, wave_tile, fixed=None):
-    """Yield (buf, P0, P1, first, split, after) exactly as gen_next does."""
-    n = len(lengths)
-    lo = w * q
-    hi = (1 << 64) - 1 if w + 1 == nwave else lo + q
-    if lo > total or n == 0:
-        return
-    if fixed is not None:
-        L = fixed
-        i = lo // L if L else 0
-        start = i * L
-    else:
-        t = wave_tile[w]
-        i = t * TILE
-        start = prefix[t]
-        while i < n:
-            ln = int(lengths[i])
-            if start + ln > lo or (ln == 0 and start >= lo):
-                break
-            start += ln
-            i += 1
-    while i < n and start < hi:
-        ln = int(lengths[i])
-        a = lo - start if lo > start else 0
-        b = min(hi - start, ln)
-        buf = i
-        i += 1
-        start += ln
-        if ln == 0:
-            yield (buf, None, None, True, False, 0)
-            continue
-        P0 = int(offsets[buf]) + a
-        P1 = int(offsets[buf]) + b
-        yield (buf, P0, P1, a == 0, a != 0 or b != ln, ln - b)
+def quantum(total, nwave):
+    """Slots per wave (k_v7prep): ceil(total / nwave), at least 4, a multiple of 4."""
+    q = (total + nwave - 1) // nwave
+    return 4 if q < 4 else (q + 3) & ~3
 
 
-def span_aligned(P0, P1):
-    return ((P1 + 15) & ~15) - (P0 & ~15)
-
-
-def loads_for_piece(P0, P1):
-    """Chunk addresses (per lane, per load) that the kernel fetches for a piece."""
+def window_loads(P0, length, m):
+    """16-byte chunk addresses of window m of a windowed buffer: (address, used)
+    per lane -- `used` is False for the chunks before the buffer, which the
+    kernel zeroes."""
+    A, E, W, lo, _, _ = geo7(P0, length)
+    wa = A - lo + 1024 * m
+    lc = min(lo, 1008)
     out = []
-    if P1 - P0 < 16:
-        return out  # byte-serial path: reads exactly [P0, P1)
-    end = (P1 + 15) & ~15
-    if span_aligned(P0, P1) <= SMALL:
-        win = end - 1024
-        for lane in range(64):
-            ca = win + int(LD_OFF[lane])
-            if ca + 16 > P0 and ca < P1:
-                out.append(ca)
-        return out
-    nblk = (span_aligned(P0, P1) + 4095) >> 12
-    vbase = end - 4096 * nblk
-    for blk in range(nblk):
-        bb = vbase + 4096 * blk
-        interior = bb >= P0 and bb + 4096 <= P1
-        for k in range(4):
-            for lane in range(64):
-                ca = bb + KOFF[k] + int(LD_OFF[lane])
-                if interior or (ca + 16 > P0 and ca < P1):
-                    out.append(ca)
+    for lane in range(64):
+        off = int(LD_OFF[lane])
+        if m == 0:
+            out.append((wa + max(off, lc), off >= lo))
+        else:
+            out.append((wa + off, True))
     return out
 
 
-def check_decomposition(lengths, offsets, nwave, fixed=None, check_loads=True):
-    """Returns (coverage dict buf -> sorted list of (a, b)), errors list."""
-    lengths = np.asarray(lengths, dtype=np.uint64)
-    offsets = np.asarray(offsets, dtype=np.uint64)
-    if fixed is None:
-        total, q, prefix, wave_tile = plan(lengths, nwave)
-    else:
-        total = int(lengths.size) * fixed
-        per = (total + nwave - 1) // nwave
-        if fixed <= per:
-            q = (per + fixed - 1) // fixed * fixed
-        else:
-            q = 4096 if per < 4096 else (per + 4095) & ~4095
-        prefix = wave_tile = None
-    cover = {}
+def small_loads(P0, length):
+    """Chunk addresses the prep kernel loads for a small buffer (len >= 16)."""
+    A, E, _, _, _, _ = geo7(P0, length)
+    nch = (E - A) >> 4
+    nc = SMALL_SPAN // 16
+    return [A + 16 * min(j, nch - 1) for j in range(nc)]
+
+
+def check_decomposition(lengths, offsets, nwave, check_loads=True):
+    """Returns (coverage dict buf -> sorted chunk addresses, errors list)."""
+    lengths = [int(x) for x in np.asarray(lengths, dtype=np.uint64)]
+    offsets = [int(x) for x in np.asarray(offsets, dtype=np.uint64)]
+    g, Ws, total = slots(lengths, offsets)
     errors = []
+    # (a) slots -> waves: contiguous, disjoint, complete
+    q = quantum(total, nwave)
+    owner = {}
     for w in range(nwave):
-        for buf, P0, P1, first, split, after in pieces_of_wave(w, nwave, lengths, offsets, total, q, prefix,
-                                                               wave_tile, fixed):
-            if P0 is None:
-                cover.setdefault(buf, []).append((0, 0))
-                continue
-            base = int(offsets[buf])
-            cover.setdefault(buf, []).append((P0 - base, P1 - base))
+        for s in range(w * q, min((w + 1) * q, total)):
+            if s in owner:
+                errors.append(("slot twice", s))
+            owner[s] = w
+    if len(owner) != total:
+        errors.append(("slots uncovered", total - len(owner)))
+    cover = {}
+    for i, (off, ln) in enumerate(zip(offsets, lengths)):
+        A, E, W, lo, k0, zt = geo7(off, ln)
+        if ln < 16:
+            continue  # byte-serial in prep: reads exactly [P0, P1)
+        if W == 0:
             if check_loads:
-                for ca in loads_for_piece(P0, P1):
-                    # a 16-byte chunk may only be fetched if it overlaps the piece
-                    if not (ca + 16 > P0 and ca < P1):
-                        errors.append(("load outside piece", w, buf, ca, P0, P1))
-                    if ca % 16:
-                        errors.append(("misaligned load", w, buf, ca))
-    for buf in range(lengths.size):
-        parts = sorted(cover.get(buf, []))
-        ln = int(lengths[buf])
-        if ln == 0:
-            if len(parts) != 1:
-                errors.append(("zero-length buffer not visited exactly once", buf, parts))
+                for ca in small_loads(off, ln):
+                    if not (ca % 16 == 0 and ca + 16 > off and ca < off + ln):
+                        errors.append(("small load outside", i, ca))
             continue
-        pos = 0
-        for a, b in parts:
-            if a != pos:
-                errors.append(("gap/overlap", buf, parts))
-                break
-            pos = b
-        if pos != ln:
-            errors.append(("not fully covered", buf, parts, ln))
+        if not (0 <= lo < 1024):
+            errors.append(("lo", i, lo))
+        used = []
+        for m in range(W):
+            for ca, u in window_loads(off, ln, m):
+                if check_loads and not (ca % 16 == 0 and ca + 16 > off and ca < off + ln):
+                    errors.append(("load outside", i, m, ca))
+                if u:
+                    used.append(ca)
+        used.sort()
+        # (b) the checksummed chunks tile [A, E) exactly once
+        if used != list(range(A, E, 16)):
+            errors.append(("coverage", i, len(used), (E - A) // 16))
+        cover[i] = used
     return cover, errors
