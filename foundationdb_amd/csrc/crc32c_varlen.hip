@@ -201,6 +201,7 @@ __device__ __forceinline__ uint32_t vmul(const uint32_t* tab, uint32_t v) {
 // register times x^(8*65536); a buffer cut by the wave range is finished as a
 // part shifted to its end and XOR-merged (atomicXor) with its other parts.
 constexpr uint32_t kTileW = 256;
+constexpr uint64_t kSelfSumTiles = 8;
 #ifndef FDBCRC_SMALL_SPAN
 #define FDBCRC_SMALL_SPAN 128
 #endif
@@ -262,6 +263,7 @@ struct V7Params {
 	uint64_t* incl;            // per tile: inclusive slot prefix
 	uint64_t ntile, nwave;
 	bool scanned;              // tsum already holds exclusive prefixes (large batches: k_scan ran)
+	bool selfsum;              // small batches: no count kernel, each prep block counts its predecessors' windows
 	uint32_t* gs;              // first slot of each buffer
 	uint32_t* cl;              // lead edge term (team-sum form)
 	uint32_t* dummy;           // 64 words per wave: target of the no-op XORs
@@ -300,6 +302,12 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	uint64_t pre = 0;
 	if (P.scanned) {
 		pre = threadIdx.x == 0 ? P.tsum[tile] : 0;
+	} else if (P.selfsum) {
+		for (uint64_t j = threadIdx.x; j < (uint64_t)tile * kTileW; j += blockDim.x) {
+			uint64_t o, l;
+			v7_buffer(P, j, o, l);
+			pre += geo7(reinterpret_cast<uint64_t>(P.base) + o, l).W;
+		}
 	} else {
 		for (uint32_t k = threadIdx.x; k < tile; k += blockDim.x) pre += P.tsum[k];
 	}
@@ -758,9 +766,12 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.cl = P.gs + count;
 	P.dummy = P.cl + count;
 	// tile prefixes: each prep block sums its predecessors (up to 8192 tiles);
-	// larger batches scan the tile sums first
+	// larger batches scan the tile sums first; batches of at most 8 tiles
+	// skip the count kernel (a prep block counts its predecessors' windows
+	// itself: one launch less, which is most of a small batch's latency)
 	P.scanned = ntile > 8192;
-	k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	P.selfsum = ntile <= kSelfSumTiles;
+	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.scanned) k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4);
 	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	k_varlen7<<<(unsigned)grid, FDBCRC_V7_THREADS, 0, stream>>>(P);
