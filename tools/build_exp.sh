@@ -6,7 +6,7 @@ NAME=$1; shift
 D=build/exp_$NAME
 mkdir -p $D
 for f in foundationdb_amd/csrc/*.hip; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $* -c $f -o $D/$(basename $f).o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -mllvm -amdgpu-atomic-optimizer-strategy=None $* -c $f -o $D/$(basename $f).o &
 done
 for f in foundationdb_amd/csrc/*.cpp; do
   g++ -O3 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $* -c $f -o $D/$(basename $f).o &
