@@ -240,6 +240,7 @@ static unsigned page_grid(uint64_t pages, int num_cus) {
 
 int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream) {
+	if (count == 0) return 0;  // the kernels clamp page indices into a non-empty batch
 	uint32_t* ctr;
 	if (page_counters(stream, num_cus, &ctr)) return -1;
 	switch (blocks_per_page) {
@@ -260,6 +261,7 @@ int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint
 // start, h bytes before the caller's window).
 int launch_pages_window(const uint8_t* pages, uint64_t stride, uint64_t count, uint32_t h, uint32_t t, uint32_t seed,
                         const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream) {
+	if (count == 0) return 0;
 	uint32_t* ctr;
 	if (page_counters(stream, num_cus, &ctr)) return -1;
 	k_pages4k<FDBCRC_PU, true><<<page_grid(count, num_cus), 1024, 0, stream>>>(pages, stride, count, seed, seeds, out,
@@ -272,6 +274,7 @@ int launch_pages_window(const uint8_t* pages, uint64_t stride, uint64_t count, u
 int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32_t* idx, const uint64_t* d_count,
                              uint64_t max_count, uint32_t h, uint32_t t, uint32_t seed, uint32_t* out,
                              const DevTables* tabs, int num_cus, hipStream_t stream) {
+	if (max_count == 0) return 0;
 	uint32_t* ctr;
 	if (page_counters(stream, num_cus, &ctr)) return -1;
 	k_pages4k<FDBCRC_PU, true, true><<<page_grid(max_count, num_cus), 1024, 0, stream>>>(
