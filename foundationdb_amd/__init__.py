@@ -16,6 +16,7 @@ from .crc32c import (  # noqa: F401
     crc32c_combine,
     crc32c_shift,
     fill_splitmix64,
+    poison_lds,
     gpu_init,
     lib,
     varlen_workspace_bytes,

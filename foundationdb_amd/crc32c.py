@@ -70,6 +70,8 @@ def lib():
         L.crc32c_host_unregister.argtypes = [vp]
         L.crc32c_testutil_fill_splitmix64.restype = ctypes.c_int
         L.crc32c_testutil_fill_splitmix64.argtypes = [vp, u64, u64, vp]
+        L.crc32c_testutil_poison_lds.restype = ctypes.c_int
+        L.crc32c_testutil_poison_lds.argtypes = [u32, ctypes.c_int, vp]
         _lib = L
     return _lib
 
@@ -184,6 +186,11 @@ def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=Non
                 _stream_handle(stream))
     _check(rc, "crc32c_gpu_batch_varlen")
     return out
+
+
+def poison_lds(pattern=0xA5A5A5A5, blocks=2048, stream=None):
+    """Test utility: leave garbage in every CU's LDS (see fdb_crc32c_testutil.h)."""
+    _check(lib().crc32c_testutil_poison_lds(pattern & 0xFFFFFFFF, blocks, _stream_handle(stream)), "poison_lds")
 
 
 def fill_splitmix64(buf, state, stream=None):

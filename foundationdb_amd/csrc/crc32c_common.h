@@ -30,30 +30,35 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // LDS fill: slice4 (1024 words) to all 32 columns, lane tables to their column.
+// Any block size: each round keeps kPer global loads per thread in flight
+// (one round for blocks of 768 or more threads).  Every entry of the image is
+// written: a kernel must never depend on what an earlier kernel left in LDS.
 __device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t) {
 	constexpr uint32_t kSlice = 1024, kLane = 64 * 128;
 	constexpr uint32_t kCompact = kSlice + kLane;  // 9216 words
-	constexpr uint32_t kPer = (kCompact + 1023) / 1024;
+	constexpr uint32_t kPer = 12;                  // 12 x 768 = 9216
 	const uint32_t* s4 = &t->slice4[0][0];
 	const uint32_t* ln = &t->lane[0][0][0];
-	uint32_t v[kPer];
+	for (uint32_t q0 = 0; q0 < kCompact; q0 += kPer * blockDim.x) {
+		uint32_t v[kPer];
 #pragma unroll
-	for (uint32_t i = 0; i < kPer; ++i) {
-		const uint32_t q = threadIdx.x + i * blockDim.x;
-		v[i] = q < kSlice ? s4[q] : (q < kCompact ? ln[q - kSlice] : 0u);
-	}
+		for (uint32_t i = 0; i < kPer; ++i) {
+			const uint32_t q = q0 + threadIdx.x + i * blockDim.x;
+			v[i] = q < kSlice ? s4[q] : (q < kCompact ? ln[q - kSlice] : 0u);
+		}
 #pragma unroll
-	for (uint32_t i = 0; i < kPer; ++i) {
-		const uint32_t q = threadIdx.x + i * blockDim.x;
-		if (q < kSlice) {  // slice4[k][idx], k = 0..3 -> T3,T2 | T1,T0 regions
-			const uint32_t k = q >> 8, idx = q & 255;
-			uint32_t* d = lds + (kS4Off / 4) + (k >> 1) * 16384 + (idx * 2 + (k & 1)) * 32;
+		for (uint32_t i = 0; i < kPer; ++i) {
+			const uint32_t q = q0 + threadIdx.x + i * blockDim.x;
+			if (q < kSlice) {  // slice4[k][idx], k = 0..3 -> T3,T2 | T1,T0 regions
+				const uint32_t k = q >> 8, idx = q & 255;
+				uint32_t* d = lds + (kS4Off / 4) + (k >> 1) * 16384 + (idx * 2 + (k & 1)) * 32;
 #pragma unroll
-			for (int c = 0; c < 32; ++c) d[c] = v[i];
-		} else if (q < kCompact) {
-			const uint32_t r = q - kSlice;
-			const uint32_t l = r >> 7, nv = r & 127;
-			lds[(kS4LaneOff / 4) + (l >> 5) * 4096 + nv * 32 + (l & 31)] = v[i];
+				for (int c = 0; c < 32; ++c) d[c] = v[i];
+			} else if (q < kCompact) {
+				const uint32_t r = q - kSlice;
+				const uint32_t l = r >> 7, nv = r & 127;
+				lds[(kS4LaneOff / 4) + (l >> 5) * 4096 + nv * 32 + (l & 31)] = v[i];
+			}
 		}
 	}
 	__syncthreads();

@@ -19,7 +19,22 @@ __global__ void k_splitmix64(uint64_t* __restrict__ dst, uint64_t nwords, uint64
 	}
 }
 
+// Fills all of a workgroup's LDS with a pattern, one workgroup per CU and
+// more: the next kernels on those CUs start with garbage in LDS, as they may
+// on a GPU that ran other work (tests: no kernel may read LDS it did not write).
+__global__ __launch_bounds__(1024) void k_poison_lds(uint32_t pattern) {
+	__shared__ uint32_t lds[160 * 1024 / 4];
+	for (uint32_t k = threadIdx.x; k < 160 * 1024 / 4; k += blockDim.x) lds[k] = pattern ^ (k * 0x9E3779B9u);
+	__syncthreads();
+	if (lds[(threadIdx.x * 37) % (160 * 1024 / 4)] == 0x12345678u && pattern == 0u) lds[0] = 1u;  // keep the stores
+}
+
 }  // namespace fdbcrc
+
+extern "C" int crc32c_testutil_poison_lds(uint32_t pattern, int blocks, void* stream) {
+	fdbcrc::k_poison_lds<<<(unsigned)(blocks > 0 ? blocks : 1), 1024, 0, reinterpret_cast<hipStream_t>(stream)>>>(pattern);
+	return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 extern "C" int crc32c_testutil_fill_splitmix64(void* d_dst, uint64_t nwords, uint64_t state, void* stream) {
 	if (nwords == 0) return 0;

@@ -10,6 +10,10 @@ extern "C" {
  * (BASELINE.md generator: z = state + (k+1)*0x9E3779B97F4A7C15, then the
  * standard splitmix64 finaliser).  Asynchronous on `stream` (hipStream_t). */
 int crc32c_testutil_fill_splitmix64(void* d_dst, uint64_t nwords, uint64_t state, void* stream);
+/* Launches `blocks` workgroups that fill their whole 160 KiB LDS with a
+ * pattern, so that the next kernels on those CUs start with garbage in LDS
+ * (tests: no kernel may depend on LDS contents it did not write). */
+int crc32c_testutil_poison_lds(uint32_t pattern, int blocks, void* stream);
 #ifdef __cplusplus
 }
 #endif
