@@ -425,7 +425,7 @@ __device__ __forceinline__ bool slot_edge(uint32_t f) {
 }
 
 #ifndef FDBCRC_V7_THREADS
-#define FDBCRC_V7_THREADS 768  // 12 waves per CU: 168 VGPRs per lane, no spills
+#define FDBCRC_V7_THREADS 768  // 12 waves per CU: 155 VGPRs per lane, no VGPR spills
 #endif
 __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	__shared__ uint32_t lds[kLdsBytesB / 4];
