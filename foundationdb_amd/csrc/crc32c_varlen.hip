@@ -201,6 +201,17 @@ __device__ __forceinline__ uint32_t vmul(const uint32_t* tab, uint32_t v) {
 // register times x^(8*65536); a buffer cut by the wave range is finished as a
 // part shifted to its end and XOR-merged (atomicXor) with its other parts.
 constexpr uint32_t kTileW = 256;
+#ifndef FDBCRC_V7_THREADS
+#define FDBCRC_V7_THREADS 768  // 12 waves per CU: 155 VGPRs per lane, no VGPR spills
+#endif
+// Slot ranges per wave.  R > 1: a workgroup owns R ranges per wave; each wave
+// starts on one and grabs the next from its workgroup's counter as it
+// finishes (the SIMD's issue arbitration favours older waves, so equal
+// ranges finish at different times).
+#ifndef FDBCRC_V7_RANGES
+#define FDBCRC_V7_RANGES 1
+#endif
+constexpr uint64_t kV7RangesPerBlock = (FDBCRC_V7_THREADS / 64) * FDBCRC_V7_RANGES;
 constexpr uint64_t kSelfSumTiles = 8;
 #ifndef FDBCRC_SMALL_SPAN
 #define FDBCRC_SMALL_SPAN 128
@@ -267,6 +278,7 @@ struct V7Params {
 	uint32_t* gs;              // first slot of each buffer
 	uint32_t* cl;              // lead edge term (team-sum form)
 	uint32_t* dummy;           // 64 words per wave: target of the no-op XORs
+	uint32_t* ctr;             // per workgroup: slot ranges grabbed (FDBCRC_V7_RANGES > 1)
 	const DevTables* tabs;
 };
 __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_t& off, uint64_t& len) {
@@ -297,6 +309,10 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 #pragma unroll
 	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = T->slice4[k][threadIdx.x];
 	const uint32_t tile = blockIdx.x;
+#if FDBCRC_V7_RANGES > 1
+	if (tile == 0)
+		for (uint64_t k = threadIdx.x; k < P.nwave / kV7RangesPerBlock; k += 256) P.ctr[k] = 0;
+#endif
 	// exclusive slot prefix of this tile: the sum of all earlier tile sums,
 	// read in parallel by the whole block (no inter-block waiting)
 	uint64_t pre = 0;
@@ -424,9 +440,6 @@ __device__ __forceinline__ bool slot_edge(uint32_t f) {
 	return (f & k7_LO) || ((f & (k7_FIN | k7_PEND)) == k7_FIN && ((f >> k7_ZT) & 15u));
 }
 
-#ifndef FDBCRC_V7_THREADS
-#define FDBCRC_V7_THREADS 768  // 12 waves per CU: 155 VGPRs per lane, no VGPR spills
-#endif
 __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const DevTables* __restrict__ T = P.tabs;
@@ -437,12 +450,19 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
 	fill_lds_b(lds, T);
 	const uint64_t wpb = blockDim.x >> 6;
-	const uint64_t w = (uint64_t)blockIdx.x * wpb + rdfirst(threadIdx.x >> 6);
 	typedef __attribute__((address_space(1))) const uint64_t g_u64;
 	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
 	const uint64_t total = rdfirst64(hp[0]), Qs = rdfirst64(hp[1]);
+	const uint64_t r_base = (uint64_t)blockIdx.x * kV7RangesPerBlock;
+	uint64_t w = r_base + rdfirst(threadIdx.x >> 6);
+	for (;;) {
 	const uint64_t lo_s64 = w * Qs;
-	if (lo_s64 >= total) return;
+	if (lo_s64 >= total || w >= r_base + kV7RangesPerBlock) return;
+#if FDBCRC_V7_RANGES > 1
+	// the next range, requested now: the atomic returns in the shadow of this range
+	uint32_t nxt = 0;
+	if (lane == 0) nxt = atomicAdd(P.ctr + blockIdx.x, 1u);
+#endif
 	const uint32_t lo_s = (uint32_t)lo_s64;
 	const uint32_t hi_s = (uint32_t)(lo_s64 + Qs < total ? lo_s64 + Qs : total);
 	// the tile holding slot lo_s: the number of tiles whose inclusive prefix is
@@ -739,19 +759,27 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		sb += 64;
 		if (!f0) phase2(t1);
 	}
+#if FDBCRC_V7_RANGES > 1
+	w = r_base + wpb + rdfirst(__shfl((int)nxt, 0));
+#else
+	(void)wpb;
+	return;
+#endif
+	}
 }
 
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 	nwave = nwave > 16 * 1024 ? nwave : 16 * 1024;  // covers any launch geometry up to 1024 CUs
+	nwave *= FDBCRC_V7_RANGES;                      // virtual waves: one per slot range
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
-	return 16 + 16 * (ntile + 1) + 4 * nwave + 8 * count + 256 * nwave + 64;
+	return 16 + 16 * (ntile + 1) + 4 * nwave + 8 * count + 256 * nwave + 4 * nwave + 64;
 }
 
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                    const DevTables* tabs, int num_cus, void* ws, hipStream_t stream) {
 	const uint64_t grid = (uint64_t)num_cus;
-	const uint64_t nwave = grid * (FDBCRC_V7_THREADS / 64);
+	const uint64_t nwave = grid * kV7RangesPerBlock;  // one virtual wave per slot range
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
 	uint8_t* wp = static_cast<uint8_t*>(ws);
 	V7Params P{};
@@ -765,6 +793,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.gs = wave_tile + nwave;
 	P.cl = P.gs + count;
 	P.dummy = P.cl + count;
+	P.ctr = P.dummy + 64 * nwave;
 	// tile prefixes: each prep block sums its predecessors (up to 8192 tiles);
 	// larger batches scan the tile sums first; batches of at most 8 tiles
 	// skip the count kernel (a prep block counts its predecessors' windows
