@@ -4,6 +4,8 @@
 #include <string.h>
 
 #include <map>
+#include <memory>
+#include <new>
 #include <mutex>
 #include <string>
 
@@ -53,12 +55,15 @@ int device_state(DeviceState** st) {
 		int cus = 0;
 		e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
 		if (e != hipSuccess) return fail(FDB_CRC32C_ENODEV, "hipDeviceGetAttribute", e);
-		DevTables host;
-		build_dev_tables(&host);
+		// ~1.3 MB: built on the heap, since the first call may come from a
+		// thread with a small stack (SQLite readers, Flow's network thread)
+		std::unique_ptr<DevTables> host(new (std::nothrow) DevTables);
+		if (!host) return fail(FDB_CRC32C_ENOMEM, "host tables");
+		build_dev_tables(host.get());
 		DevTables* dt = nullptr;
 		e = hipMalloc(reinterpret_cast<void**>(&dt), sizeof(DevTables));
 		if (e != hipSuccess) return fail(FDB_CRC32C_ENOMEM, "hipMalloc(tables)", e);
-		e = hipMemcpy(dt, &host, sizeof(DevTables), hipMemcpyHostToDevice);
+		e = hipMemcpy(dt, host.get(), sizeof(DevTables), hipMemcpyHostToDevice);
 		if (e != hipSuccess) {
 			(void)hipFree(dt);
 			return fail(FDB_CRC32C_EHIP, "hipMemcpy(tables)", e);
@@ -106,7 +111,7 @@ int check_launch(const char* what) {
 // Grab counters of the page kernels for `stream` on the current device:
 // zeroed once here, left at zero by every page launch.
 int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr) {
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	std::lock_guard<std::mutex> lock(g_mu);
 	uint32_t*& p = st->ctr[stream];
@@ -128,7 +133,7 @@ int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr) {
 
 // used by the host pipeline (crc32c_pipeline.cpp)
 int device_tables(const DevTables** tabs, int* num_cus) {
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	*tabs = st->tables;
 	*num_cus = st->num_cus;
@@ -183,7 +188,7 @@ void debug_window_varlen(const void* base, const uint64_t* d_off, const uint64_t
 extern "C" {
 
 int crc32c_gpu_init(void) {
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	return device_state(&st);
 }
 
@@ -191,7 +196,7 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
                            const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
 	if (count == 0) return 0;
 	if (!d_out || (!d_base && length)) return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_fixed: null pointer");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 	const uint8_t* base = static_cast<const uint8_t*>(d_base);
@@ -229,7 +234,7 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
 }
 
 uint64_t crc32c_gpu_varlen_workspace_bytes(uint64_t count) {
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (device_state(&st)) return 0;
 	return varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16);
 }
@@ -240,7 +245,7 @@ int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, co
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths || !d_base)
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	const uint64_t need = varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16);
 	if (!d_workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(d_workspace) % 16)
@@ -262,7 +267,7 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths || !d_base)
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
@@ -278,7 +283,7 @@ int xxh3_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length, u
                          const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
 	if (count == 0) return 0;
 	if (!d_out || (!d_base && length)) return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_fixed: null pointer");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	fdbxxh::XxhParams P{};
 	P.base = static_cast<const uint8_t*>(d_base);
@@ -294,7 +299,7 @@ int xxh3_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length, u
 }
 
 uint64_t xxh3_gpu_varlen_workspace_bytes(uint64_t count) {
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (device_state(&st)) return 0;
 	return fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus));
 }
@@ -305,7 +310,7 @@ int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, cons
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths || !d_base)
 		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: null pointer");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	const uint64_t need = fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus));
 	if (!d_workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(d_workspace) % 16)
@@ -328,7 +333,7 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths || !d_base)
 		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: null pointer");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
@@ -361,7 +366,7 @@ int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t
 	if (int rc = pages_ok(d_pages, page_size, count, d_status, "fdb_sqlite_verify_pages: null pointer")) return rc;
 	if (!d_workspace || workspace_bytes < fdbpc::workspace_bytes(count) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
 		return fail(FDB_CRC32C_EINVAL, "fdb_sqlite_verify_pages: workspace too small or misaligned");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	if (fdbpc::sqlite_verify(static_cast<const uint8_t*>(d_pages), page_size, count, first_pgno, d_status, d_bad,
 	                         st->tables, st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream)))
@@ -374,7 +379,7 @@ int fdb_sqlite_verify_pages(const void* d_pages, uint64_t page_size, uint64_t co
 	if (count == 0) return fdb_sqlite_verify_pages_ws(d_pages, page_size, 0, first_pgno, d_status, d_bad, nullptr, 0,
 	                                                  stream);
 	if (int rc = pages_ok(d_pages, page_size, count, d_status, "fdb_sqlite_verify_pages: null pointer")) return rc;
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
@@ -392,7 +397,7 @@ int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d
 	if (int rc = pages_ok(d_pages, 4096, count, d_ok, "fdb_diskqueue_check_pages: null pointer")) return rc;
 	if (!d_workspace || workspace_bytes < fdbpc::workspace_bytes(count) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
 		return fail(FDB_CRC32C_EINVAL, "fdb_diskqueue_check_pages: workspace too small or misaligned");
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	if (fdbpc::diskqueue_check(static_cast<const uint8_t*>(d_pages), count, d_ok, d_bad, st->tables, st->num_cus,
 	                           d_workspace, reinterpret_cast<hipStream_t>(stream)))
@@ -403,7 +408,7 @@ int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d
 int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad, void* stream) {
 	if (count == 0) return fdb_diskqueue_check_pages_ws(d_pages, 0, d_ok, d_bad, nullptr, 0, stream);
 	if (int rc = pages_ok(d_pages, 4096, count, d_ok, "fdb_diskqueue_check_pages: null pointer")) return rc;
-	DeviceState* st;
+	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
