@@ -216,6 +216,10 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
 		rc = launch_pages_window(base - h, stride, count, (uint32_t)h, (uint32_t)(4096 - h - length), seed, d_seeds,
 		                         d_out, st->tables, st->num_cus, s);
 	else {
+		// the varlen engine numbers 1 KiB windows with 32-bit slot indices
+		const uint64_t wpb = (length + 30) / 1024 + 1;  // windows per buffer, an upper bound
+		if (count >= (1ull << 32) / wpb)
+			return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_fixed: batch covers 2^32 or more 1 KiB windows");
 #ifdef FDBCRC_DEBUG
 		crc32c_debug_bounds((uint64_t)base, (uint64_t)base + (count - 1) * stride + length);
 #endif

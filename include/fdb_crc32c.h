@@ -87,7 +87,11 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
  * 64 B packets is split over several wavefronts and merged on the device.
  * Uses a library-owned workspace per (device, stream); it is allocated on
  * first use and grown (with one stream synchronisation) when a larger batch
- * arrives. */
+ * arrives.
+ * Limit: the engine numbers 1 KiB windows with 32-bit slot indices, so a
+ * batch may cover fewer than 2^32 windows in total (about 4 TiB of checksummed
+ * bytes, overlapping buffers counted once each) -- far above what one GPU
+ * holds unless buffers overlap heavily. */
 int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                             uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
 
