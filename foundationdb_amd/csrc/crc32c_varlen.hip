@@ -406,13 +406,17 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	// end is masked by the streaming kernel (it always sits in lane 63).
 	u32x4 ch = u32x4{0u, 0u, 0u, 0u};
 	if (g.k0) ch = ld16(reinterpret_cast<const uint8_t*>(g.A));
+	// Four 4-byte steps: the garbage bytes below k0 kept (~lm), ~seed XORed in
+	// at byte k0 (inj); for k0 > 12 the part of ~seed past the chunk is still
+	// in the register after it (spill).
+	const Masks mk = edge_masks(g.k0, 16u, s0);
 	uint32_t x = 0;
 #pragma unroll
-	for (uint32_t b = 0; b < 16; ++b) {
-		if (b == g.k0) x ^= s0;
-		const uint32_t byte = b < g.k0 ? (ch[b >> 2] >> (8 * (b & 3))) & 255u : 0u;
-		x = (x >> 8) ^ s4[3][(x ^ byte) & 255u];
+	for (int d = 0; d < 4; ++d) {
+		x ^= (ch[d] & ~mk.lm[d]) ^ mk.inj[d];
+		x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
 	}
+	x ^= mk.spill;
 	P.cl[i] = vmul(&T->chunkpow[64u * (gi & 3u) + (g.lo >> 4)][0][0], x);
 }
 
