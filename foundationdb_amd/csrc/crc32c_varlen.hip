@@ -373,13 +373,15 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		// small buffer: its chunks [A, E) as 4-byte words from a zero register,
 		// the bytes before P0 zeroed and ~seed injected at P0 (crc32c.cpp:197),
 		// the zt bytes after P1 zeroed and then divided out (x^(-8 zt)).  All
-		// chunk loads are issued first (clamped to the last chunk): one latency.
+		// chunk loads are issued first: one latency.
 		constexpr uint32_t NC = kSmallSpan / 16;
 		const uint32_t nch = (uint32_t)(((P0 + len + 15) & ~uint64_t(15)) - g.A) >> 4;
+		// chunks past the buffer's last are not loaded (exec-masked: 1 Mi x 64 B
+		// packets 0.057 -> 0.048 ms against clamped re-reads of the last chunk)
 		u32x4 ch[NC];
 #pragma unroll
 		for (uint32_t j = 0; j < NC; ++j)
-			ch[j] = ld16(reinterpret_cast<const uint8_t*>(g.A + 16 * (j < nch ? j : nch - 1)));
+			ch[j] = j < nch ? ld16(reinterpret_cast<const uint8_t*>(g.A + 16 * j)) : u32x4{0u, 0u, 0u, 0u};
 		const Masks mk = edge_masks(g.k0, 16u - g.zt, s0);
 		uint32_t x = 0;
 #pragma unroll
