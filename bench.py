@@ -94,6 +94,36 @@ def cpu_baseline(wl, seconds):
                       f"core {core} of {len(old)} allowed; host CPU: {cpu_model()}"}
 
 
+def cpu_baseline_threads(wl, seconds, threads=16):
+    """Context only: the reference crc32c_append over the same sample split
+    across `threads` host threads (the GPU box's CPU share is 16 cores per
+    GPU); ctypes releases the GIL, so the slices run in parallel.  Fixed-stride
+    samples only; None otherwise."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    sample = wl.cpu_sample()
+    if sample.offsets is not None or sample.ref or not sample.available(O):
+        return None
+    n = max(1, min(threads, len(os.sched_getaffinity(0))))
+    cuts = [sample.count * k // n for k in range(n + 1)]
+    parts = [(sample.buf[cuts[k] * sample.stride:], cuts[k + 1] - cuts[k]) for k in range(n)]
+
+    def once(pool):
+        t = time.perf_counter()
+        list(pool.map(lambda bc: O.reference_batch_fixed(bc[0], sample.stride, sample.length, bc[1],
+                                                         seed=sample.seed), parts))
+        return time.perf_counter() - t
+
+    with ThreadPoolExecutor(n) as pool:
+        once(pool)
+        best, total, reps = 1e30, 0.0, 0
+        while total < seconds or reps < 3:
+            dt = once(pool)
+            best, total, reps = min(best, dt), total + dt, reps + 1
+    return {"value": round(sample.nbytes / best / GIB, 3), "unit": "GiB/s", "cores": n, "kind": "reference",
+            "sample": f"{sample.desc}; {n} threads over contiguous slices, best of {reps} passes"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,6 +229,9 @@ def main():
             rec["data"] = "DRY RUN on CPU (harness test, not a measurement)"
         elif args.cpu_seconds > 0 and world == 1:  # reported at N=1 only
             rec["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
+            mt = cpu_baseline_threads(wl, min(args.cpu_seconds, 3.0))
+            if mt:
+                rec["cpu_baseline_threads"] = mt  # context: the same reference path on 16 host cores
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
