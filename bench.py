@@ -7,10 +7,16 @@ pass of the engine over the whole batch (one kernel launch).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload pages4k|pages8k|zipf|chunks]
 
-N > 1 is launched by torch.distributed.run, one rank per GPU.  Pages shard
-trivially: every rank checksums its own batch of the same shape (weak
-scaling, no data-path collective); RCCL is used only to take the max elapsed
-time over ranks and to gather the per-rank byte counts.
+N > 1: one rank per GPU.  Started as `python bench.py --gpus N` (no
+WORLD_SIZE in the environment) it launches `torch.distributed.run
+--nproc-per-node N` on itself as a child process, before anything touches the
+GPU, and exits with the child's status; under an outer launcher it uses the
+launcher's ranks.  Every rank checks that the world size equals --gpus.
+Pages shard trivially (the whole-file scan of
+fdbserver/kvstore/KeyValueStoreSQLite.cpp:1378-1470 split by page range):
+every rank checksums its own batch of the same shape (weak scaling, no
+data-path collective); RCCL is used only to take the max elapsed time over
+ranks and to gather the per-rank byte counts and kernel times.
 
 Rank 0 prints ONE JSON line.  `value` is GiB/s of buffer bytes read, whole
 job, from the host clock around the K timed steps.  `roofline.achieved` is the
@@ -124,16 +130,37 @@ def cpu_baseline_threads(wl, seconds, threads=16):
             "sample": f"{sample.desc}; {n} threads over contiguous slices, best of {reps} passes"}
 
 
+def launch_ranks(args):
+    """`--gpus N` without an outer launcher: run torch.distributed.run on this
+    script as a child process (never an exec: nothing here has touched the GPU
+    yet, and the parent never does) and return its exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: world size {world} != --gpus {args.gpus}")
     dry = args.dry_cpu
     if dry:
         dev = torch.device("cpu")
         if world > 1:
             dist.init_process_group("gloo")
+            assert dist.get_world_size() == args.gpus
         wl = W.DryCpuPages(rank)
         sync = lambda: None  # noqa: E731
         stream = None
@@ -141,6 +168,8 @@ def main():
         if world > 1:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if dist.get_world_size() != args.gpus:
+                sys.exit(f"bench.py: RCCL world size {dist.get_world_size()} != --gpus {args.gpus}")
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
         F.gpu_init()
@@ -177,19 +206,16 @@ def main():
     if not args.no_verify:
         ok = wl.verify()
 
-    stats = torch.tensor([elapsed, float(wl.bytes_per_step), 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, float(wl.bytes_per_step), 0.0 if ok else 1.0, kernel_ms], dtype=torch.float64,
+                         device=dev)
+    per_rank = [stats]
     if world > 1:
-        t_max = stats[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        bytes_all = stats[1:2].clone()
-        dist.all_reduce(bytes_all, op=dist.ReduceOp.SUM)
-        bad = stats[2:3].clone()
-        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
-        elapsed = float(t_max.item())
-        total_bytes = float(bytes_all.item()) * args.steps
-        ok = bad.item() == 0
-    else:
-        total_bytes = float(wl.bytes_per_step) * args.steps
+        per_rank = [torch.empty_like(stats) for _ in range(world)]
+        dist.all_gather(per_rank, stats)
+    per_rank = [[float(x) for x in t.cpu()] for t in per_rank]
+    elapsed = max(r[0] for r in per_rank)
+    total_bytes = sum(r[1] for r in per_rank) * args.steps
+    ok = all(r[2] == 0.0 for r in per_rank)
 
     if rank == 0:
         value = total_bytes / elapsed / GIB
@@ -197,7 +223,7 @@ def main():
         achieved = wl.algorithmic_bytes_per_step / (kernel_ms * 1e-3) / 1e9
         peak = wl.pcie_peak_gbs if host_timed else HBM_PEAK_GBS
         rec = {
-            "metric": getattr(wl, "metric", METRIC),
+            "metric": getattr(wl, "metric", None) or METRIC,
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -213,6 +239,9 @@ def main():
                                                   "for max-time / byte-count reduction"),
             "pct_of_hbm_read_peak": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS, 2),
             "parity_ok": bool(ok),
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "per_rank": [{"rank": i, "bytes_per_step": int(r[1]), "elapsed_s": round(r[0], 6),
+                          "avg_launch_ms": round(r[3], 4), "parity_ok": r[2] == 0.0} for i, r in enumerate(per_rank)],
             "roofline": {
                 "bound": "pcie" if host_timed else "hbm",
                 "kernel": wl.kernel_name,

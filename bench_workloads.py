@@ -72,10 +72,13 @@ class CpuSample:
 
 
 class Pages:
+    """configs[1] (4 KiB) and configs[3]'s per-GPU shard (8 KiB SQLite pages)."""
 
     def __init__(self, dev, rank, page_bytes=4096, count=1 << 20, seed=0):
         self.dev, self.page_bytes, self.count, self.seed = dev, page_bytes, count, seed
         self.kernel_name = "fdbcrc::k_pages4k<2>" if page_bytes == 4096 else "fdbcrc::k_pages4k<2, PAIR> (8 KiB pages as block pairs)"
+        if page_bytes != 4096:
+            self.metric = f"device-resident CRC32C GiB/s on {page_bytes // 1024} KiB page batches; % of HBM-read peak"
         self.buf = torch.empty(count * page_bytes, dtype=torch.uint8, device=dev)
         F.fill_splitmix64(self.buf, STATE)
         self.out = torch.empty(count, dtype=torch.uint32, device=dev)
@@ -126,8 +129,9 @@ def _spot_check(buf, offsets, lengths, seed, got, n=512):
 class VarLen:
     kernel_name = "fdbcrc::k_varlen7 (+ k_v7count, k_v7prep)"
 
-    def __init__(self, dev, rank, lengths, align, desc, seed=0):
+    def __init__(self, dev, rank, lengths, align, desc, seed=0, metric=None):
         self.dev, self.seed = dev, seed
+        self.metric = metric
         lengths = np.asarray(lengths, dtype=np.uint64)
         padded = (lengths + (align - 1)) // align * align
         offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.uint64)
@@ -193,6 +197,7 @@ class HostChunks:
     through the pinned H2D -> kernel -> D2H pipeline (4 streams, 64 MiB segments).
     The rate includes both PCIe copies; it is PCIe-bound by design."""
     kernel_name = "host pipeline (H2D + fdbcrc::k_varlen7 + D2H)"
+    metric = "host-to-host CRC32C GiB/s on 4 KiB-1 MiB chunk batches (pinned H2D + kernel + D2H); % of PCIe peak"
     host_timed = True
     pcie_peak_gbs = 63.0  # PCIe Gen5 x16 per direction, MI355X_MICROARCH.md
 
@@ -245,6 +250,7 @@ class HostPages(HostChunks):
     -> D2H pipeline (4 streams, 64 MiB segments).  PCIe-bound by design; the
     device-resident rate of the same batch is the `pages4k` workload."""
     kernel_name = "host pipeline (H2D + fdbcrc::k_pages4k + D2H)"
+    metric = "host-to-host CRC32C GiB/s on 4 KiB page batches (pinned H2D + kernel + D2H); % of PCIe peak"
 
     def __init__(self, dev, rank, count=1 << 20, seed=0):
         self.count, self.seed = count, seed
@@ -352,9 +358,13 @@ WORKLOADS = {
     "pages4k": lambda dev, rank: Pages(dev, rank, 4096, 1 << 20, 0),
     "pages8k": lambda dev, rank: Pages(dev, rank, 8192, 1 << 19, 0xFDBEEFDB),
     "zipf": lambda dev, rank: VarLen(dev, rank, zipf_lengths(), 256,
-                                     "Zipf(1.0) packet sizes 64 B - 16 KiB, ~1 GiB per batch, 256 B-aligned offsets"),
+                                     "Zipf(1.0) packet sizes 64 B - 16 KiB, ~1 GiB per batch, 256 B-aligned offsets",
+                                     metric="device-resident CRC32C GiB/s on Zipf 64 B-16 KiB packet batches; "
+                                            "% of HBM-read peak"),
     "chunks": lambda dev, rank: VarLen(dev, rank, chunk_lengths(), 4096,
-                                       "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch"),
+                                       "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch",
+                                       metric="device-resident CRC32C GiB/s on 4 KiB-1 MiB chunk batches; "
+                                              "% of HBM-read peak"),
     "chunks-host": lambda dev, rank: HostChunks(dev, rank),
     "pages4k-host": lambda dev, rank: HostPages(dev, rank),
     "xxh3-pages4k": lambda dev, rank: Xxh3Pages(dev, rank),

@@ -79,9 +79,30 @@ def test_shard_bounds_cover():
         assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
 
 
-def test_bench_dry_run_two_ranks():
-    """bench.py's N>1 aggregation (barrier, max time over ranks, byte sum) under
-    torch.distributed.run with gloo on CPU (--dry-cpu: host checksums)."""
+def _bench(args, env=None, timeout=300):
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, cwd=ROOT, env=dict(os.environ, OMP_NUM_THREADS="1", **(env or {})))
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`python bench.py --gpus 2` exactly as the driver calls it (no outer
+    launcher): bench.py starts two ranks itself, every rank checks the world
+    size, and rank 0's single line aggregates both (barrier, max time over
+    ranks, byte sum, per-rank kernel times).  --dry-cpu: gloo + host checksums."""
+    r = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-cpu"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["scaling"] == "weak" and rec["parity_ok"]
+    assert [p["rank"] for p in rec["per_rank"]] == [0, 1]
+    assert sum(p["bytes_per_step"] for p in rec["per_rank"]) * 3 / rec["value"] / (1 << 30) == \
+        pytest.approx(max(p["elapsed_s"] for p in rec["per_rank"]), rel=0.02)
+    assert rec["value"] > 0 and rec["steps"] == 3
+
+
+def test_bench_under_outer_launcher():
+    """The same harness under an outer torch.distributed.run (ranks from the env)."""
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
@@ -92,5 +113,12 @@ def test_bench_dry_run_two_ranks():
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 2 and rec["scaling"] == "weak" and rec["parity_ok"]
-    assert rec["value"] > 0 and rec["steps"] == 3
+    assert rec["n_gpus"] == 2 and rec["parity_ok"] and len(rec["per_rank"]) == 2
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A world size that disagrees with --gpus is an error, never a mislabelled line."""
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--dry-cpu"],
+               env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
+    assert r.returncode != 0 and "world size 1 != --gpus 2" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
