@@ -1,0 +1,76 @@
+"""Batch shapes of the BASELINE.json variable-length configs, torch-free so the
+golden-vector script (tests/golden/make_golden.py), the GPU tests and
+bench_workloads.py all build the very same batches.
+
+configs[2]  Zipf packet sizes 64 B - 16 KiB        zipf_lengths(),  offsets 256 B aligned
+configs[4]  log-uniform 4 KiB - 1 MiB backup chunks chunk_lengths(), offsets 4 KiB aligned
+
+Data bytes are the splitmix64 stream (BASELINE.md generator, state 0x5EED)
+laid over the whole padded extent, so buffer i is bytes
+[offsets[i], offsets[i] + lengths[i]) of that stream.
+"""
+import hashlib
+
+import numpy as np
+
+STATE = 0x5EED
+ZIPF_ALIGN = 256
+CHUNK_ALIGN = 4096
+
+
+def zipf_lengths(total_bytes=1 << 30, seed=1):
+    """Packet sizes: bucket k in 1..256 with P(k) ~ 1/k (Zipf, exponent 1.0),
+    length = clip(64*k - u, 64, 16384) with u uniform in [0, 63]."""
+    rng = np.random.default_rng(seed)
+    k = np.arange(1, 257)
+    p = (1.0 / k) / (1.0 / k).sum()
+    mean = float((p * (64 * k - 31.5)).sum())
+    n = int(total_bytes / mean)
+    ks = rng.choice(k, size=n, p=p)
+    u = rng.integers(0, 64, n)
+    return np.clip(64 * ks - u, 64, 16384).astype(np.uint64)
+
+
+def chunk_lengths(total_bytes=1 << 30, seed=5):
+    """Backup-sized chunks, log-uniform on [4 KiB, 1 MiB]."""
+    rng = np.random.default_rng(seed)
+    out, tot = [], 0
+    while tot < total_bytes:
+        L = int(np.exp(rng.uniform(np.log(4096), np.log(1 << 20))))
+        out.append(L)
+        tot += L
+    return np.array(out, dtype=np.uint64)
+
+
+def layout(lengths, align):
+    """Back-to-back buffers, each starting at a multiple of `align`.
+    Returns (offsets u64, extent in bytes rounded up to 8)."""
+    lengths = np.asarray(lengths, dtype=np.uint64)
+    padded = (lengths + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.uint64)
+    total = int(offsets[-1] + padded[-1]) if lengths.size else 0
+    return offsets, (total + 7) // 8 * 8
+
+
+def lengths_digest(lengths):
+    """sha256 of the little-endian u64 length list: pins the shape across numpy versions."""
+    return hashlib.sha256(np.ascontiguousarray(lengths, dtype="<u8").tobytes()).hexdigest()
+
+
+SHAPES = {
+    "zipf": (zipf_lengths, ZIPF_ALIGN),
+    "chunks": (chunk_lengths, CHUNK_ALIGN),
+}
+
+
+def shape(name):
+    """(lengths, offsets, extent_bytes) of the named configs batch."""
+    fn, align = SHAPES[name]
+    lengths = fn()
+    offsets, extent = layout(lengths, align)
+    return lengths, offsets, extent
+
+
+def digest(crcs):
+    crcs = np.asarray(crcs, dtype=np.uint32)
+    return {"xor": int(np.bitwise_xor.reduce(crcs)) if crcs.size else 0, "sum": int(crcs.astype(np.uint64).sum())}

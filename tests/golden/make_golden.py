@@ -8,8 +8,10 @@ a splitmix64 stream (BASELINE.md generator) or a closed-form pattern, so the
 JSON holds parameters and the reference's outputs only.
 
 Usage (in the container that has /root/reference):
-    make -C oracle && python tests/golden/make_golden.py
+    make -C oracle && python tests/golden/make_golden.py            # everything
+    python tests/golden/make_golden.py --varlen                       # only "varlen_full"
 """
+import ctypes
 import json
 import os
 import sys
@@ -30,7 +32,41 @@ def sm_bytes(nbytes, state):
     return w.view(np.uint8)[:nbytes].copy()
 
 
+def varlen_full(g):
+    """BASELINE configs[2] (Zipf packets) and configs[4] (backup chunks) at their
+    exact bench shapes (bench_shapes.py): the reference's crc32c_append over
+    every buffer of each ~1 GiB batch, as xor/sum digests plus the first 64
+    checksums, for seeds 0 and 0xFDBEEFDB."""
+    import bench_shapes as S
+    ref = O.reference()
+    out = {}
+    for name in ("zipf", "chunks"):
+        lengths, offsets, extent = S.shape(name)
+        data = O.splitmix64(extent // 8, S.STATE).view(np.uint8)
+        ent = {"state": S.STATE, "count": int(lengths.size), "total_bytes": int(lengths.sum()),
+               "extent": extent, "align": S.SHAPES[name][1], "lengths_sha256": S.lengths_digest(lengths),
+               "digests": []}
+        for seed in (0, 0xFDBEEFDB):
+            c = np.zeros(lengths.size, np.uint32)
+            f = ref.lib.ref_batch_varlen
+            f.restype = None
+            f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+            f(data.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, lengths.size, seed, c.ctypes.data)
+            ent["digests"].append(dict(S.digest(c), seed=seed, first64=[int(x) for x in c[:64]]))
+        out[name] = ent
+        del data
+    g["varlen_full"] = out
+
+
 def main():
+    if "--varlen" in sys.argv:
+        with open(OUT) as fh:
+            g = json.load(fh)
+        varlen_full(g)
+        with open(OUT, "w") as fh:
+            json.dump(g, fh, separators=(",", ":"))
+        print("updated varlen_full in", OUT)
+        return
     ref = O.reference()
     crc = ref.append
     g = {"generator": "splitmix64: word k = mix(state + (k+1)*0x9E3779B97F4A7C15), little-endian u64",
@@ -128,6 +164,8 @@ def main():
         ch = crc(ch, th_data[i:i + 8192])
     g["chained"] = {"state": th_state, "nbytes": 1 << 20, "read": 8192, "seed": 0, "crc": ch,
                     "oneshot": crc(0, th_data[:1 << 20])}
+
+    varlen_full(g)
 
     with open(OUT, "w") as fh:
         json.dump(g, fh, separators=(",", ":"))

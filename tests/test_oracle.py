@@ -116,3 +116,19 @@ def test_oracle_matches_compiled_reference_random():
         n = min(n, buf.size - off)
         s = int(rng.integers(0, 2**32))
         assert O.crc32c(s, buf[off:off + n]) == ref.append(s, buf[off:off + n])
+
+
+@pytest.mark.parametrize("name", ["zipf", "chunks"])
+def test_oracle_varlen_configs_exact_batches(oracle_mod, golden, name):
+    """The oracle reproduces the reference's digests of the exact configs[2] /
+    configs[4] batches (and the shape generator still yields the pinned list)."""
+    import bench_shapes as S
+    O = oracle_mod
+    ent = golden["varlen_full"][name]
+    lengths, offsets, extent = S.shape(name)
+    assert S.lengths_digest(lengths) == ent["lengths_sha256"]
+    data = O.splitmix64(extent // 8, ent["state"]).view(np.uint8)
+    d = ent["digests"][1]
+    got = O.batch_varlen(data, offsets, lengths, seed=d["seed"])
+    assert S.digest(got) == {"xor": d["xor"], "sum": d["sum"]}
+    assert [int(x) for x in got[:64]] == d["first64"]
