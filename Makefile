@@ -20,7 +20,16 @@ CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJ)/%.cpp.o,$(CPP_SRCS))
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
 CXXFLAGS := -O3 -fPIC -std=c++17 -Wall -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
-all: $(LIB) oracle
+# test/bench utilities (synthetic data in HBM, LDS poisoning): their own
+# library, never linked into the product
+TU_LIB := foundationdb_amd/lib/libfdb_crc32c_testutil.so
+TU_SRCS := $(wildcard foundationdb_amd/testutil/*.hip)
+
+all: $(LIB) $(TU_LIB) oracle
+
+$(TU_LIB): $(TU_SRCS) foundationdb_amd/testutil/fdb_crc32c_testutil.h
+	@mkdir -p $(dir $(TU_LIB))
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TU_SRCS)
 
 # the page kernels' grab requests must stay single-lane atomics whose return is
 # awaited only where it is used (the atomic optimizer's wave reduction reads it
@@ -51,7 +60,7 @@ debug: $(HIP_SRCS) $(CPP_SRCS) $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(DBG_LIB) build/dbg/*.o
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(TU_LIB)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean debug

@@ -8,6 +8,7 @@ batched device entry points over torch-allocated HBM buffers.
 from .crc32c import (  # noqa: F401
     CRC32CError,
     Pipeline,
+    PipelineJob,
     LIB_PATH,
     batch_fixed,
     batch_varlen,
@@ -17,6 +18,9 @@ from .crc32c import (  # noqa: F401
     crc32c_shift,
     fill_splitmix64,
     poison_lds,
+    release_stream,
+    stream_bytes,
+    testutil_lib,
     gpu_init,
     lib,
     varlen_workspace_bytes,

@@ -17,6 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FDBCRC_LIB") or os.path.join(_HERE, "lib", "libfdb_crc32c.so")
+TESTUTIL_LIB_PATH = os.path.join(_HERE, "lib", "libfdb_crc32c_testutil.so")
 
 
 class CRC32CError(RuntimeError):
@@ -64,16 +65,52 @@ def lib():
         L.crc32c_pipeline_varlen.argtypes = [vp, vp, vp, vp, u64, u32, vp, vp]
         L.crc32c_pipeline_fixed.restype = ctypes.c_int
         L.crc32c_pipeline_fixed.argtypes = [vp, vp, u64, u64, u64, u32, vp, vp]
+        L.crc32c_pipeline_submit_varlen.restype = ctypes.c_int
+        L.crc32c_pipeline_submit_varlen.argtypes = [vp, vp, vp, vp, u64, u32, vp, vp, ctypes.POINTER(u64)]
+        L.crc32c_pipeline_submit_fixed.restype = ctypes.c_int
+        L.crc32c_pipeline_submit_fixed.argtypes = [vp, vp, u64, u64, u64, u32, vp, vp, ctypes.POINTER(u64)]
+        L.crc32c_pipeline_poll.restype = ctypes.c_int
+        L.crc32c_pipeline_poll.argtypes = [vp, u64]
+        L.crc32c_pipeline_wait.restype = ctypes.c_int
+        L.crc32c_pipeline_wait.argtypes = [vp, u64]
+        L.fdb_sqlite_verify_pages_host.restype = ctypes.c_int
+        L.fdb_sqlite_verify_pages_host.argtypes = [vp, vp, u64, u64, u32, vp, vp]
+        L.fdb_sqlite_verify_pages_host_submit.restype = ctypes.c_int
+        L.fdb_sqlite_verify_pages_host_submit.argtypes = [vp, vp, u64, u64, u32, vp, vp, ctypes.POINTER(u64)]
+        L.fdb_diskqueue_check_pages_host.restype = ctypes.c_int
+        L.fdb_diskqueue_check_pages_host.argtypes = [vp, vp, u64, vp, vp]
+        L.fdb_diskqueue_check_pages_host_submit.restype = ctypes.c_int
+        L.fdb_diskqueue_check_pages_host_submit.argtypes = [vp, vp, u64, vp, vp, ctypes.POINTER(u64)]
+        L.crc32c_gpu_release_stream.restype = ctypes.c_int
+        L.crc32c_gpu_release_stream.argtypes = [vp]
+        L.crc32c_gpu_stream_bytes.restype = u64
+        L.crc32c_gpu_stream_bytes.argtypes = [vp]
         L.crc32c_host_register.restype = ctypes.c_int
         L.crc32c_host_register.argtypes = [vp, u64]
         L.crc32c_host_unregister.restype = ctypes.c_int
         L.crc32c_host_unregister.argtypes = [vp]
-        L.crc32c_testutil_fill_splitmix64.restype = ctypes.c_int
-        L.crc32c_testutil_fill_splitmix64.argtypes = [vp, u64, u64, vp]
-        L.crc32c_testutil_poison_lds.restype = ctypes.c_int
-        L.crc32c_testutil_poison_lds.argtypes = [u32, ctypes.c_int, vp]
         _lib = L
     return _lib
+
+
+_tlib = None
+
+
+def testutil_lib():
+    """libfdb_crc32c_testutil.so: synthetic data and LDS poisoning for tests
+    and bench.py (a separate library; nothing in the product links it)."""
+    global _tlib
+    if _tlib is None:
+        if not os.path.exists(TESTUTIL_LIB_PATH):
+            raise CRC32CError(f"{TESTUTIL_LIB_PATH} missing: run `make`")
+        L = ctypes.CDLL(TESTUTIL_LIB_PATH)
+        L.crc32c_testutil_fill_splitmix64.restype = ctypes.c_int
+        L.crc32c_testutil_fill_splitmix64.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                      ctypes.c_void_p]
+        L.crc32c_testutil_poison_lds.restype = ctypes.c_int
+        L.crc32c_testutil_poison_lds.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+        _tlib = L
+    return _tlib
 
 
 # ---------------------------------------------------------------- host scalar
@@ -114,9 +151,26 @@ def _stream_handle(stream):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
-def _require_device(t, name):
+def _require_device(t, name, device=None, dtypes=None, min_numel=None):
+    """Every tensor handed to the C ABI: on the GPU (on `device` if given),
+    contiguous (the kernels read flat memory), of an accepted dtype, and at
+    least `min_numel` elements (the kernels write out[0..count) and read
+    seeds[0..count) without bounds)."""
     if not isinstance(t, torch.Tensor) or not t.is_cuda:
         raise CRC32CError(f"{name} must be a device (HBM) tensor")
+    if device is not None and t.device != device:
+        raise CRC32CError(f"{name} is on {t.device}, expected {device}")
+    if not t.is_contiguous():
+        raise CRC32CError(f"{name} must be contiguous")
+    if dtypes is not None and t.dtype not in dtypes:
+        raise CRC32CError(f"{name} has dtype {t.dtype}, expected one of {[str(d) for d in dtypes]}")
+    if min_numel is not None and t.numel() < min_numel:
+        raise CRC32CError(f"{name} has {t.numel()} elements, needs at least {min_numel}")
+
+
+U32 = (torch.uint32, torch.int32)
+I64 = (torch.int64, torch.uint64)
+U64 = (torch.uint64, torch.int64)
 
 
 def gpu_init():
@@ -130,15 +184,17 @@ def batch_fixed(buf, stride, length, count, seed=0, seeds=None, out=None, stream
     crc32c_append(seed or seeds[i], ...)).  Asynchronous on `stream`.
     """
     _require_device(buf, "buf")
-    count = int(count)
+    count, stride, length, byte_offset = int(count), int(stride), int(length), int(byte_offset)
+    if min(count, stride, length, byte_offset) < 0:
+        raise CRC32CError("batch_fixed: negative count/stride/length/byte_offset")
     if count and byte_offset + (count - 1) * stride + length > buf.numel() * buf.element_size():
         raise CRC32CError("batch_fixed: buffers extend past the end of `buf`")
     if out is None:
         out = torch.empty(count, dtype=torch.uint32, device=buf.device)
-    _require_device(out, "out")
+    _require_device(out, "out", buf.device, U32, count)
     sp = None
     if seeds is not None:
-        _require_device(seeds, "seeds")
+        _require_device(seeds, "seeds", buf.device, U32, count)
         sp = ctypes.c_void_p(seeds.data_ptr())
     with torch.cuda.device(buf.device):
         rc = lib().crc32c_gpu_batch_fixed(ctypes.c_void_p(buf.data_ptr() + byte_offset), stride, length, count,
@@ -159,18 +215,17 @@ def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=Non
     bytes (caller-owned planning workspace; otherwise the library's per-stream one).
     """
     _require_device(buf, "buf")
-    _require_device(offsets, "offsets")
-    _require_device(lengths, "lengths")
-    if offsets.dtype not in (torch.int64, torch.uint64) or lengths.dtype not in (torch.int64, torch.uint64):
-        raise CRC32CError("offsets/lengths must be 64-bit integer tensors")
+    _require_device(offsets, "offsets", buf.device, I64)
+    _require_device(lengths, "lengths", buf.device, I64)
     count = offsets.numel()
     if lengths.numel() != count:
         raise CRC32CError("offsets and lengths differ in size")
     if out is None:
         out = torch.empty(count, dtype=torch.uint32, device=buf.device)
+    _require_device(out, "out", buf.device, U32, count)
     sp = None
     if seeds is not None:
-        _require_device(seeds, "seeds")
+        _require_device(seeds, "seeds", buf.device, U32, count)
         sp = ctypes.c_void_p(seeds.data_ptr())
     with torch.cuda.device(buf.device):
         if workspace is None:
@@ -178,7 +233,7 @@ def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=Non
                                                ctypes.c_void_p(lengths.data_ptr()), count, seed & 0xFFFFFFFF, sp,
                                                ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
         else:
-            _require_device(workspace, "workspace")
+            _require_device(workspace, "workspace", buf.device)
             rc = lib().crc32c_gpu_batch_varlen_ws(
                 ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
                 ctypes.c_void_p(lengths.data_ptr()), count, seed & 0xFFFFFFFF, sp, ctypes.c_void_p(out.data_ptr()),
@@ -188,20 +243,32 @@ def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=Non
     return out
 
 
+def release_stream(stream):
+    """Free the library's per-stream state (workspace, page counters) before
+    the stream is destroyed (crc32c_gpu_release_stream)."""
+    _check(lib().crc32c_gpu_release_stream(_stream_handle(stream)), "crc32c_gpu_release_stream")
+
+
+def stream_bytes(stream=None):
+    """Device bytes the library holds for `stream` (crc32c_gpu_stream_bytes)."""
+    return int(lib().crc32c_gpu_stream_bytes(_stream_handle(stream)))
+
+
 def poison_lds(pattern=0xA5A5A5A5, blocks=2048, stream=None):
-    """Test utility: leave garbage in every CU's LDS (see fdb_crc32c_testutil.h)."""
-    _check(lib().crc32c_testutil_poison_lds(pattern & 0xFFFFFFFF, blocks, _stream_handle(stream)), "poison_lds")
+    """Test utility: leave garbage in every CU's LDS (testutil/fdb_crc32c_testutil.h)."""
+    _check(testutil_lib().crc32c_testutil_poison_lds(pattern & 0xFFFFFFFF, blocks, _stream_handle(stream)),
+           "poison_lds")
 
 
 def fill_splitmix64(buf, state, stream=None):
-    """Fill a device tensor with the BASELINE.md splitmix64 word stream."""
+    """Test/bench utility: fill a device tensor with the BASELINE.md splitmix64 word stream."""
     _require_device(buf, "buf")
     nbytes = buf.numel() * buf.element_size()
     if nbytes % 8:
         raise CRC32CError("fill_splitmix64 needs a multiple of 8 bytes")
     with torch.cuda.device(buf.device):
-        rc = lib().crc32c_testutil_fill_splitmix64(ctypes.c_void_p(buf.data_ptr()), nbytes // 8, state,
-                                                   _stream_handle(stream))
+        rc = testutil_lib().crc32c_testutil_fill_splitmix64(ctypes.c_void_p(buf.data_ptr()), nbytes // 8, state,
+                                                            _stream_handle(stream))
     _check(rc, "crc32c_testutil_fill_splitmix64")
     return buf
 
@@ -243,29 +310,151 @@ class Pipeline:
             return a.data_ptr()
         return a.ctypes.data
 
-    def varlen(self, buf, offsets, lengths, seed=0, seeds=None, out=None):
+    # The host arrays of a submitted job must stay alive until it completes:
+    # the pipeline keeps references to them per ticket.
+    def _varlen_args(self, buf, offsets, lengths, seeds, out):
         import numpy as np
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
         n = offsets.size
-        if out is None:
-            out = np.empty(n, dtype=np.uint32)
-        sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+        if lengths.size != n:
+            raise CRC32CError("offsets and lengths differ in size")
+        if n and int((offsets + lengths).max()) > _nbytes(buf):
+            raise CRC32CError("pipeline varlen: buffers extend past the end of `buf`")
+        out = _host_out(out, n, np.uint32)
+        sd = None if seeds is None else _host_seeds(seeds, n)
+        return offsets, lengths, n, sd, out
+
+    def _fixed_args(self, buf, stride, length, count, seeds, out):
+        import numpy as np
+        if count and (count - 1) * stride + length > _nbytes(buf):
+            raise CRC32CError("pipeline fixed: buffers extend past the end of `buf`")
+        return _host_out(out, count, np.uint32), None if seeds is None else _host_seeds(seeds, count)
+
+    def submit_varlen(self, buf, offsets, lengths, seed=0, seeds=None, out=None):
+        """Queue a host-resident varlen batch; returns a PipelineJob (poll()/wait())."""
+        offsets, lengths, n, sd, out = self._varlen_args(buf, offsets, lengths, seeds, out)
+        t = ctypes.c_uint64()
+        _check(lib().crc32c_pipeline_submit_varlen(self._p, ctypes.c_void_p(self._addr(buf)), offsets.ctypes.data,
+                                                   lengths.ctypes.data, n, seed & 0xFFFFFFFF, _np_ptr(sd),
+                                                   ctypes.c_void_p(self._addr(out)), ctypes.byref(t)),
+               "crc32c_pipeline_submit_varlen")
+        return PipelineJob(self, t.value, out, keep=(buf, offsets, lengths, sd))
+
+    def submit_fixed(self, buf, stride, length, count, seed=0, seeds=None, out=None):
+        out, sd = self._fixed_args(buf, stride, length, count, seeds, out)
+        t = ctypes.c_uint64()
+        _check(lib().crc32c_pipeline_submit_fixed(self._p, ctypes.c_void_p(self._addr(buf)), stride, length, count,
+                                                  seed & 0xFFFFFFFF, _np_ptr(sd), ctypes.c_void_p(self._addr(out)),
+                                                  ctypes.byref(t)), "crc32c_pipeline_submit_fixed")
+        return PipelineJob(self, t.value, out, keep=(buf, sd))
+
+    def varlen(self, buf, offsets, lengths, seed=0, seeds=None, out=None):
+        offsets, lengths, n, sd, out = self._varlen_args(buf, offsets, lengths, seeds, out)
         _check(lib().crc32c_pipeline_varlen(self._p, ctypes.c_void_p(self._addr(buf)), offsets.ctypes.data,
-                                            lengths.ctypes.data, n, seed & 0xFFFFFFFF,
-                                            None if sd is None else sd.ctypes.data, ctypes.c_void_p(self._addr(out))),
-               "crc32c_pipeline_varlen")
+                                            lengths.ctypes.data, n, seed & 0xFFFFFFFF, _np_ptr(sd),
+                                            ctypes.c_void_p(self._addr(out))), "crc32c_pipeline_varlen")
         return out
 
     def fixed(self, buf, stride, length, count, seed=0, seeds=None, out=None):
-        import numpy as np
-        if out is None:
-            out = np.empty(count, dtype=np.uint32)
-        sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+        out, sd = self._fixed_args(buf, stride, length, count, seeds, out)
         _check(lib().crc32c_pipeline_fixed(self._p, ctypes.c_void_p(self._addr(buf)), stride, length, count,
-                                           seed & 0xFFFFFFFF, None if sd is None else sd.ctypes.data,
-                                           ctypes.c_void_p(self._addr(out))), "crc32c_pipeline_fixed")
+                                           seed & 0xFFFFFFFF, _np_ptr(sd), ctypes.c_void_p(self._addr(out))),
+               "crc32c_pipeline_fixed")
         return out
+
+    # ---- host-resident page verifiers (include/fdb_pagecheck.h)
+    def sqlite_verify_pages(self, pages, page_size, count=None, first_pgno=1, submit=False):
+        """Status byte per page (pagecheck.STATUS_*) and the bad-page count for
+        host-resident SQLite pages; submit=True returns a PipelineJob whose
+        result is (status, bad)."""
+        import numpy as np
+        count = _nbytes(pages) // page_size if count is None else int(count)
+        if count * page_size > _nbytes(pages):
+            raise CRC32CError("sqlite_verify_pages: pages extend past the buffer")
+        status = np.empty(count, np.uint8)
+        bad = np.zeros(1, np.uint64)
+        if submit:
+            t = ctypes.c_uint64()
+            _check(lib().fdb_sqlite_verify_pages_host_submit(self._p, ctypes.c_void_p(self._addr(pages)), page_size,
+                                                             count, first_pgno, status.ctypes.data, bad.ctypes.data,
+                                                             ctypes.byref(t)), "fdb_sqlite_verify_pages_host_submit")
+            return PipelineJob(self, t.value, (status, bad), keep=(pages,))
+        _check(lib().fdb_sqlite_verify_pages_host(self._p, ctypes.c_void_p(self._addr(pages)), page_size, count,
+                                                  first_pgno, status.ctypes.data, bad.ctypes.data),
+               "fdb_sqlite_verify_pages_host")
+        return status, bad
+
+    def diskqueue_check_pages(self, pages, count=None, submit=False):
+        import numpy as np
+        count = _nbytes(pages) // 4096 if count is None else int(count)
+        if count * 4096 > _nbytes(pages):
+            raise CRC32CError("diskqueue_check_pages: pages extend past the buffer")
+        ok = np.empty(count, np.uint8)
+        bad = np.zeros(1, np.uint64)
+        if submit:
+            t = ctypes.c_uint64()
+            _check(lib().fdb_diskqueue_check_pages_host_submit(self._p, ctypes.c_void_p(self._addr(pages)), count,
+                                                               ok.ctypes.data, bad.ctypes.data, ctypes.byref(t)),
+                   "fdb_diskqueue_check_pages_host_submit")
+            return PipelineJob(self, t.value, (ok, bad), keep=(pages,))
+        _check(lib().fdb_diskqueue_check_pages_host(self._p, ctypes.c_void_p(self._addr(pages)), count,
+                                                    ok.ctypes.data, bad.ctypes.data), "fdb_diskqueue_check_pages_host")
+        return ok, bad
+
+
+class PipelineJob:
+    """A submitted host-resident batch (crc32c_pipeline_poll / _wait)."""
+
+    def __init__(self, pipe, ticket, result, keep=()):
+        self.pipe, self.ticket, self.result, self._keep = pipe, ticket, result, keep
+        self.done = False
+
+    def poll(self):
+        """Non-blocking: True once the job's results are in place."""
+        if not self.done:
+            rc = lib().crc32c_pipeline_poll(self.pipe._p, self.ticket)
+            if rc < 0:
+                _check(rc, "crc32c_pipeline_poll")
+            self.done = rc == 1
+        return self.done
+
+    def wait(self):
+        if not self.done:
+            _check(lib().crc32c_pipeline_wait(self.pipe._p, self.ticket), "crc32c_pipeline_wait")
+            self.done = True
+        return self.result
+
+
+def _nbytes(a):
+    if isinstance(a, torch.Tensor):
+        return a.numel() * a.element_size()
+    return a.nbytes
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def _host_out(out, n, dtype):
+    import numpy as np
+    if out is None:
+        return np.empty(n, dtype=dtype)
+    if isinstance(out, torch.Tensor):
+        if out.is_cuda or not out.is_contiguous() or out.numel() < n or out.element_size() != 4:
+            raise CRC32CError("out must be a contiguous host array of >= count 32-bit elements")
+        return out
+    if not out.flags.c_contiguous or out.size < n or out.dtype.itemsize != 4:
+        raise CRC32CError("out must be a contiguous host array of >= count 32-bit elements")
+    return out
+
+
+def _host_seeds(seeds, n):
+    import numpy as np
+    sd = np.ascontiguousarray(seeds, dtype=np.uint32)
+    if sd.size < n:
+        raise CRC32CError("seeds has fewer than count elements")
+    return sd
 
 
 class _NullCtx:

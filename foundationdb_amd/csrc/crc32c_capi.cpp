@@ -21,12 +21,23 @@ namespace {
 
 constexpr int kMaxDevices = 64;
 
+// Library-owned state of one (device, stream).  `mu` is held from the
+// workspace lookup through the enqueue of the kernels that use it, so a
+// thread that grows (frees and reallocates) the workspace can never free a
+// buffer another thread has been handed but not yet launched on.
+struct StreamState {
+	std::mutex mu;
+	void* ws = nullptr;  // planning workspace (varlen, XXH3 varlen, verifiers)
+	uint64_t ws_bytes = 0;
+	uint32_t* ctr = nullptr;  // page-kernel grab counters
+	uint64_t ctr_bytes = 0;
+};
+
 struct DeviceState {
 	DevTables* tables = nullptr;  // device copy
 	int num_cus = 0;
 	bool ready = false;
-	std::map<hipStream_t, std::pair<void*, uint64_t>> ws;  // varlen planning workspace per stream
-	std::map<hipStream_t, uint32_t*> ctr;                  // page-kernel grab counters per stream
+	std::map<hipStream_t, std::unique_ptr<StreamState>> streams;  // guarded by g_mu
 };
 
 std::mutex g_mu;
@@ -76,27 +87,40 @@ int device_state(DeviceState** st) {
 	return 0;
 }
 
-// Planning workspace owned by the library for the convenience entry point,
-// one per (device, stream) so concurrent streams never share it.  Growing it
-// synchronises the stream once (the old buffer may still be in use).
-int stream_workspace(DeviceState* st, hipStream_t s, uint64_t need, void** ws, uint64_t* have) {
+StreamState* stream_state(DeviceState* st, hipStream_t s) {
 	std::lock_guard<std::mutex> lock(g_mu);
-	auto& slot = st->ws[s];
-	if (slot.second < need) {
-		if (slot.first) {
+	auto& p = st->streams[s];
+	if (!p) p.reset(new StreamState);
+	return p.get();
+}
+
+// Planning workspace owned by the library for the convenience entry points,
+// one per (device, stream) so concurrent streams never share it.  On success
+// `hold` owns the stream's lock: keep it until the kernels using *ws are
+// enqueued.  Growing synchronises the stream once (the old buffer may still be
+// in use by launches already enqueued).
+int stream_workspace(DeviceState* st, hipStream_t s, uint64_t need, void** ws, uint64_t* have,
+                     std::unique_lock<std::mutex>* hold) {
+	StreamState* ss = stream_state(st, s);
+	std::unique_lock<std::mutex> lock(ss->mu);
+	if (ss->ws_bytes < need) {
+		if (ss->ws) {
 			hipError_t e = hipStreamSynchronize(s);
 			if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "hipStreamSynchronize(workspace)", e);
-			(void)hipFree(slot.first);
-			slot = {nullptr, 0};
+			(void)hipFree(ss->ws);
+			ss->ws = nullptr;
+			ss->ws_bytes = 0;
 		}
 		uint64_t sz = need < (1u << 20) ? (1u << 20) : need * 2;
 		void* p = nullptr;
 		hipError_t e = hipMalloc(&p, sz);
 		if (e != hipSuccess) return fail(FDB_CRC32C_ENOMEM, "hipMalloc(workspace)", e);
-		slot = {p, sz};
+		ss->ws = p;
+		ss->ws_bytes = sz;
 	}
-	*ws = slot.first;
-	*have = slot.second;
+	*ws = ss->ws;
+	*have = ss->ws_bytes;
+	*hold = std::move(lock);
 	return 0;
 }
 
@@ -110,25 +134,58 @@ int check_launch(const char* what) {
 
 // Grab counters of the page kernels for `stream` on the current device:
 // zeroed once here, left at zero by every page launch.
+// The zeroing is enqueued on `stream` itself, ahead of the first page launch.
+// (Allocation happens under g_mu, not the stream lock: the verifiers launch
+// page kernels while holding their stream's workspace lock.)
 int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr) {
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
+	StreamState* ss = stream_state(st, stream);
 	std::lock_guard<std::mutex> lock(g_mu);
-	uint32_t*& p = st->ctr[stream];
-	if (!p) {
+	if (!ss->ctr) {
 		const size_t bytes = (size_t)(num_cus > st->num_cus ? num_cus : st->num_cus) * kPageCtrWords * 4;
 		uint32_t* q = nullptr;
 		hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), bytes);
 		if (e != hipSuccess) return fail(FDB_CRC32C_ENOMEM, "hipMalloc(page counters)", e);
-		e = hipMemset(q, 0, bytes);
+		e = hipMemsetAsync(q, 0, bytes, stream);
 		if (e != hipSuccess) {
 			(void)hipFree(q);
-			return fail(FDB_CRC32C_EHIP, "hipMemset(page counters)", e);
+			return fail(FDB_CRC32C_EHIP, "hipMemsetAsync(page counters)", e);
 		}
-		p = q;
+		ss->ctr = q;
+		ss->ctr_bytes = bytes;
 	}
-	*ctr = p;
+	*ctr = ss->ctr;
 	return 0;
+}
+
+// Frees what the library holds for `stream` on the current device.
+int release_stream(hipStream_t stream) {
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	std::unique_ptr<StreamState> ss;
+	{
+		std::lock_guard<std::mutex> lock(g_mu);
+		auto it = st->streams.find(stream);
+		if (it == st->streams.end()) return 0;
+		ss = std::move(it->second);
+		st->streams.erase(it);
+	}
+	std::lock_guard<std::mutex> lock(ss->mu);  // wait for an enqueue in progress
+	hipError_t e = hipStreamSynchronize(stream);
+	if (ss->ws) (void)hipFree(ss->ws);
+	if (ss->ctr) (void)hipFree(ss->ctr);
+	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "hipStreamSynchronize(release)", e);
+	return 0;
+}
+
+uint64_t stream_bytes(hipStream_t stream) {
+	DeviceState* st = nullptr;
+	if (device_state(&st)) return 0;
+	std::lock_guard<std::mutex> lock(g_mu);
+	auto it = st->streams.find(stream);
+	if (it == st->streams.end()) return 0;
+	return it->second->ws_bytes + it->second->ctr_bytes;
 }
 
 // used by the host pipeline (crc32c_pipeline.cpp)
@@ -225,7 +282,9 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
 #endif
 		void* ws = nullptr;
 		uint64_t have = 0;
-		if (int wrc = stream_workspace(st, s, varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have))
+		std::unique_lock<std::mutex> hold;
+		if (int wrc = stream_workspace(st, s, varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have,
+		                               &hold))
 			return wrc;
 		rc = launch_fixed_general(base, stride, length, count, seed, d_seeds, d_out, st->tables, st->num_cus, ws, s);
 #ifdef FDBCRC_DEBUG
@@ -275,8 +334,9 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
 	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
-	                              varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have))
+	                              varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have, &hold))
 		return rc;
 	return crc32c_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
 }
@@ -341,8 +401,10 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
 	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
-	                              fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus)), &ws, &have))
+	                              fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus)), &ws, &have,
+	                              &hold))
 		return rc;
 	return xxh3_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
 }
@@ -387,7 +449,9 @@ int fdb_sqlite_verify_pages(const void* d_pages, uint64_t page_size, uint64_t co
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
-	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have))
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have,
+	                              &hold))
 		return rc;
 	return fdb_sqlite_verify_pages_ws(d_pages, page_size, count, first_pgno, d_status, d_bad, ws, have, stream);
 }
@@ -416,10 +480,16 @@ int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok
 	if (int rc = device_state(&st)) return rc;
 	void* ws = nullptr;
 	uint64_t have = 0;
-	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have))
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have,
+	                              &hold))
 		return rc;
 	return fdb_diskqueue_check_pages_ws(d_pages, count, d_ok, d_bad, ws, have, stream);
 }
+
+int crc32c_gpu_release_stream(void* stream) { return release_stream(reinterpret_cast<hipStream_t>(stream)); }
+
+uint64_t crc32c_gpu_stream_bytes(void* stream) { return stream_bytes(reinterpret_cast<hipStream_t>(stream)); }
 
 const char* crc32c_gpu_last_error(void) { return t_err.c_str(); }
 

@@ -280,7 +280,10 @@ struct fdb_write_checker {
 			(void)hipHostFree(s.h);
 			(void)hipEventDestroy(s.ev);
 		}
-		if (stream) (void)hipStreamDestroy(stream);
+		if (stream) {
+			(void)crc32c_gpu_release_stream(stream);
+			(void)hipStreamDestroy(stream);
+		}
 		if (pipe) crc32c_pipeline_destroy(pipe);
 	}
 };

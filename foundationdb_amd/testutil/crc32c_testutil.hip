@@ -1,11 +1,12 @@
-// Synthetic-input generator for tests and bench.py (not on the checksum path).
+// Test and bench utilities, built into their own libfdb_crc32c_testutil.so (never
+// linked into the product library).  Synthetic-input generator:
 // Fills device memory with the splitmix64 stream of BASELINE.md: word k is
 // mix(state + (k+1)*0x9E3779B97F4A7C15), little-endian -- the same stream as
 // oracle_splitmix64_fill, so 4 GiB page batches need no host-to-device copy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/fdb_crc32c_testutil.h"
+#include "fdb_crc32c_testutil.h"
 
 namespace fdbcrc {
 

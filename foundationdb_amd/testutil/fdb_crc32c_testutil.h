@@ -1,5 +1,6 @@
-/* fdb_crc32c_testutil.h -- synthetic data generation for tests and bench.py.
- * Not part of the checksum path. */
+/* fdb_crc32c_testutil.h -- synthetic data generation and LDS poisoning for
+ * tests and bench.py, exported by libfdb_crc32c_testutil.so.  Not part of the
+ * product library or its boundary (include/). */
 #ifndef FDB_CRC32C_TESTUTIL_H
 #define FDB_CRC32C_TESTUTIL_H
 #include <stdint.h>

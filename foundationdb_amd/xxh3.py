@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from .crc32c import CRC32CError, _check, _require_device, _stream_handle, lib
+from .crc32c import I64, U64, CRC32CError, _check, _require_device, _stream_handle, lib
 
 _bound = False
 
@@ -39,14 +39,16 @@ def _vp(t):
 def batch_fixed(buf, stride, length, count, seed=0, seeds=None, out=None, stream=None, byte_offset=0):
     """XXH3-64 of bytes [byte_offset + i*stride, +length) of device tensor `buf`, i < count."""
     _require_device(buf, "buf")
-    count = int(count)
+    count, stride, length, byte_offset = int(count), int(stride), int(length), int(byte_offset)
+    if min(count, stride, length, byte_offset) < 0:
+        raise CRC32CError("xxh3 batch_fixed: negative count/stride/length/byte_offset")
     if count and byte_offset + (count - 1) * stride + length > buf.numel() * buf.element_size():
         raise CRC32CError("xxh3 batch_fixed: buffers extend past the end of `buf`")
     if out is None:
         out = torch.empty(count, dtype=torch.uint64, device=buf.device)
-    _require_device(out, "out")
+    _require_device(out, "out", buf.device, U64, count)
     if seeds is not None:
-        _require_device(seeds, "seeds")
+        _require_device(seeds, "seeds", buf.device, U64, count)
     with torch.cuda.device(buf.device):
         rc = _lib().xxh3_gpu_batch_fixed(ctypes.c_void_p(buf.data_ptr() + byte_offset), stride, length, count,
                                          seed & 0xFFFFFFFFFFFFFFFF, _vp(seeds), _vp(out), _stream_handle(stream))
@@ -61,20 +63,22 @@ def varlen_workspace_bytes(count):
 def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=None, workspace=None):
     """XXH3-64 of bytes [offsets[i], +lengths[i]) of device tensor `buf` (int64 device tensors)."""
     _require_device(buf, "buf")
-    _require_device(offsets, "offsets")
-    _require_device(lengths, "lengths")
+    _require_device(offsets, "offsets", buf.device, I64)
+    _require_device(lengths, "lengths", buf.device, I64)
     n = offsets.numel()
     if lengths.numel() != n:
         raise CRC32CError("xxh3 batch_varlen: offsets and lengths differ in size")
     if out is None:
         out = torch.empty(n, dtype=torch.uint64, device=buf.device)
+    _require_device(out, "out", buf.device, U64, n)
     if seeds is not None:
-        _require_device(seeds, "seeds")
+        _require_device(seeds, "seeds", buf.device, U64, n)
     with torch.cuda.device(buf.device):
         if workspace is None:
             rc = _lib().xxh3_gpu_batch_varlen(_vp(buf), _vp(offsets), _vp(lengths), n, seed & 0xFFFFFFFFFFFFFFFF,
                                               _vp(seeds), _vp(out), _stream_handle(stream))
         else:
+            _require_device(workspace, "workspace", buf.device)
             rc = _lib().xxh3_gpu_batch_varlen_ws(_vp(buf), _vp(offsets), _vp(lengths), n, seed & 0xFFFFFFFFFFFFFFFF,
                                                  _vp(seeds), _vp(out), _vp(workspace),
                                                  workspace.numel() * workspace.element_size(), _stream_handle(stream))

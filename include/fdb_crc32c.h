@@ -88,10 +88,13 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
  * Uses a library-owned workspace per (device, stream); it is allocated on
  * first use and grown (with one stream synchronisation) when a larger batch
  * arrives.
+ * Thread-safe: concurrent calls on the same stream serialise on the
+ * stream's workspace from lookup to enqueue.
  * Limit: the engine numbers 1 KiB windows with 32-bit slot indices, so a
- * batch may cover fewer than 2^32 windows in total (about 4 TiB of checksummed
- * bytes, overlapping buffers counted once each) -- far above what one GPU
- * holds unless buffers overlap heavily. */
+ * batch must cover fewer than 2^32 windows in total (about 4 TiB of
+ * checksummed bytes, overlapping buffers counted once each) -- far above what
+ * one GPU holds unless buffers overlap heavily.  The lengths live in device
+ * memory, so the host cannot refuse such a batch: its output is undefined. */
 int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                             uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
 
@@ -104,17 +107,44 @@ int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, co
                                uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
                                uint64_t workspace_bytes, void* stream);
 
+/* Per-stream library state.  The library keeps, per (device, stream) it has
+ * seen, the planning workspace of the convenience entry points and the page
+ * kernels' counters (crc32c_gpu_stream_bytes reports how many device bytes).
+ * Call crc32c_gpu_release_stream before hipStreamDestroy: it waits for the
+ * stream's work and frees that state, so a later stream that reuses the handle
+ * starts clean.  A stream never seen is a no-op.  Returns 0 or FDB_CRC32C_EHIP. */
+int crc32c_gpu_release_stream(void* stream);
+uint64_t crc32c_gpu_stream_bytes(void* stream);
+
 /* ---- Batched, host-resident (pinned H2D -> kernel -> D2H, overlapped) -- */
 
 /* The bytes start and end in host memory (pages read from disk, chunks of a
- * file, packets from a socket).  The pipeline cuts the batch into segments of
- * at most `segment_bytes` (covering byte range), round-robins them over
- * `nstreams` HIP streams on the current device, and overlaps each segment's
- * H2D copy with the previous segments' kernels and result copies.  Calls are
- * synchronous: h_out is complete on return.  Host memory registered with
+ * file, packets from a socket).  The pipeline cuts each submitted batch (a
+ * JOB) into segments of at most `segment_bytes` (covering byte range), runs
+ * them on `nstreams` HIP streams of the current device, and overlaps each
+ * segment's H2D copy with the previous segments' kernels and result copies.
+ * Fixed-stride batches of 4 KiB / 8 KiB pages (and the 4088 B / 4092 B page
+ * windows, at the same host alignment) run the page kernel; everything else
+ * the variable-length engine.  Host memory registered with
  * crc32c_host_register (or allocated pinned) is copied directly; pageable
  * memory is staged through the pipeline's pinned buffers.  A pipeline object
- * is not thread-safe; use one per thread. */
+ * is not thread-safe; use one per thread (or per Flow run loop).
+ *
+ * Asynchronous form (FoundationDB's file wrappers return Futures,
+ * fdbrpc/AsyncFileWriteChecker.h:59-67; the run loop must never block):
+ *   crc32c_pipeline_submit_*  queue a job, start what fits on free streams,
+ *                             return a ticket at once.  The host arrays (data,
+ *                             offsets, lengths, seeds, out) must stay valid and
+ *                             unchanged until the job completes.
+ *   crc32c_pipeline_poll      non-blocking (event queries only): retire
+ *                             finished segments, start queued ones, and return
+ *                             1 if job `ticket` is complete (h_out filled),
+ *                             0 if pending, < 0 its error.  Jobs advance only
+ *                             inside poll/wait/submit calls: poll from the run
+ *                             loop until it returns non-zero.
+ *   crc32c_pipeline_wait      block until job `ticket` completes: 0 or < 0.
+ * Synchronous form: crc32c_pipeline_varlen / _fixed = submit + wait.
+ * A buffer longer than segment_bytes is refused (EINVAL). */
 typedef struct fdb_crc32c_pipeline fdb_crc32c_pipeline;
 int crc32c_pipeline_create(fdb_crc32c_pipeline** out, uint64_t segment_bytes, int nstreams);
 void crc32c_pipeline_destroy(fdb_crc32c_pipeline* p);
@@ -123,6 +153,14 @@ int crc32c_pipeline_varlen(fdb_crc32c_pipeline* p, const void* h_base, const uin
                            uint32_t* h_out);
 int crc32c_pipeline_fixed(fdb_crc32c_pipeline* p, const void* h_base, uint64_t stride, uint64_t length,
                           uint64_t count, uint32_t seed, const uint32_t* h_seeds, uint32_t* h_out);
+int crc32c_pipeline_submit_varlen(fdb_crc32c_pipeline* p, const void* h_base, const uint64_t* h_offsets,
+                                  const uint64_t* h_lengths, uint64_t count, uint32_t seed, const uint32_t* h_seeds,
+                                  uint32_t* h_out, uint64_t* ticket);
+int crc32c_pipeline_submit_fixed(fdb_crc32c_pipeline* p, const void* h_base, uint64_t stride, uint64_t length,
+                                 uint64_t count, uint32_t seed, const uint32_t* h_seeds, uint32_t* h_out,
+                                 uint64_t* ticket);
+int crc32c_pipeline_poll(fdb_crc32c_pipeline* p, uint64_t ticket);
+int crc32c_pipeline_wait(fdb_crc32c_pipeline* p, uint64_t ticket);
 int crc32c_host_register(void* h_ptr, uint64_t bytes);
 int crc32c_host_unregister(void* h_ptr);
 

@@ -48,6 +48,24 @@ int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t
 int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad,
                                  void* d_workspace, uint64_t workspace_bytes, void* stream);
 
+/* Host-resident pages (a file scan reading pages from disk, as
+ * checkAllPageChecksums does, KeyValueStoreSQLite.cpp:1378-1470, or a DiskQueue
+ * recovery reading page runs, DiskQueue.cpp:1230-1290): the same verification
+ * through a crc32c_pipeline (pinned H2D -> verifier kernels -> D2H of one
+ * status byte per page, overlapped over the pipeline's streams).  Host
+ * pointers; *h_bad receives the number of failed pages.  The _submit forms
+ * return a ticket for crc32c_pipeline_poll / crc32c_pipeline_wait (host arrays
+ * must stay valid until then); the others block until done. */
+int fdb_sqlite_verify_pages_host(fdb_crc32c_pipeline* p, const void* h_pages, uint64_t page_size, uint64_t count,
+                                 uint32_t first_pgno, uint8_t* h_status, uint64_t* h_bad);
+int fdb_sqlite_verify_pages_host_submit(fdb_crc32c_pipeline* p, const void* h_pages, uint64_t page_size,
+                                        uint64_t count, uint32_t first_pgno, uint8_t* h_status, uint64_t* h_bad,
+                                        uint64_t* ticket);
+int fdb_diskqueue_check_pages_host(fdb_crc32c_pipeline* p, const void* h_pages, uint64_t count, uint8_t* h_ok,
+                                   uint64_t* h_bad);
+int fdb_diskqueue_check_pages_host_submit(fdb_crc32c_pipeline* p, const void* h_pages, uint64_t count, uint8_t* h_ok,
+                                          uint64_t* h_bad, uint64_t* ticket);
+
 #ifdef __cplusplus
 }
 #endif

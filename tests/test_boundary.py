@@ -15,9 +15,9 @@ from oracle import oracle as O
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
+def declared_functions(pattern=os.path.join(ROOT, "include", "*.h")):
     names = set()
-    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+    for h in glob.glob(pattern):
         text = open(h).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s+\*?([a-z_][a-z0-9_]*)\s*\(", text, re.M):
@@ -28,9 +28,20 @@ def declared_functions():
 def test_library_exports_every_declared_symbol():
     names = declared_functions()
     assert {"crc32c_append", "crc32c_gpu_batch_fixed", "crc32c_gpu_batch_varlen", "crc32c_combine"} <= names
+    assert {"crc32c_gpu_release_stream", "crc32c_pipeline_submit_varlen", "crc32c_pipeline_poll",
+            "fdb_sqlite_verify_pages_host", "fdb_diskqueue_check_pages_host_submit"} <= names
     lib = ctypes.CDLL(F.LIB_PATH)
     missing = [n for n in sorted(names) if not hasattr(lib, n)]
     assert not missing, missing
+
+
+def test_test_utilities_are_not_in_the_product_library():
+    """The splitmix64 generator and LDS poisoning live in their own
+    libfdb_crc32c_testutil.so; the product library exports none of them."""
+    names = declared_functions(os.path.join(ROOT, "foundationdb_amd", "testutil", "*.h"))
+    assert names == {"crc32c_testutil_fill_splitmix64", "crc32c_testutil_poison_lds"}
+    prod, tu = ctypes.CDLL(F.LIB_PATH), ctypes.CDLL(F.crc32c.TESTUTIL_LIB_PATH)
+    assert all(hasattr(tu, n) and not hasattr(prod, n) for n in names)
 
 
 def test_reference_signature():

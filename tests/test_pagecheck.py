@@ -131,3 +131,38 @@ def test_gpu_pagecheck_all_one_kind_and_empty(cuda):
     assert (status.cpu().numpy() == 2).all() and int(bad.cpu().numpy().view(np.uint64)[0]) == 0
     s0, b0 = PC.sqlite_verify_pages(d, 4096, count=0)
     assert s0.numel() == 0 and int(b0.cpu().numpy().view(np.uint64)[0]) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [True, False])
+def test_gpu_host_resident_verifiers(cuda, pinned):
+    """Pages that start in host memory (a file scan reading from disk,
+    KeyValueStoreSQLite.cpp:1378-1470; DiskQueue page runs, DiskQueue.cpp:1230-1290)
+    through the pipeline: small segments so a batch spans many segments and
+    every lane, pinned and pageable sources, blocking and submit/poll forms."""
+    import torch
+    import foundationdb_amd as F
+    pages, exp = make_sqlite_batch(3000, 4096, 5, 41)
+    dq, dq_exp = make_dq_batch(2500, 43)
+
+    def host(a):
+        if not pinned:
+            return a.reshape(-1).copy()
+        t = torch.empty(a.size, dtype=torch.uint8).pin_memory()
+        t.numpy()[:] = a.reshape(-1)
+        return t
+    hp, hd = host(pages), host(dq)
+    pipe = F.Pipeline(segment_bytes=1 << 20, nstreams=3)
+    status, bad = pipe.sqlite_verify_pages(hp, 4096, first_pgno=5)
+    assert np.array_equal(status, exp) and int(bad[0]) == int((exp == 0).sum())
+    ok, bad = pipe.diskqueue_check_pages(hd)
+    assert np.array_equal(ok, dq_exp) and int(bad[0]) == int((dq_exp == 0).sum())
+    j1 = pipe.sqlite_verify_pages(hp, 4096, first_pgno=5, submit=True)
+    j2 = pipe.diskqueue_check_pages(hd, submit=True)
+    while not (j1.poll() and j2.poll()):
+        pass
+    assert np.array_equal(j1.result[0], exp) and np.array_equal(j2.result[0], dq_exp)
+    assert int(j2.result[1][0]) == int((dq_exp == 0).sum())
+    s0, b0 = pipe.sqlite_verify_pages(hp, 4096, count=0)
+    assert s0.size == 0 and int(b0[0]) == 0
+    pipe.close()
