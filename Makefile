@@ -59,8 +59,22 @@ debug: $(HIP_SRCS) $(CPP_SRCS) $(HDRS)
 	for f in $(CPP_SRCS); do $(CXX) $(CXXFLAGS) -DFDBCRC_DEBUG -c $$f -o build/dbg/$$(basename $$f).o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(DBG_LIB) build/dbg/*.o
 
+# ASan + UBSan build of the host code (reference: cmake/ConfigureCompiler.cmake:5-12):
+# every .cpp instrumented, the device objects as in the product; load it with
+#   LD_PRELOAD=$$(g++ -print-file-name=libasan.so) FDBCRC_LIB=$(ASAN_LIB) python ...
+# (tools/run_asan.sh runs the non-GPU suite that way).
+ASAN_LIB := foundationdb_amd/lib/libfdb_crc32c_asan.so
+SANFLAGS := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
+ASAN_OBJS := $(patsubst $(CSRC)/%.cpp,build/asan/%.cpp.o,$(CPP_SRCS))
+build/asan/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build/asan
+	$(CXX) $(CXXFLAGS) $(SANFLAGS) -c $< -o $@
+$(ASAN_LIB): $(HIP_OBJS) $(ASAN_OBJS)
+	$(CXX) -shared $(SANFLAGS) -o $@ $^ -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+asan: $(ASAN_LIB)
+
 clean:
-	rm -rf build $(LIB) $(TU_LIB)
+	rm -rf build $(LIB) $(TU_LIB) $(ASAN_LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean debug
+.PHONY: all oracle clean debug asan

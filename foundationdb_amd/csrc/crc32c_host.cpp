@@ -7,10 +7,17 @@
 // contrib/crc32 for its single-buffer call sites; the batched GPU entry points
 // never route through it.
 //
-// Implementation: SSE4.2 crc32q over three independent streams of kBlock
-// bytes each, merged with byte-indexed tables of x^(8*kBlock) (own generator,
-// crc32c_math.h); a sliced-table fallback when the CPU lacks SSE4.2.
+// Implementation: SSE4.2 crc32q (8 bytes per instruction; the reference's
+// Linux build takes its 4-byte crc32l branch, since _M_X64 is an MSVC macro,
+// crc32c.cpp:207-299) over three independent streams -- kBlock bytes each while
+// 3*kBlock remain, then kShort bytes each while 3*kShort remain (the
+// reference's two tiers, crc32c.cpp:212-244, at other distances) -- merged with
+// byte-indexed tables of x^(8*kBlock) / x^(8*kShort) (own generator,
+// crc32c_math.h); a sliced-table fallback when the CPU lacks SSE4.2 or
+// FDB_CRC32C_FORCE_SOFTWARE is set in the environment (crc32c_host_impl()
+// names the implementation in use).
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #if defined(__x86_64__)
@@ -24,20 +31,25 @@ namespace fdbcrc {
 namespace {
 
 constexpr size_t kBlock = 1024;  // bytes per stream per interleaved round
+constexpr size_t kShort = 256;   // the same for 768 B .. 3 KiB remainders
 
 struct HostTables {
 	uint32_t slice[8][256];     // slice[k][b]: byte b followed by k zero bytes
 	uint32_t merge[4][256];     // x^(8*kBlock) as byte tables
+	uint32_t merge_s[4][256];   // x^(8*kShort)
 	bool sse42 = false;
 	HostTables() {
 		for (uint32_t b = 0; b < 256; ++b) slice[0][b] = byte_step(b);
 		for (int k = 1; k < 8; ++k)
 			for (uint32_t b = 0; b < 256; ++b) slice[k][b] = (slice[k - 1][b] >> 8) ^ slice[0][slice[k - 1][b] & 0xffu];
 		mul_tables_byte(xpow8(kBlock), merge);
+		mul_tables_byte(xpow8(kShort), merge_s);
 #if defined(__x86_64__)
 		unsigned a, b, c, d;
 		if (__get_cpuid(1, &a, &b, &c, &d)) sse42 = (c & bit_SSE4_2) != 0;
 #endif
+		const char* force = getenv("FDB_CRC32C_FORCE_SOFTWARE");
+		if (force && *force && *force != '0') sse42 = false;
 	}
 };
 
@@ -46,8 +58,8 @@ const HostTables& tables() {
 	return t;
 }
 
-inline uint32_t apply_merge(const HostTables& t, uint32_t r) {
-	return t.merge[0][r & 0xff] ^ t.merge[1][(r >> 8) & 0xff] ^ t.merge[2][(r >> 16) & 0xff] ^ t.merge[3][r >> 24];
+inline uint32_t apply_merge(const uint32_t (&m)[4][256], uint32_t r) {
+	return m[0][r & 0xff] ^ m[1][(r >> 8) & 0xff] ^ m[2][(r >> 16) & 0xff] ^ m[3][r >> 24];
 }
 
 inline uint64_t load64(const uint8_t* p) {
@@ -82,9 +94,21 @@ __attribute__((target("sse4.2"))) uint32_t raw_sse42(const HostTables& t, uint32
 			s1 = _mm_crc32_u64(s1, load64(q + kBlock));
 			s2 = _mm_crc32_u64(s2, load64(q + 2 * kBlock));
 		}
-		s0 = apply_merge(t, apply_merge(t, (uint32_t)s0) ^ (uint32_t)s1) ^ (uint32_t)s2;
+		s0 = apply_merge(t.merge, apply_merge(t.merge, (uint32_t)s0) ^ (uint32_t)s1) ^ (uint32_t)s2;
 		p += 3 * kBlock;
 		n -= 3 * kBlock;
+	}
+	while (n >= 3 * kShort) {
+		uint64_t s1 = 0, s2 = 0;
+		const uint8_t* q = p;
+		for (const uint8_t* end = p + kShort; q < end; q += 8) {
+			s0 = _mm_crc32_u64(s0, load64(q));
+			s1 = _mm_crc32_u64(s1, load64(q + kShort));
+			s2 = _mm_crc32_u64(s2, load64(q + 2 * kShort));
+		}
+		s0 = apply_merge(t.merge_s, apply_merge(t.merge_s, (uint32_t)s0) ^ (uint32_t)s1) ^ (uint32_t)s2;
+		p += 3 * kShort;
+		n -= 3 * kShort;
 	}
 	for (; n >= 8; n -= 8, p += 8) s0 = _mm_crc32_u64(s0, load64(p));
 	uint32_t r = (uint32_t)s0;
@@ -105,6 +129,8 @@ uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length) {
 #endif
 	return ~fdbcrc::raw_sliced(t, ~crc, input, length);
 }
+
+const char* crc32c_host_impl(void) { return fdbcrc::tables().sse42 ? "sse4.2" : "sliced"; }
 
 uint32_t crc32c_shift(uint32_t reg, uint64_t nbytes) { return fdbcrc::gf2_mul(reg, fdbcrc::xpow8(nbytes)); }
 

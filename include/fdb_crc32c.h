@@ -47,6 +47,12 @@ extern "C" {
  * Same name, arguments, return value and total behaviour. */
 uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length);
 
+/* Which host implementation crc32c_append uses: "sse4.2" (the CPU has the
+ * crc32 instruction; the reference's hw_available, crc32c.cpp:326-344) or
+ * "sliced" (table fallback, the reference's append_table, :124-172; also
+ * forced by FDB_CRC32C_FORCE_SOFTWARE=1 in the environment at load time). */
+const char* crc32c_host_impl(void);
+
 /* ---- GF(2) helpers, host ----------------------------------------------- */
 
 /* Raw register times x^(8*nbytes) mod P: the zeros operator that the
