@@ -10,6 +10,7 @@ from .crc32c import (  # noqa: F401
     Pipeline,
     PipelineJob,
     LIB_PATH,
+    batch_chained,
     batch_fixed,
     batch_varlen,
     crc32c_append,
@@ -22,6 +23,7 @@ from .crc32c import (  # noqa: F401
     stream_bytes,
     testutil_lib,
     gpu_init,
+    host_impl,
     lib,
     varlen_workspace_bytes,
 )

@@ -81,6 +81,14 @@ def lib():
         L.fdb_diskqueue_check_pages_host.argtypes = [vp, vp, u64, vp, vp]
         L.fdb_diskqueue_check_pages_host_submit.restype = ctypes.c_int
         L.fdb_diskqueue_check_pages_host_submit.argtypes = [vp, vp, u64, vp, vp, ctypes.POINTER(u64)]
+        L.crc32c_gpu_batch_chained.restype = ctypes.c_int
+        L.crc32c_gpu_batch_chained.argtypes = [vp, vp, vp, u64, vp, u64, u32, vp, vp, vp]
+        L.crc32c_gpu_chained_workspace_bytes.restype = u64
+        L.crc32c_gpu_chained_workspace_bytes.argtypes = [u64]
+        L.crc32c_gpu_batch_chained_ws.restype = ctypes.c_int
+        L.crc32c_gpu_batch_chained_ws.argtypes = [vp, vp, vp, u64, vp, u64, u32, vp, vp, vp, u64, vp]
+        L.crc32c_host_impl.restype = ctypes.c_char_p
+        L.crc32c_host_impl.argtypes = []
         L.crc32c_gpu_release_stream.restype = ctypes.c_int
         L.crc32c_gpu_release_stream.argtypes = [vp]
         L.crc32c_gpu_stream_bytes.restype = u64
@@ -241,6 +249,40 @@ def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=Non
                 _stream_handle(stream))
     _check(rc, "crc32c_gpu_batch_varlen")
     return out
+
+
+def batch_chained(buf, seg_offsets, seg_lengths, chain_starts, seed=0, seeds=None, out=None, stream=None):
+    """One CRC per chain of segments (crc32c_gpu_batch_chained): chain c is
+    segments [chain_starts[c], chain_starts[c+1]) of (seg_offsets, seg_lengths)
+    into device tensor `buf`, fed in order with the running CRC as the next
+    seed -- e.g. MutationRef's crc = type; append(param1); append(param2)."""
+    _require_device(buf, "buf")
+    _require_device(seg_offsets, "seg_offsets", buf.device, I64)
+    _require_device(seg_lengths, "seg_lengths", buf.device, I64)
+    _require_device(chain_starts, "chain_starts", buf.device, I64)
+    nsegs = seg_offsets.numel()
+    if seg_lengths.numel() != nsegs:
+        raise CRC32CError("seg_offsets and seg_lengths differ in size")
+    nchains = max(chain_starts.numel() - 1, 0)
+    if out is None:
+        out = torch.empty(nchains, dtype=torch.uint32, device=buf.device)
+    _require_device(out, "out", buf.device, U32, nchains)
+    sp = None
+    if seeds is not None:
+        _require_device(seeds, "seeds", buf.device, U32, nchains)
+        sp = ctypes.c_void_p(seeds.data_ptr())
+    with torch.cuda.device(buf.device):
+        rc = lib().crc32c_gpu_batch_chained(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(seg_offsets.data_ptr()),
+                                            ctypes.c_void_p(seg_lengths.data_ptr()), nsegs,
+                                            ctypes.c_void_p(chain_starts.data_ptr()), nchains, seed & 0xFFFFFFFF, sp,
+                                            ctypes.c_void_p(out.data_ptr()), _stream_handle(stream))
+    _check(rc, "crc32c_gpu_batch_chained")
+    return out
+
+
+def host_impl():
+    """"sse4.2" or "sliced": the implementation behind the host crc32c_append."""
+    return lib().crc32c_host_impl().decode()
 
 
 def release_stream(stream):

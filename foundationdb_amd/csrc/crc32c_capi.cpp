@@ -341,6 +341,55 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 	return crc32c_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
 }
 
+// ---- grouped chains ------------------------------------------------------------
+
+static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+
+uint64_t crc32c_gpu_chained_workspace_bytes(uint64_t nsegs) {
+	DeviceState* st = nullptr;
+	if (device_state(&st)) return 0;
+	return align16(varlen_workspace_bytes(nsegs ? nsegs : 1, (uint64_t)st->num_cus * 16)) + align16(4 * nsegs + 4);
+}
+
+int crc32c_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                                uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
+                                const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace, uint64_t workspace_bytes,
+                                void* stream) {
+	if (nchains == 0) return 0;
+	if (!d_out || !d_chain_starts || (nsegs && (!d_base || !d_seg_offsets || !d_seg_lengths)))
+		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_chained: null pointer");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	const uint64_t vws = align16(varlen_workspace_bytes(nsegs ? nsegs : 1, (uint64_t)st->num_cus * 16));
+	if (!d_workspace || workspace_bytes < vws + align16(4 * nsegs + 4) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_chained: workspace too small or misaligned");
+	hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+	uint32_t* segcrc = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_workspace) + vws);
+	if (nsegs)  // raw(0, M_j) of every segment: seed 0xffffffff
+		launch_varlen(static_cast<const uint8_t*>(d_base), d_seg_offsets, d_seg_lengths, nsegs, 0xffffffffu, nullptr,
+		              segcrc, st->tables, st->num_cus, d_workspace, s);
+	launch_chain_fold(d_chain_starts, nchains, d_seg_lengths, segcrc, seed, d_seeds, d_out, st->tables, st->num_cus, s);
+	return check_launch("crc32c_gpu_batch_chained launch");
+}
+
+int crc32c_gpu_batch_chained(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                             uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
+                             const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
+	if (nchains == 0) return 0;
+	if (!d_out || !d_chain_starts || (nsegs && (!d_base || !d_seg_offsets || !d_seg_lengths)))
+		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_chained: null pointer");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), crc32c_gpu_chained_workspace_bytes(nsegs),
+	                              &ws, &have, &hold))
+		return rc;
+	return crc32c_gpu_batch_chained_ws(d_base, d_seg_offsets, d_seg_lengths, nsegs, d_chain_starts, nchains, seed,
+	                                   d_seeds, d_out, ws, have, stream);
+}
+
 // ---- XXH3-64 (include/fdb_xxh3.h) -------------------------------------------
 
 int xxh3_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length, uint64_t count, uint64_t seed,

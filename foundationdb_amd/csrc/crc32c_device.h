@@ -54,6 +54,11 @@ uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                    const DevTables* tabs, int num_cus, void* ws, hipStream_t stream);
+// Grouped chains (crc32c_chain.hip): out[c] = fold of segments [starts[c], starts[c+1])
+// whose independent registers segcrc[j] = crc32c_append(0xffffffff, segment j).
+int launch_chain_fold(const uint64_t* starts, uint64_t nchains, const uint64_t* lengths, const uint32_t* segcrc,
+                      uint32_t seed, const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus,
+                      hipStream_t stream);
 int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out, hipStream_t stream);
 
 }  // namespace fdbcrc

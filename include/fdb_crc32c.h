@@ -113,6 +113,30 @@ int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, co
                                uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
                                uint64_t workspace_bytes, void* stream);
 
+/* Grouped chains: one checksum per CHAIN of non-contiguous segments, the
+ * value of feeding the segments one after another through crc32c_append with
+ * the running CRC as seed -- the reference's chained call sites:
+ *   crc = type; crc = append(crc, param1); crc = append(crc, param2)
+ *     (MutationRef checksums, fdbclient/include/fdbclient/CommitTransaction.h:302-304, 330-332)
+ *   crc = 0; for each 8 KiB read: crc = append(crc, read)   (fdbrpc/FileTransfer.cpp:29-37)
+ * Segment j is the d_seg_lengths[j] bytes at d_base + d_seg_offsets[j] (any
+ * alignment, any order, overlaps allowed); chain c is segments
+ * [d_chain_starts[c], d_chain_starts[c+1]) in that order (d_chain_starts holds
+ * nchains + 1 non-decreasing values <= nsegs; an empty chain yields its seed).
+ * Seed of chain c: d_seeds ? d_seeds[c] : seed.  Writes d_out[c].  Segments
+ * are checksummed independently (byte-balanced over the GPU) and every chain
+ * is folded on the device with GF(2) shifts: no host round trip.  The _ws form
+ * takes a caller-owned workspace of crc32c_gpu_chained_workspace_bytes(nsegs)
+ * bytes (16-byte aligned). */
+int crc32c_gpu_batch_chained(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                             uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
+                             const uint32_t* d_seeds, uint32_t* d_out, void* stream);
+uint64_t crc32c_gpu_chained_workspace_bytes(uint64_t nsegs);
+int crc32c_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                                uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
+                                const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace, uint64_t workspace_bytes,
+                                void* stream);
+
 /* Per-stream library state.  The library keeps, per (device, stream) it has
  * seen, the planning workspace of the convenience entry points and the page
  * kernels' counters (crc32c_gpu_stream_bytes reports how many device bytes).

@@ -111,6 +111,24 @@ def crc32c(crc, data):
     return oracle().append(crc, data)
 
 
+def chained(buf, seg_offsets, seg_lengths, chain_starts, seed=0, seeds=None):
+    """One CRC per chain of segments, fed in order with the running CRC as the
+    next seed -- the reference's chained call sites: MutationRef checksums
+    (fdbclient/include/fdbclient/CommitTransaction.h:302-304: crc = type;
+    append(param1); append(param2)) and FileTransfer's whole-file CRC
+    (fdbrpc/FileTransfer.cpp:29-37).  Chain c = segments [starts[c], starts[c+1])."""
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    n = len(chain_starts) - 1
+    out = np.zeros(n, np.uint32)
+    for c in range(n):
+        crc = int(seeds[c]) if seeds is not None else seed
+        for j in range(int(chain_starts[c]), int(chain_starts[c + 1])):
+            o, ln = int(seg_offsets[j]), int(seg_lengths[j])
+            crc = crc32c(crc, buf[o:o + ln])
+        out[c] = crc
+    return out
+
+
 def crc32c_bitwise(crc, data):
     b = bytes(data)
     return oracle().lib.oracle_crc32c_bitwise(crc & 0xFFFFFFFF, b, len(b))

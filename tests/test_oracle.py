@@ -132,3 +132,14 @@ def test_oracle_varlen_configs_exact_batches(oracle_mod, golden, name):
     got = O.batch_varlen(data, offsets, lengths, seed=d["seed"])
     assert S.digest(got) == {"xor": d["xor"], "sum": d["sum"]}
     assert [int(x) for x in got[:64]] == d["first64"]
+
+
+def test_oracle_chained_matches_reference_file_transfer(golden, oracle_mod):
+    """O.chained (the test oracle of crc32c_gpu_batch_chained) reproduces the
+    reference's own FileTransfer-style chained CRC fixture."""
+    c = golden["chained"]
+    data = sm_bytes(c["nbytes"] + 64, c["state"])
+    offs = list(range(0, c["nbytes"], c["read"]))
+    lens = [min(c["read"], c["nbytes"] - o) for o in offs]
+    assert int(O.chained(data, offs, lens, [0, len(offs)], seed=c["seed"])[0]) == c["crc"]
+    assert int(O.chained(data, [0], [c["nbytes"]], [0, 1])[0]) == c["oneshot"] == c["crc"]
