@@ -280,6 +280,7 @@ struct V7Params {
 	uint32_t* dummy;           // 64 words per wave: target of the no-op XORs
 	uint32_t* ctr;             // per workgroup: slot ranges grabbed (FDBCRC_V7_RANGES > 1)
 	const DevTables* tabs;
+	uint32_t qalign;           // slots per wave rounded to a multiple of this (power of two)
 };
 __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_t& off, uint64_t& len) {
 	off = P.offsets ? P.offsets[i] : i * P.stride;
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		if (tile + 1 == P.ntile) {
 			const uint64_t total = (uint64_t)excl + agg;
 			uint64_t q = (total + P.nwave - 1) / P.nwave;
-			q = q < 4 ? 4 : (q + 3) & ~uint64_t(3);
+			q = q < P.qalign ? P.qalign : (q + P.qalign - 1) & ~uint64_t(P.qalign - 1);
 			P.hdr[0] = total;
 			P.hdr[1] = q;
 		}
@@ -402,6 +403,7 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		return;
 	}
 	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
+	if (!P.cl) return;  // v8 masks the lead chunk and injects the seed itself
 	// lead term: the lead chunk's bytes below k0 (read only when the buffer
 	// starts inside its chunk) with the register ~seed injected at k0, carried
 	// to the end of the pass block (chunkpow).  The garbage after the buffer's
@@ -791,7 +793,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	V7Params P{};
 	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
 	P.seed = seed; P.seeds = seeds; P.out = out; P.tabs = tabs;
-	P.ntile = ntile; P.nwave = nwave;
+	P.ntile = ntile; P.nwave = nwave; P.qalign = 4;
 	P.hdr = reinterpret_cast<uint64_t*>(wp);
 	P.tsum = reinterpret_cast<uint64_t*>(wp + 16);
 	P.incl = P.tsum + ntile + 1;
@@ -814,14 +816,410 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 }
 
 // ---------------------------------------------------------------------------
+// v8 (experiment, -DFDBCRC_VARLEN=8): the same window slots, streamed like the page kernel
+// ---------------------------------------------------------------------------
+// Status: bit-exact (the full -m gpu suite passes with it), but slower than v7
+// on every shape measured (chunks 0.250 vs 0.230 ms, zipf 0.483 vs 0.299 ms,
+// 4 KiB buffers 0.380 vs 0.233 ms): the scalar cursor and the per-window
+// records sit between a unit's compute and the next unit's loads, and 118
+// SGPRs spill.  Kept for the next iteration (lane-parallel walk ahead of the
+// loads), not built by default.
+// v7 keeps a 64-slot table per wave in vector registers (155 VGPRs: 12 waves
+// per CU, one 4 KiB pass in flight per wave) and runs at ~5 TB/s even on
+// large buffers.  v8 moves the control to the scalar unit so the streaming
+// loop is the page kernel's: 1024-thread blocks (16 waves per CU, <= 128
+// VGPRs), two passes computed together (ILP 2) while the next two are in
+// flight -- 8 KiB per wave.
+//
+//  * A scalar CURSOR walks the wave's slot range [lo_s, hi_s) window by
+//    window: buffer j, window m, geometry from the buffer's offset/length
+//    (read with v_readlane from a 64-buffer metadata BATCH held in VGPRs; two
+//    batches, the next one loading while the cursor is in the current one).
+//    Buffers without windows (finished by prep) are skipped.
+//  * For every slot the cursor writes a RECORD into lane q of four record
+//    VGPRs (flags, buffer index, seed, windows remaining): the computing unit
+//    reads them back with v_readlane one unit later.  Lanes 0..7 / 8..15
+//    belong to the two units in flight.
+//  * The lead window zeroes its chunks before the buffer's first chunk (their
+//    loads are clamped to that chunk), masks the bytes before P0 and injects
+//    ~seed at P0 (crc32c.cpp:197: leading zeros are free); the last window
+//    masks the bytes after P1 in lane 63's chunk.  No prep-side edge terms.
+//  * Combining is scalar and per pass: the 16-lane team sums S_t (block
+//    layout, S_t = Rw_t * x^(8*1024*(3-t))) of one buffer add up normalised to
+//    the pass block's end; a buffer open across passes is carried by one
+//    multiply by x^(8*4096); a buffer finishing at team t is multiplied by
+//    x^(-8*(1024*(3-t) + zt)) (table corr).  Finished checksums collect in
+//    lanes and leave 64 at a time (plain stores; atomicXor for the parts of
+//    buffers split between waves, out[] zeroed by prep).
+constexpr uint32_t kV8Threads = 1024;
+constexpr uint32_t r8_VALID = 1u << 0;
+constexpr uint32_t r8_LEAD = 1u << 1;    // window 0: chunks before lo zeroed, seed injected at k0
+constexpr uint32_t r8_LAST = 1u << 2;    // the buffer's last window: tail mask zt, finish
+constexpr uint32_t r8_PSTART = 1u << 3;  // first window of the buffer's part in this wave
+constexpr uint32_t r8_PEND = 1u << 4;    // last slot of the wave, the buffer continues (rec_r: windows left)
+constexpr uint32_t r8_LO = 8;            // lo / 16 (6 bits)
+constexpr uint32_t r8_K0 = 16;           // P0 % 16 (4 bits)
+constexpr uint32_t r8_ZT = 20;           // trailing zeros (4 bits)
+
+// v in lane `lane` of `old` (uniform v and lane): a compare and a select
+__device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t lane, uint32_t old) {
+	return (threadIdx.x & 63) == lane ? v : old;
+}
+
+__global__ __launch_bounds__(kV8Threads) void k_varlen8(const V7Params P_) {
+	__shared__ uint32_t lds[kLdsBytesB / 4];
+	// kernel arguments as plain locals: the lambdas below capture by reference,
+	// and a captured struct would be copied to scratch (every use a VGPR load)
+	const DevTables* __restrict__ const T = P_.tabs;
+	const uint64_t count = P_.count, stride = P_.stride, length = P_.length;
+	const uint64_t* __restrict__ const offsets = P_.offsets;
+	const uint64_t* __restrict__ const lengths = P_.lengths;
+	const uint32_t* __restrict__ const seeds = P_.seeds;
+	const uint32_t seed = P_.seed;
+	const uint32_t* __restrict__ const gs = P_.gs;
+	uint32_t* const out = P_.out;
+	uint32_t* const dummy_base = P_.dummy;
+	const uint64_t* const hdr = P_.hdr;
+	const uint8_t* const pbase = P_.base;
+	typedef __attribute__((address_space(1))) const uint64_t g_u64;
+	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(hdr);
+	const uint64_t total = rdfirst64(hp[0]), Qs = rdfirst64(hp[1]);
+	const uint64_t w = (uint64_t)blockIdx.x * (kV8Threads / 64) + rdfirst(threadIdx.x >> 6);
+	const uint64_t lo_s = w * Qs;
+	if (lo_s >= total) {  // no slots: take part in the LDS fill's barrier and leave
+		fill_lds_b(lds, T);
+		return;
+	}
+	const uint64_t nslot = lo_s + Qs < total ? Qs : total - lo_s;
+	const LaneCtx c = make_ctx();
+	const int lane = c.lane;
+	const uint32_t col4 = (lane & 31) * 4;
+	const uint32_t c4 = col4 | 0x10000u;
+	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
+	const uint64_t base = reinterpret_cast<uint64_t>(pbase);
+
+	// ---- the buffer holding slot lo_s: the largest j with gs[j] <= lo_s (buffers
+	// without windows share the first slot of the next windowed buffer) ----
+	uint64_t j = 0;
+	{
+		uint64_t a = 0, n = count;  // answer in [a, a + n)
+		while (n > 1) {
+			const uint64_t stp = (n + 63) >> 6;
+			const uint64_t k = (uint64_t)lane * stp;
+			bool le = false;
+			if (k < n && k > 0) le = gld32(&gs[a + k]) <= (uint32_t)lo_s;
+			const uint64_t cnt = __builtin_popcountll(__ballot(le));
+			a += cnt * stp;
+			n = (cnt + 1) * stp <= n ? stp : n - cnt * stp;
+		}
+		j = rdfirst64(a);
+	}
+	const uint64_t j_first = j;
+
+	// ---- metadata batches: lane l of batch slot (kb & 1) holds buffer 64*kb + l ----
+	uint64_t b_off0 = 0, b_len0 = 0, b_off1 = 0, b_len1 = 0;
+	uint32_t b_s0 = 0, b_s1 = 0;
+	auto fetch = [&](uint64_t kbn, uint64_t& off, uint64_t& len, uint32_t& sd) __attribute__((always_inline)) {
+		const uint64_t i = kbn * 64 + (uint64_t)lane;
+		const uint64_t ic = i < count ? i : count - 1;
+		off = offsets ? gld64(&offsets[ic]) : ic * stride;
+		len = lengths ? gld64(&lengths[ic]) : length;
+		sd = ~(seeds ? gld32(&seeds[ic]) : seed);
+	};
+	uint64_t kb = j >> 6;
+	if (kb & 1) {
+		fetch(kb, b_off1, b_len1, b_s1);
+		fetch(kb + 1, b_off0, b_len0, b_s0);
+	} else {
+		fetch(kb, b_off0, b_len0, b_s0);
+		fetch(kb + 1, b_off1, b_len1, b_s1);
+	}
+
+	// ---- cursor (uniform) ----
+	uint32_t W = 0, lo = 0, k0 = 0, zt = 0, s0 = 0;
+	uint64_t wb = 0, m = 0;
+	uint64_t rem = nslot;  // slots left to walk
+	auto enter = [&]() __attribute__((always_inline)) {   // geometry of buffer j; buffers without windows are skipped
+		for (;;) {
+			if (j >= count) {
+				W = 0;
+				return;
+			}
+			if ((j >> 6) != kb) {  // the next batch: the slot just left gets batch kb + 2
+				++kb;
+				if (kb & 1)
+					fetch(kb + 1, b_off0, b_len0, b_s0);
+				else
+					fetch(kb + 1, b_off1, b_len1, b_s1);
+			}
+			const int l = (int)(j & 63);
+			const bool odd = kb & 1;
+			const uint64_t off = odd ? rdlane64(b_off1, l) : rdlane64(b_off0, l);
+			const uint64_t len = odd ? rdlane64(b_len1, l) : rdlane64(b_len0, l);
+			const Geo7 g = geo7(base + off, len);
+			if (rdfirst(g.W)) {
+				W = rdfirst(g.W);
+				lo = rdfirst(g.lo);
+				k0 = rdfirst(g.k0);
+				zt = rdfirst(g.zt);
+				wb = rdfirst64(g.A - g.lo);
+				s0 = rdfirst(odd ? rdlane(b_s1, l) : rdlane(b_s0, l));
+				return;
+			}
+			j = rdfirst64(j + 1);
+		}
+	};
+	enter();
+	m = lo_s - rdfirst(gld32(&gs[j]));
+	// empty slots (past the range's end) load the last chunk of the range's first
+	// window, which always holds bytes of its buffer (windows end at E)
+	const uint64_t safe_wa = wb + 1024 * m;
+	bool at_start = true;
+
+	uint32_t rec_f = 0, rec_j = 0, rec_s = 0, rec_r = 0;
+	// one window into record lane q; returns its address and the clamp of its loads
+	auto walk1 = [&](uint32_t q, uint64_t& wa, uint32_t& clamp) __attribute__((always_inline)) {
+		if (rem == 0 || W == 0) {
+			rec_f = wrlane(0u, q, rec_f);
+			wa = safe_wa;
+			clamp = 1008;
+			return;
+		}
+		const bool last = m + 1 == W;
+		// zt in every record: a part that ends with the wave (PEND) is moved to
+		// the buffer's end too, so it drops the same trailing zeros
+		const uint32_t f = r8_VALID | (m == 0 ? (r8_LEAD | ((lo >> 4) << r8_LO) | (k0 << r8_K0)) : 0u) |
+		                   ((m == 0 || at_start) ? r8_PSTART : 0u) | (last ? r8_LAST : 0u) | (zt << r8_ZT) |
+		                   ((rem == 1 && !last) ? r8_PEND : 0u);
+		rec_f = wrlane(f, q, rec_f);
+		rec_j = wrlane((uint32_t)(j - j_first), q, rec_j);
+		rec_s = wrlane(s0, q, rec_s);
+		rec_r = wrlane((uint32_t)(W - m - 1), q, rec_r);
+		wa = wb + 1024 * m;
+		clamp = m == 0 ? lo : 0u;
+		at_start = false;
+		--rem;
+		if (last) {
+			++j;
+			m = 0;
+			enter();
+		} else {
+			++m;
+		}
+	};
+
+	Block u0[2], u1[2];
+	// a unit: two passes of four windows; load k of a pass fetches team {0,2,1,3}[k].
+	// PLAIN unit: eight interior windows of one buffer whose part is already
+	// open (not its first or last window, not the wave's last slot): contiguous
+	// 8 KiB, no records, no masks, combined as two 4 KiB blocks.
+	auto load_unit = [&](Block (&u)[2], uint32_t q0, bool& plain) __attribute__((always_inline)) {
+		plain = rem > 8 && W != 0 && !at_start && m > 0 && m + 8 < W;
+		if (plain) {
+			const uint64_t wa0 = wb + 1024 * m;
+			m += 8;
+			rem -= 8;
+#pragma unroll
+			for (int p = 0; p < 2; ++p)
+#pragma unroll
+				for (int k = 0; k < 4; ++k) {
+					const int t = ((k & 1) << 1) | (k >> 1);
+					u[p].r[k] = ld16(reinterpret_cast<const uint8_t*>(wa0 + 4096 * p + 1024 * t + c.ld_off));
+				}
+			return;
+		}
+#pragma unroll
+		for (int p = 0; p < 2; ++p) {
+			uint64_t wa[4];
+			uint32_t cl[4];
+#pragma unroll
+			for (int t = 0; t < 4; ++t) walk1(q0 + 4 * p + t, wa[t], cl[t]);
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				const int t = ((k & 1) << 1) | (k >> 1);
+				const uint32_t off = c.ld_off > cl[t] ? c.ld_off : cl[t];
+				u[p].r[k] = ld16(reinterpret_cast<const uint8_t*>(wa[t] + off));
+			}
+		}
+	};
+	bool plainA = false, plainB = false;
+	load_unit(u0, 0, plainA);
+	fill_lds_b(lds, T);
+
+	// ---- combine state (uniform) ----
+	uint32_t acc = 0;
+	bool open = false, part_mid = false;  // part_mid: the open part began after the buffer's window 0
+	uint32_t mine = 0, myidx = 0, mysplit = 0;  // finished checksums: lane k holds the k-th
+	uint32_t nfin = 0;
+	uint32_t* const dummy = dummy_base + w * 64;
+	auto flush = [&]() __attribute__((always_inline)) {  // unconditional vector memory operations (dummy targets)
+		bool have = (uint32_t)lane < nfin;
+#ifdef FDBCRC_DEBUG
+		if (have && j_first + myidx >= count) {
+			if (atomicAdd(&g_dbg[2], 1ull) == 0) {
+				g_dbg[3] = j_first + myidx;
+				g_dbg[4] = 10;
+			}
+			have = false;
+		}
+#endif
+		const bool sp = have && mysplit;
+		*((have && !sp) ? out + j_first + myidx : dummy + lane) = mine;
+		atomicXor(sp ? out + j_first + myidx : dummy + lane, sp ? mine : 0u);
+		nfin = 0;
+	};
+	auto emit = [&](uint32_t jr, uint32_t v, bool split) __attribute__((always_inline)) {
+		mine = wrlane(v, nfin, mine);
+		myidx = wrlane(jr, nfin, myidx);
+		mysplit = wrlane(split ? 1u : 0u, nfin, mysplit);
+		if (++nfin == 64) flush();
+	};
+	auto combine_pass = [&](uint32_t R, uint32_t q0) __attribute__((always_inline)) {
+		if (open) acc = umul(T->block, acc);  // to this pass block's end
+#pragma unroll
+		for (int t = 0; t < 4; ++t) {
+			const uint32_t f = rdlane(rec_f, (int)(q0 + t));
+			if (!(f & r8_VALID)) continue;
+			uint32_t S = rdlane(R, 16 * t);
+			if (f & r8_PSTART) {
+				acc = 0;
+				part_mid = !(f & r8_LEAD);
+			}
+			// the seed's bytes past the lead chunk when that chunk ends the window:
+			// an XOR into the register at the window's end
+			if ((f & r8_LEAD) && ((f >> r8_LO) & 63u) == 63u && ((f >> r8_K0) & 15u) > 12u) {
+				const uint32_t kk = (f >> r8_K0) & 15u;
+				S ^= mul_xpow(T, rdlane(rec_s, (int)(q0 + t)) >> (8 * (16 - kk)), 1024 * (3 - t));
+			}
+			acc ^= S;
+			open = true;
+			if (f & (r8_LAST | r8_PEND)) {
+				uint32_t v = umul(T->corr[t][(f >> r8_ZT) & 15u], acc);
+				if (f & r8_PEND) v = mul_xpow(T, v, 1024 * (uint64_t)rdlane(rec_r, (int)(q0 + t)));
+				const bool split = part_mid || (f & r8_PEND);
+				emit(rdlane(rec_j, (int)(q0 + t)), part_mid ? v : ~v, split);  // window 0's part inverts
+				open = false;
+			}
+		}
+	};
+	auto compute_unit = [&](Block (&u)[2], uint32_t q0, bool plain) __attribute__((always_inline)) {
+		// edge masks: lead windows (chunks before lo, the lead chunk with the seed
+		// injected, the seed's spill into the next chunk) and last windows
+#pragma unroll
+		for (int p = 0; p < 2 && !plain; ++p) {
+			uint32_t fl[4];
+			uint32_t any = 0;
+#pragma unroll
+			for (int t = 0; t < 4; ++t) {
+				fl[t] = rdlane(rec_f, (int)(q0 + 4 * p + t));
+				any |= fl[t];
+			}
+			if (any & (r8_LEAD | r8_LAST)) {
+#pragma unroll
+				for (int k = 0; k < 4; ++k) {
+					const int t = ((k & 1) << 1) | (k >> 1);
+					const uint32_t f = fl[t];
+					if (f & r8_LEAD) {
+						const uint32_t lo16 = ((f >> r8_LO) & 63u) << 4, kk = (f >> r8_K0) & 15u;
+						const Masks mk = edge_masks(kk, 16u, rdlane(rec_s, (int)(q0 + 4 * p + t)));
+						const bool z = c.ld_off < lo16, ld = c.ld_off == lo16, sp = c.ld_off == lo16 + 16;
+#pragma unroll
+						for (int d = 0; d < 4; ++d) {
+							uint32_t v = z ? 0u : u[p].r[k][d];
+							v = ld ? ((v & mk.lm[d]) ^ mk.inj[d]) : v;
+							v ^= (sp && d == 0) ? mk.spill : 0u;
+							u[p].r[k][d] = v;
+						}
+					}
+					if ((f & r8_LAST) && ((f >> r8_ZT) & 15u)) {
+						uint32_t km[4];
+						keep_below7(16u - ((f >> r8_ZT) & 15u), km);
+#pragma unroll
+						for (int d = 0; d < 4; ++d) u[p].r[k][d] &= lane == 63 ? km[d] : ~0u;
+					}
+				}
+			}
+		}
+		unswizzle(u[0]);
+		unswizzle(u[1]);
+		uint32_t x0 = u[0].r[0][0], x1 = u[1].r[0][0];
+#pragma unroll
+		for (int wd = 0; wd < 16; ++wd) {
+			x0 = word_step4_next(lds, x0, wd < 15 ? u[0].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u, c4);
+			x1 = word_step4_next(lds, x1, wd < 15 ? u[1].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u, c4);
+		}
+		const uint32_t R0 = row_xor(mul_nibbles(lds, x0, c_lane));
+		const uint32_t R1 = row_xor(mul_nibbles(lds, x1, c_lane));
+		if (plain) {  // two whole 4 KiB blocks of the open part
+			const uint32_t B0 = rdlane(R0, 0) ^ rdlane(R0, 16) ^ rdlane(R0, 32) ^ rdlane(R0, 48);
+			const uint32_t B1 = rdlane(R1, 0) ^ rdlane(R1, 16) ^ rdlane(R1, 32) ^ rdlane(R1, 48);
+			acc = umul(T->block, umul(T->block, acc) ^ B0) ^ B1;
+			return;
+		}
+		combine_pass(R0, q0);
+		combine_pass(R1, q0 + 4);
+	};
+
+	const uint64_t nunit = (nslot + 7) >> 3;
+	for (uint64_t un = 0; un < nunit; un += 2) {
+		load_unit(u1, 8, plainB);
+		__builtin_amdgcn_sched_barrier(0);
+		compute_unit(u0, 0, plainA);
+		__builtin_amdgcn_sched_barrier(0);
+		load_unit(u0, 0, plainA);
+		__builtin_amdgcn_sched_barrier(0);
+		if (un + 1 < nunit) compute_unit(u1, 8, plainB);
+		__builtin_amdgcn_sched_barrier(0);
+	}
+	if (nfin) flush();
+}
+
+int launch_varlen8(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
+                   uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
+                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream) {
+	const uint64_t grid = (uint64_t)num_cus;
+	const uint64_t nwave = grid * (kV8Threads / 64);
+	const uint64_t ntile = (count + kTileW - 1) / kTileW;
+	uint8_t* wp = static_cast<uint8_t*>(ws);
+	V7Params P{};
+	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
+	P.seed = seed; P.seeds = seeds; P.out = out; P.tabs = tabs;
+	P.ntile = ntile; P.nwave = nwave; P.qalign = 8;
+	P.hdr = reinterpret_cast<uint64_t*>(wp);
+	P.tsum = reinterpret_cast<uint64_t*>(wp + 16);
+	P.incl = P.tsum + ntile + 1;
+	uint32_t* wave_tile = reinterpret_cast<uint32_t*>(P.incl + ntile + 1);
+	P.gs = wave_tile + nwave;
+	P.cl = nullptr;  // no prep-side lead terms
+	P.dummy = P.gs + 2 * count;
+	P.ctr = P.dummy + 64 * nwave;
+	P.scanned = ntile > 8192;
+	P.selfsum = ntile <= kSelfSumTiles;
+	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	if (P.scanned) k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 8, 8);
+	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	k_varlen8<<<(unsigned)grid, kV8Threads, 0, stream>>>(P);
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) { return varlen7_workspace_bytes(count, nwave); }
 
+// Streaming kernel: v7 (default) or the v8 experiment (-DFDBCRC_VARLEN=8: correct,
+// measured slower -- DESIGN.md §3.2)
+#ifndef FDBCRC_VARLEN
+#define FDBCRC_VARLEN 7
+#endif
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                   hipStream_t stream) {
+#if FDBCRC_VARLEN == 8
+	return launch_varlen8(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream);
+#else
 	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream);
+#endif
 }
 
 // Fixed stride, any length and alignment: the same engine with metadata
@@ -829,7 +1227,11 @@ int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
                          const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                          hipStream_t stream) {
+#if FDBCRC_VARLEN == 8
+	return launch_varlen8(base, nullptr, nullptr, stride, length, count, seed, seeds, out, tabs, num_cus, ws, stream);
+#else
 	return launch_varlen7(base, nullptr, nullptr, stride, length, count, seed, seeds, out, tabs, num_cus, ws, stream);
+#endif
 }
 
 #ifdef FDBCRC_DEBUG
