@@ -40,13 +40,16 @@ def pmc_traffic(workload):
 
 class CpuSample:
     def __init__(self, desc, nbytes, buf, stride=None, length=None, count=None, offsets=None, lengths=None, seed=0,
-                 ref=None, port=None):
+                 ref=None, port=None, port_only=False):
         self.desc, self.nbytes, self.buf = desc, nbytes, buf
+        self.port_only = port_only  # no compiled reference for this path: time the oracle restatement
         self.stride, self.length, self.count = stride, length, count
         self.offsets, self.lengths, self.seed = offsets, lengths, seed
         self.ref, self.port = ref, port  # optional callables(O) for non-CRC workloads
 
     def available(self, O):
+        if self.port_only:
+            return False
         return O.xxh3_reference_available() if self.ref else O.reference_available()
 
     def run_reference(self, O):
@@ -348,6 +351,140 @@ class Xxh3Pages:
                          port=lambda O: O.xxh3_batch_fixed(buf, 4096, self.length, n, threads=1))
 
 
+def _sqlite_pages_on_device(dev, count, kinds_per=16):
+    """1 Mi SQLite pages of 4 KiB in HBM, the mix a database written by several
+    FoundationDB versions holds: trailers from the current writer (XXH3,
+    KeyValueStoreSQLite.cpp:106-116) on 12 of every 16 pages, from the legacy
+    writer (CRC-32C, :119-128) on 3, and a corrupt trailer on 1.  The trailers
+    are built with the engine's own batch kernels; verify() re-checks a sample
+    with the CPU oracle, so nothing here is circular."""
+    import foundationdb_amd.xxh3 as X
+    buf = torch.empty(count * 4096, dtype=torch.uint8, device=dev)
+    F.fill_splitmix64(buf, STATE)
+    pages = buf.view(count, 4096)
+    h = X.batch_fixed(buf, 4096, 4088, count)
+    c = F.batch_fixed(buf, 4096, 4088, count, seed=0xFDBEEFDB)
+    kind = torch.arange(count, device=dev) % kinds_per
+    hv = h.view(torch.int64)
+    p1x = ((hv >> 32) & 0x00FFFFFF).to(torch.int32)
+    p2x = (hv & 0xFFFFFFFF).to(torch.int64).to(torch.int32)
+    tr = torch.zeros(count, 2, dtype=torch.int32, device=dev)
+    xx = kind < 12
+    cr = (kind >= 12) & (kind < 15)
+    tr[:, 0] = torch.where(xx, p1x, torch.where(cr, torch.zeros_like(p1x), torch.full_like(p1x, 0x7E000001)))
+    tr[:, 1] = torch.where(xx, p2x, torch.where(cr, c.view(torch.int32), p2x ^ 0x5A5A5A5A))
+    pages[:, 4088:4096] = tr.view(torch.uint8).view(count, 8)
+    expect = torch.where(xx, 2, torch.where(cr, 1, 0)).to(torch.uint8)
+    return buf, expect
+
+
+class SqliteVerify:
+    """SQLite whole-file page verification (SQLiteDB::checkAllPageChecksums,
+    KeyValueStoreSQLite.cpp:1378-1470 -> PageChecksumCodec::checksum(write=false),
+    :100-201): 1 Mi mixed 4 KiB pages, device-resident (fdb_sqlite_verify_pages)."""
+    metric = "device-resident SQLite page verification GiB/s (1 Mi mixed 4 KiB pages); % of HBM-read peak"
+    kernel_name = "fdb_sqlite_verify_pages (classify + k_pages4k list + k_xxh3_rows list + compare)"
+
+    def __init__(self, dev, rank, count=1 << 20):
+        import foundationdb_amd.pagecheck as PC
+        self.PC, self.count = PC, count
+        self.buf, self.expect = _sqlite_pages_on_device(dev, count)
+        self.bytes_per_step = count * 4096
+        self.algorithmic_bytes_per_step = count * (4096 + 1)
+        self.data_desc = (f"synthetic: splitmix64 pages (state 0x{STATE:X}) in HBM with XXH3 / CRC-32C / corrupt "
+                          "trailers 12:3:1")
+        self.config = {"workload": f"{count} x 4 KiB SQLite pages, mixed trailers, device-resident", "pages": count}
+        self.status = None
+
+    def step(self, stream):
+        self.status, self.bad = self.PC.sqlite_verify_pages(self.buf, 4096, self.count, first_pgno=1, stream=stream)
+
+    def verify(self):
+        from oracle import oracle as O
+        if not torch.equal(self.status, self.expect):
+            return False
+        if int(self.bad.cpu().numpy().view(np.uint64)[0]) != self.count // 16:
+            return False
+        h = self.buf.view(self.count, 4096)
+        st = self.status.cpu().numpy()
+        for i in np.random.default_rng(0).choice(self.count, 128, replace=False):
+            if O.sqlite_verify_page(h[i].cpu().numpy(), int(i) + 1) != int(st[i]):
+                return False
+        return True
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        n = 4096
+        host = self.buf[:n * 4096].cpu().numpy()
+        return CpuSample(f"first {n} pages of the batch through the oracle's PageChecksumCodec::checksum "
+                         "restatement (reference-pinned CRC-32C / XXH3 / lookup3 primitives, one call per page)",
+                         n * 4096, host, port_only=True,
+                         port=lambda O_: [O_.sqlite_verify_page(host[4096 * i:4096 * (i + 1)], i + 1)
+                                          for i in range(n)])
+
+
+class SqliteVerifyHost(SqliteVerify):
+    """The same 1 Mi pages starting in pinned host memory (as read from disk):
+    fdb_sqlite_verify_pages_host through the pipeline (PCIe-bound by design)."""
+    metric = "host-to-host SQLite page verification GiB/s (1 Mi mixed 4 KiB pages); % of PCIe peak"
+    kernel_name = "host pipeline (H2D + fdb_sqlite_verify_pages + D2H of status bytes)"
+    host_timed = True
+    pcie_peak_gbs = 63.0
+
+    def __init__(self, dev, rank, count=1 << 20):
+        super().__init__(dev, rank, count)
+        dbuf = self.buf
+        self.buf = torch.empty(count * 4096, dtype=torch.uint8).pin_memory()
+        self.buf.copy_(dbuf)
+        self.expect = self.expect.cpu()
+        del dbuf
+        self.pipe = F.Pipeline(segment_bytes=64 << 20, nstreams=4)
+        self.config = {"workload": f"{count} x 4 KiB SQLite pages, mixed trailers, host-resident, pinned pipeline "
+                                   "(4 streams x 64 MiB)", "pages": count}
+
+    def step(self, stream):
+        st, bad = self.pipe.sqlite_verify_pages(self.buf, 4096, self.count, first_pgno=1)
+        self.status, self.bad = torch.from_numpy(st), torch.from_numpy(bad.view(np.int64))
+
+
+class Xxh3Zipf(VarLen):
+    """XXH3-64 of every packet of the configs[2] Zipf batch (FlowTransport packet
+    checksum, fdbrpc/FlowTransport.cpp:2025-2068), device-resident."""
+    metric = "device-resident XXH3-64 GiB/s on Zipf 64 B-16 KiB packet batches; % of HBM-read peak"
+    kernel_name = "fdbxxh::k_xxh3 (+ planner)"
+
+    def __init__(self, dev, rank):
+        import foundationdb_amd.xxh3 as X
+        super().__init__(dev, rank, zipf_lengths(), S.ZIPF_ALIGN,
+                         "Zipf(1.0) packet sizes 64 B - 16 KiB, ~1 GiB per batch, XXH3-64 per packet")
+        self.X = X
+        self.metric = Xxh3Zipf.metric
+        self.out = torch.empty(self.h_lengths.size, dtype=torch.uint64, device=dev)
+        self.algorithmic_bytes_per_step = self.bytes_per_step + 24 * self.h_lengths.size
+
+    def step(self, stream):
+        self.X.batch_varlen(self.buf, self.offsets, self.lengths, out=self.out, stream=stream)
+
+    def verify(self):
+        from oracle import oracle as O
+        got = self.out.cpu().numpy().view(np.uint64)
+        rng = np.random.default_rng(0)
+        # every packet against the reference's own flow/xxhash.c over the same bytes
+        want = O.ref_xxh3_batch_varlen(self.buf.cpu().numpy(), self.h_offsets, self.h_lengths)
+        return bool(np.array_equal(got, want))
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        k = 120000
+        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        host = self.buf[:end].cpu().numpy()
+        offs, lens = self.h_offsets[:k], self.h_lengths[:k]
+        return CpuSample(f"first {k} packets ({int(lens.sum()) >> 20} MiB), reference flow/xxhash.c XXH3_64bits",
+                         int(lens.sum()), host,
+                         ref=lambda O_: O_.ref_xxh3_batch_varlen(host, offs, lens),
+                         port=lambda O_: O_.xxh3_batch_varlen(host, offs, lens, threads=1))
+
+
 WORKLOADS = {
     "pages4k": lambda dev, rank: Pages(dev, rank, 4096, 1 << 20, 0),
     "pages8k": lambda dev, rank: Pages(dev, rank, 8192, 1 << 19, 0xFDBEEFDB),
@@ -362,4 +499,7 @@ WORKLOADS = {
     "chunks-host": lambda dev, rank: HostChunks(dev, rank),
     "pages4k-host": lambda dev, rank: HostPages(dev, rank),
     "xxh3-pages4k": lambda dev, rank: Xxh3Pages(dev, rank),
+    "xxh3-zipf": lambda dev, rank: Xxh3Zipf(dev, rank),
+    "sqlite-verify": lambda dev, rank: SqliteVerify(dev, rank),
+    "sqlite-verify-host": lambda dev, rank: SqliteVerifyHost(dev, rank),
 }

@@ -289,6 +289,22 @@ def ref_hashlittle2(data, pc, pb):
     return c.value, b.value
 
 
+def ref_xxh3_batch_varlen(buf, offsets, lengths):
+    """Single-threaded C loop over the reference XXH3_64bits, one packet per
+    (offset, length) (ref_bench_xxh3.c; bench cpu_baseline)."""
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+    if offsets.size:
+        assert int((offsets + lengths).max()) <= buf.nbytes
+    f = xxh3_reference().ref_xxh3_batch_varlen
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    out = np.zeros(offsets.size, np.uint64)
+    f(buf.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, offsets.size, out.ctypes.data)
+    return out
+
+
 def ref_xxh3_batch_fixed(buf, stride, length, count, seed=0):
     """Single-threaded C loop over the reference XXH3_64bits (ref_bench_xxh3.c; bench cpu_baseline)."""
     buf = np.ascontiguousarray(buf).view(np.uint8)

@@ -18,3 +18,9 @@ void ref_xxh3_batch_fixed(const uint8_t* base, uint64_t stride, uint64_t length,
 	else
 		for (uint64_t i = 0; i < count; ++i) out[i] = XXH3_64bits_withSeed(base + i * stride, (size_t)length, seed);
 }
+
+/* The FlowTransport packet shape: one packet per (offset, length). */
+void ref_xxh3_batch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count,
+                           uint64_t* out) {
+	for (uint64_t i = 0; i < count; ++i) out[i] = XXH3_64bits(base + offsets[i], (size_t)lengths[i]);
+}

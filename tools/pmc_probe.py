@@ -32,6 +32,8 @@ for _ in range(5):
         X.batch_fixed(big, 4096, 4088, n, out=out64)
     elif mode == "pages4k":
         F.batch_fixed(big, 4096, 4096, n, out=out)
+    elif mode == "pages8k":
+        F.batch_fixed(big, 8192, 8192, n // 2, seed=0xFDBEEFDB, out=out)
     elif mode == "stride0":
         F.batch_fixed(big, 0, 4096, n, out=out)
 torch.cuda.synchronize()

@@ -39,8 +39,10 @@ def main(mode="pages4k", workload="pages4k", kernel=("k_pages4k",), algorithmic=
     mean, dur, launches = load(mode, kernel)
     fetch = mean["FETCH_SIZE"] * 1024 * 2
     write = mean["WRITE_SIZE"] * 1024
+    commit_file = os.path.join(ROOT, "gpurun_out", "pmc", "commit.txt")
     out = {
         "workload": workload,
+        "commit": open(commit_file).read().strip() if os.path.exists(commit_file) else None,
         "kernel": " + ".join(kernel),
         "source": f"rocprofv3 --pmc <counters> --kernel-trace, separate passes, {launches} launches per pass",
         "correction": "FETCH_SIZE(KiB)*1024*2 (gfx950 reports half of wide streaming reads) + WRITE_SIZE(KiB)*1024",
@@ -75,6 +77,7 @@ def _varlen(fn):
 VARLEN_KERNELS = ("k_v7count", "k_v7prep", "k_scan", "k_varlen7")
 PRESETS = {
     "pages4k": ("pages4k", "pages4k", ("k_pages4k",), (1 << 20) * 4100, 1 << 20),
+    "pages8k": ("pages8k", "pages8k", ("k_pages4k",), (1 << 19) * 8196, 1 << 19),
     "xxh3": ("xxh3", "xxh3-pages4k", ("k_xxh3_rows",), (1 << 20) * (4088 + 8), 1 << 20),
     "zipf": ("zipf", "zipf", VARLEN_KERNELS, _varlen("zipf_lengths"), None),
     "chunks": ("chunks", "chunks", VARLEN_KERNELS, _varlen("chunk_lengths"), None),
