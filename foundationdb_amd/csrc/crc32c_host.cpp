@@ -21,7 +21,6 @@
 #include <string.h>
 
 #if defined(__x86_64__)
-#include <cpuid.h>
 #include <nmmintrin.h>
 #endif
 
@@ -37,26 +36,19 @@ struct HostTables {
 	uint32_t slice[8][256];     // slice[k][b]: byte b followed by k zero bytes
 	uint32_t merge[4][256];     // x^(8*kBlock) as byte tables
 	uint32_t merge_s[4][256];   // x^(8*kShort)
-	bool sse42 = false;
 	HostTables() {
 		for (uint32_t b = 0; b < 256; ++b) slice[0][b] = byte_step(b);
 		for (int k = 1; k < 8; ++k)
 			for (uint32_t b = 0; b < 256; ++b) slice[k][b] = (slice[k - 1][b] >> 8) ^ slice[0][slice[k - 1][b] & 0xffu];
 		mul_tables_byte(xpow8(kBlock), merge);
 		mul_tables_byte(xpow8(kShort), merge_s);
-#if defined(__x86_64__)
-		unsigned a, b, c, d;
-		if (__get_cpuid(1, &a, &b, &c, &d)) sse42 = (c & bit_SSE4_2) != 0;
-#endif
-		const char* force = getenv("FDB_CRC32C_FORCE_SOFTWARE");
-		if (force && *force && *force != '0') sse42 = false;
 	}
 };
 
-const HostTables& tables() {
-	static const HostTables t;
-	return t;
-}
+// Built when the library is loaded (as the reference's static hw_available,
+// crc32c.cpp:344): no initialisation guard on the per-call path.
+const HostTables g_tables;
+
 
 inline uint32_t apply_merge(const uint32_t (&m)[4][256], uint32_t r) {
 	return m[0][r & 0xff] ^ m[1][(r >> 8) & 0xff] ^ m[2][(r >> 16) & 0xff] ^ m[3][r >> 24];
@@ -80,7 +72,30 @@ uint32_t raw_sliced(const HostTables& t, uint32_t s, const uint8_t* p, size_t n)
 }
 
 #if defined(__x86_64__)
+// Short buffers (< 64 B: keys, small values, packet headers): no alignment
+// prologue (x86 loads need none), 8-byte steps, then 4/2/1-byte steps.
+__attribute__((target("sse4.2"))) inline uint32_t raw_sse42_short(uint32_t s, const uint8_t* p, size_t n) {
+	uint64_t s0 = s;
+	for (; n >= 8; n -= 8, p += 8) s0 = _mm_crc32_u64(s0, load64(p));
+	uint32_t r = (uint32_t)s0;
+	if (n & 4) {
+		uint32_t v;
+		memcpy(&v, p, 4);
+		r = _mm_crc32_u32(r, v);
+		p += 4;
+	}
+	if (n & 2) {
+		uint16_t v;
+		memcpy(&v, p, 2);
+		r = _mm_crc32_u16(r, v);
+		p += 2;
+	}
+	if (n & 1) r = _mm_crc32_u8(r, *p);
+	return r;
+}
+
 __attribute__((target("sse4.2"))) uint32_t raw_sse42(const HostTables& t, uint32_t s, const uint8_t* p, size_t n) {
+	if (n < 64) return raw_sse42_short(s, p, n);
 	while (n && (reinterpret_cast<uintptr_t>(p) & 7)) {
 		s = _mm_crc32_u8(s, *p++);
 		--n;
@@ -110,27 +125,56 @@ __attribute__((target("sse4.2"))) uint32_t raw_sse42(const HostTables& t, uint32
 		p += 3 * kShort;
 		n -= 3 * kShort;
 	}
-	for (; n >= 8; n -= 8, p += 8) s0 = _mm_crc32_u64(s0, load64(p));
-	uint32_t r = (uint32_t)s0;
-	for (; n; --n) r = _mm_crc32_u8(r, *p++);
-	return r;
+	return raw_sse42_short((uint32_t)s0, p, n);
 }
 #endif
 
 }  // namespace
 }  // namespace fdbcrc
 
-extern "C" {
+// Dispatch once, at load time (GNU ifunc): crc32c_append binds straight to the
+// SSE4.2 or the sliced implementation, with no per-call test -- the reference
+// tests its static hw_available on every call (crc32c.cpp:344-356).
+namespace fdbcrc {
+namespace {
+int g_impl = 0;  // 1: sse4.2, 2: sliced (set by the resolver, before any constructor runs)
 
-uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length) {
-	const fdbcrc::HostTables& t = fdbcrc::tables();
 #if defined(__x86_64__)
-	if (t.sse42) return ~fdbcrc::raw_sse42(t, ~crc, input, length);
+__attribute__((target("sse4.2"))) uint32_t append_sse42(uint32_t crc, const uint8_t* input, size_t length) {
+	if (length < 64) return ~raw_sse42_short(~crc, input, length);
+	return ~raw_sse42(g_tables, ~crc, input, length);
+}
 #endif
-	return ~fdbcrc::raw_sliced(t, ~crc, input, length);
+
+uint32_t append_sliced(uint32_t crc, const uint8_t* input, size_t length) {
+	return ~raw_sliced(g_tables, ~crc, input, length);
 }
 
-const char* crc32c_host_impl(void) { return fdbcrc::tables().sse42 ? "sse4.2" : "sliced"; }
+}  // namespace
+}  // namespace fdbcrc
+
+extern "C" {
+
+typedef uint32_t (*crc32c_fn)(uint32_t, const uint8_t*, size_t);
+
+static crc32c_fn resolve_crc32c_append(void) {
+	bool sse = false;
+#if defined(__x86_64__)
+	__builtin_cpu_init();
+	sse = __builtin_cpu_supports("sse4.2");
+#endif
+	const char* force = getenv("FDB_CRC32C_FORCE_SOFTWARE");
+	if (force && *force && *force != '0') sse = false;
+	fdbcrc::g_impl = sse ? 1 : 2;
+#if defined(__x86_64__)
+	if (sse) return fdbcrc::append_sse42;
+#endif
+	return fdbcrc::append_sliced;
+}
+
+uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length) __attribute__((ifunc("resolve_crc32c_append")));
+
+const char* crc32c_host_impl(void) { return fdbcrc::g_impl == 1 ? "sse4.2" : "sliced"; }
 
 uint32_t crc32c_shift(uint32_t reg, uint64_t nbytes) { return fdbcrc::gf2_mul(reg, fdbcrc::xpow8(nbytes)); }
 

@@ -2,7 +2,8 @@
 # workloads, CPU baselines), rocprofv3 kernel-trace summaries, PMC passes and
 # the scalar drop-in benchmark on the box's host CPU.  Outputs under
 # gpurun_out/$ROUND/ (copied into profiles/$ROUND/ afterwards).
-#   gpurun -- "ROUND=round2 COMMIT=$(git rev-parse --short HEAD) bash tools/profile_round.sh"
+#   gpurun -- "STAGE=1 ROUND=round2 COMMIT=$(git rev-parse --short HEAD) bash tools/profile_round.sh"  (tests, benches)
+#   gpurun -- "STAGE=2 ..."  (rocprofv3 kernel traces and PMC passes)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -12,6 +13,7 @@ P=gpurun_out/pmc
 mkdir -p $R $P
 echo "${COMMIT:-unknown}" > $R/commit.txt
 echo "${COMMIT:-unknown}" > $P/commit.txt
+if [ "${STAGE:-1}" = 1 ]; then
 timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $R/pytest_gpu.txt 2>&1 || { tail -5 $R/pytest_gpu.txt; exit 1; }
 tail -1 $R/pytest_gpu.txt
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $R/smoke.txt 2>&1 || exit 1
@@ -22,6 +24,9 @@ done
 echo benches done
 gcc -O2 -o /tmp/bench_scalar tools/bench_scalar.c -ldl && timeout -k 10 200 /tmp/bench_scalar > $R/bench_scalar.jsonl || exit 1
 grep "model name" /proc/cpuinfo | head -1 > $R/host_cpu.txt
+for f in $R/bench_*.json; do echo "$f $(cut -c1-200 $f)"; done
+exit 0
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_pages4k -o pages4k -- python bench.py --cpu-seconds 0 > $R/prof_pages4k.log 2>&1 || exit 1
 for w in pages8k zipf chunks xxh3-pages4k xxh3-zipf sqlite-verify; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_$w -o $w -- python bench.py --workload $w --steps 20 --cpu-seconds 0 --no-verify > $R/prof_$w.log 2>&1 || exit 1
@@ -34,4 +39,3 @@ for MODE in pages4k pages8k xxh3 zipf chunks; do
   done
 done
 echo pmc done
-for f in $R/bench_*.json; do echo "$f $(cut -c1-200 $f)"; done
