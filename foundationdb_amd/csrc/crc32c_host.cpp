@@ -157,7 +157,9 @@ extern "C" {
 
 typedef uint32_t (*crc32c_fn)(uint32_t, const uint8_t*, size_t);
 
-static crc32c_fn resolve_crc32c_append(void) {
+// Runs while the dynamic linker processes relocations, before any constructor
+// (sanitizer runtimes included): kept uninstrumented.
+__attribute__((no_sanitize("address", "undefined"))) static crc32c_fn resolve_crc32c_append(void) {
 	bool sse = false;
 #if defined(__x86_64__)
 	__builtin_cpu_init();
