@@ -18,13 +18,15 @@
 //   V2: hash64 == XXH3_64bits(page + 8, 4088)
 //   other versions: false.
 //
-// Pipeline (all on the caller's stream): a classify kernel compacts the page
-// numbers that need each algorithm into device lists, the windowed page
-// kernels (crc32c_kernels.hip, xxh3_kernels.hip) checksum only those pages, a
-// compare kernel writes the status, and the rare pages left undecided get
-// lookup3 serially, one lane each.  Every page is read by the algorithm its
-// trailer/header selects and by no other (for the SQLite fall-through, a
-// page whose CRC check failed is also offered to XXH3, as in the reference).
+// Pipeline (all on the caller's stream): ONE classify pass over the
+// trailers/headers compacts the page numbers that need each algorithm into
+// device lists, the list-mode page kernels (crc32c_kernels.hip,
+// xxh3_kernels.hip) checksum only those pages, compare kernels write the
+// status and append the pages a check rejected to the next algorithm's list
+// (CRC -> XXH3 -> lookup3, the reference's order), and the lookup3 pages run
+// densely, one lane each.  Every page is read by the algorithm its
+// trailer/header selects and by no other, plus the later algorithms only
+// after a rejection.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -53,179 +55,339 @@ __device__ __forceinline__ void push(bool want, uint32_t i, uint32_t* list, unsi
 	if (want) list[base + __builtin_popcountll(m & ((1ull << lane) - 1))] = i;
 }
 
-// lookup3 hashlittle2 (flow/Hash3.c:566-700), one lane, 4-byte aligned data.
-__device__ void hashlittle2(const uint8_t* k, uint64_t length, uint32_t* pc, uint32_t* pb) {
+// lookup3 hashlittle2 (flow/Hash3.c:566-700), one lane, 16-byte aligned data:
+// four rounds (48 bytes) per step from three 16-byte loads, a quarter of the
+// load instructions of a word-by-word walk (one lane walks one page, so every
+// load touches its own cache line: the fall-through is load-issue bound, not
+// HBM bound); the last 1..48 bytes word by word, the final 1..12 with the
+// reference's tail mix (same values as its masked reads).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+__device__ void hashlittle2_a16(const uint8_t* k, uint64_t length, uint32_t* pc, uint32_t* pb) {
 	uint32_t a, b, c;
 	a = b = c = 0xdeadbeefu + (uint32_t)length + *pc;
 	c += *pb;
 #define ROT(x, r) (((x) << (r)) | ((x) >> (32 - (r))))
-	while (length > 12) {
-		a += ld32(k);
-		b += ld32(k + 4);
-		c += ld32(k + 8);
-		a -= c; a ^= ROT(c, 4);  c += b;
-		b -= a; b ^= ROT(a, 6);  a += c;
-		c -= b; c ^= ROT(b, 8);  b += a;
-		a -= c; a ^= ROT(c, 16); c += b;
-		b -= a; b ^= ROT(a, 19); a += c;
-		c -= b; c ^= ROT(b, 4);  b += a;
-		length -= 12;
-		k += 12;
+#define MIX()                                                                                                          \
+	a -= c; a ^= ROT(c, 4);  c += b;                                                                                  \
+	b -= a; b ^= ROT(a, 6);  a += c;                                                                                  \
+	c -= b; c ^= ROT(b, 8);  b += a;                                                                                  \
+	a -= c; a ^= ROT(c, 16); c += b;                                                                                  \
+	b -= a; b ^= ROT(a, 19); a += c;                                                                                  \
+	c -= b; c ^= ROT(b, 4);  b += a;
+	while (length > 48) {  // four whole rounds, and more data after them
+		const u32x4 x = *((g_u32x4*)reinterpret_cast<uintptr_t>(k));
+		const u32x4 y = *((g_u32x4*)reinterpret_cast<uintptr_t>(k + 16));
+		const u32x4 z = *((g_u32x4*)reinterpret_cast<uintptr_t>(k + 32));
+		a += x[0]; b += x[1]; c += x[2]; MIX();
+		a += x[3]; b += y[0]; c += y[1]; MIX();
+		a += y[2]; b += y[3]; c += z[0]; MIX();
+		a += z[1]; b += z[2]; c += z[3]; MIX();
+		length -= 48;
+		k += 48;
 	}
-	if (length == 0) {
-		*pc = c;
-		*pb = b;
-		return;
-	}
-	// tail of 1..12 bytes: whole words where the word is complete, bytes
-	// otherwise (same values as the reference's masked reads)
-	uint32_t w[3] = {0, 0, 0};
-	for (uint64_t i = 0; i < length; ++i) w[i >> 2] |= (uint32_t)k[i] << (8 * (i & 3));
-	a += w[0];
-	b += w[1];
-	c += w[2];
-	c ^= b; c -= ROT(b, 14);
-	a ^= c; a -= ROT(c, 11);
-	b ^= a; b -= ROT(a, 25);
-	c ^= b; c -= ROT(b, 16);
-	a ^= c; a -= ROT(c, 4);
-	b ^= a; b -= ROT(a, 14);
-	c ^= b; c -= ROT(b, 24);
+#undef MIX
 #undef ROT
-	*pc = c;
-	*pb = b;
+	uint32_t c2 = c, b2 = b;
+	// the last 1..48 bytes: the word-by-word form, continuing from (a, b, c)
+	uint32_t aa = a;
+	{
+#define ROT(x, r) (((x) << (r)) | ((x) >> (32 - (r))))
+		while (length > 12) {
+			aa += ld32(k);
+			b2 += ld32(k + 4);
+			c2 += ld32(k + 8);
+			aa -= c2; aa ^= ROT(c2, 4);  c2 += b2;
+			b2 -= aa; b2 ^= ROT(aa, 6);  aa += c2;
+			c2 -= b2; c2 ^= ROT(b2, 8);  b2 += aa;
+			aa -= c2; aa ^= ROT(c2, 16); c2 += b2;
+			b2 -= aa; b2 ^= ROT(aa, 19); aa += c2;
+			c2 -= b2; c2 ^= ROT(b2, 4);  b2 += aa;
+			length -= 12;
+			k += 12;
+		}
+		if (length == 0) {
+			*pc = c2;
+			*pb = b2;
+			return;
+		}
+		uint32_t w[3] = {0, 0, 0};
+		for (uint64_t i = 0; i < length; ++i) w[i >> 2] |= (uint32_t)k[i] << (8 * (i & 3));
+		aa += w[0];
+		b2 += w[1];
+		c2 += w[2];
+		c2 ^= b2; c2 -= ROT(b2, 14);
+		aa ^= c2; aa -= ROT(c2, 11);
+		b2 ^= aa; b2 -= ROT(aa, 25);
+		c2 ^= b2; c2 -= ROT(b2, 16);
+		aa ^= c2; aa -= ROT(c2, 4);
+		b2 ^= aa; b2 -= ROT(aa, 14);
+		c2 ^= b2; c2 -= ROT(b2, 24);
+#undef ROT
+	}
+	*pc = c2;
+	*pb = b2;
+}
+
+// ---------------------------------------------------------------------------
+// Device lists, appended per workgroup
+// ---------------------------------------------------------------------------
+// A workgroup of kCB threads handles kCB * kPer consecutive entries; each
+// list's appends collect in LDS (one LDS atomic per wave) and leave with ONE
+// global atomic per list per workgroup.  (One global counter takes ~12 ns per
+// atomic: a wave-aggregated append over 1 Mi pages -- 16 Ki atomics on one
+// word -- cost ~200 us per pass, more than the pass's reads.)
+constexpr uint32_t kCB = 1024, kPer = 4, kSpan = kCB * kPer;
+
+template <int NL>
+struct Stage {
+	uint32_t cnt[NL];
+	unsigned long long base[NL];
+	uint32_t item[NL][kSpan];
+};
+
+template <int NL>
+__device__ __forceinline__ void stage_init(Stage<NL>& S) {
+	if (threadIdx.x < NL) S.cnt[threadIdx.x] = 0;
+	__syncthreads();
+}
+
+template <int NL>
+__device__ __forceinline__ void stage_push(Stage<NL>& S, int L, bool want, uint32_t v) {
+	const uint64_t m = __ballot(want);
+	if (!m) return;
+	const int lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
+	uint32_t pos = 0;
+	if (lane == lead) pos = atomicAdd(&S.cnt[L], (uint32_t)__builtin_popcountll(m));
+	pos = (uint32_t)__shfl((int)pos, lead);
+	if (want) S.item[L][pos + __builtin_popcountll(m & ((1ull << lane) - 1))] = v;
+}
+
+template <int NL>
+__device__ __forceinline__ void stage_flush(Stage<NL>& S, uint32_t* const (&lists)[NL], unsigned long long* ctr) {
+	__syncthreads();
+	if (threadIdx.x < NL) S.base[threadIdx.x] = S.cnt[threadIdx.x] ? atomicAdd(&ctr[threadIdx.x], (unsigned long long)S.cnt[threadIdx.x]) : 0;
+	__syncthreads();
+#pragma unroll
+	for (int L = 0; L < NL; ++L)
+		for (uint32_t k = threadIdx.x; k < S.cnt[L]; k += kCB) lists[L][S.base[L] + k] = S.item[L][k];
+}
+
+// failure count: one global atomic per workgroup
+__device__ __forceinline__ void count_bad(bool bad, uint32_t* s_bad, unsigned long long* ctr_bad) {
+	const uint64_t m = __ballot(bad);
+	if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(s_bad, (uint32_t)__builtin_popcountll(m));
+	__syncthreads();
+	if (threadIdx.x == 0 && *s_bad) atomicAdd(ctr_bad, (unsigned long long)*s_bad);
 }
 
 // ---------------------------------------------------------------------------
 // SQLite
 // ---------------------------------------------------------------------------
+// ctr[0] CRC list, ctr[1] XXH3 list, ctr[2] lookup3 list, ctr[3] corrupt pages.
 constexpr uint8_t kPending = 0xFF;
+enum { L_CRC = 0, L_XXH = 1, L_L3 = 2 };
 
-__global__ void k_sq_classify(const uint8_t* __restrict__ pages, uint64_t ps, uint64_t count,
-                              uint8_t* __restrict__ status, uint32_t* __restrict__ crc_list,
-                              unsigned long long* __restrict__ ctr) {
-	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	const bool in = i < count;
-	const uint32_t part1 = in ? ld32(pages + i * ps + ps - 8) : 1u;
-	if (in) status[i] = kPending;
-	push(in && part1 == 0, (uint32_t)i, crc_list, &ctr[0]);
+// One pass over the trailers: part1 == 0 -> CRC list; else top byte zero ->
+// XXH3 list; else lookup3 list.
+__global__ __launch_bounds__(kCB) void k_sq_classify(const uint8_t* __restrict__ pages, uint64_t ps, uint64_t count,
+                                                     uint8_t* __restrict__ status, uint32_t* crc_l, uint32_t* xxh_l,
+                                                     uint32_t* l3_l, unsigned long long* __restrict__ ctr) {
+	__shared__ Stage<3> S;
+	stage_init(S);
+	const uint64_t i0 = (uint64_t)blockIdx.x * kSpan;
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; ++k) {
+		const uint64_t i = i0 + k * kCB + threadIdx.x;
+		const bool in = i < count;
+		const uint32_t part1 = in ? ld32(pages + i * ps + ps - 8) : 1u;
+		if (in) status[i] = kPending;
+		stage_push(S, L_CRC, in && part1 == 0, (uint32_t)i);
+		stage_push(S, L_XXH, in && part1 != 0 && (part1 >> 24) == 0, (uint32_t)i);
+		stage_push(S, L_L3, in && (part1 >> 24) != 0, (uint32_t)i);
+	}
+	uint32_t* const lists[3] = {crc_l, xxh_l, l3_l};
+	stage_flush(S, lists, ctr);
 }
 
-// CRC results (list order) -> status 1; then every undecided page whose part1
-// has a zero top byte goes to the XXH3 list.
-__global__ void k_sq_after_crc(const uint8_t* __restrict__ pages, uint64_t ps, const uint32_t* __restrict__ crc_list,
-                               const unsigned long long* __restrict__ ctr, const uint32_t* __restrict__ crc_out,
-                               uint8_t* __restrict__ status) {
+// CRC results -> status 1; a failed CRC page (part1 == 0, so a zero top
+// byte) is offered to XXH3 next, as the reference does (:131).
+// by_page: the results are indexed by page (page sizes other than 4 KiB run
+// the general engine over every page) instead of by list position.
+__global__ __launch_bounds__(kCB) void k_sq_after_crc(const uint8_t* __restrict__ pages, uint64_t ps,
+                                                      const uint32_t* __restrict__ crc_l, const uint32_t* __restrict__ crc_out,
+                                                      bool by_page, uint8_t* __restrict__ status, uint32_t* xxh_l,
+                                                      unsigned long long* __restrict__ ctr) {
+	const uint64_t n = ctr[L_CRC];
+	const uint64_t j0 = (uint64_t)blockIdx.x * kSpan;
+	if (j0 >= n) return;  // uniform: the whole workgroup leaves
+	__shared__ Stage<1> S;
+	stage_init(S);
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; ++k) {
+		const uint64_t j = j0 + k * kCB + threadIdx.x;
+		bool fail = false;
+		uint32_t i = 0;
+		if (j < n) {
+			i = crc_l[j];
+			const bool ok = (by_page ? crc_out[i] : crc_out[j]) == ld32(pages + i * ps + ps - 4);
+			if (ok) status[i] = 1;
+			fail = !ok;
+		}
+		stage_push(S, 0, fail, i);
+	}
+	uint32_t* const lists[1] = {xxh_l};
+	stage_flush(S, lists, ctr + L_XXH);
+}
+
+__global__ __launch_bounds__(kCB) void k_sq_after_xxh(const uint8_t* __restrict__ pages, uint64_t ps,
+                                                      const uint32_t* __restrict__ xxh_l, const uint64_t* __restrict__ xxh_out,
+                                                      uint8_t* __restrict__ status, uint32_t* l3_l,
+                                                      unsigned long long* __restrict__ ctr) {
+	const uint64_t n = ctr[L_XXH];
+	const uint64_t j0 = (uint64_t)blockIdx.x * kSpan;
+	if (j0 >= n) return;
+	__shared__ Stage<1> S;
+	stage_init(S);
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; ++k) {
+		const uint64_t j = j0 + k * kCB + threadIdx.x;
+		bool fail = false;
+		uint32_t i = 0;
+		if (j < n) {
+			i = xxh_l[j];
+			const uint64_t h = xxh_out[j];
+			const uint8_t* t = pages + i * ps + ps - 8;
+			const bool ok = ld32(t) == (uint32_t)((h >> 32) & 0x00ffffffu) && ld32(t + 4) == (uint32_t)h;
+			if (ok) status[i] = 2;
+			fail = !ok;
+		}
+		stage_push(S, 0, fail, i);
+	}
+	uint32_t* const lists[1] = {l3_l};
+	stage_flush(S, lists, ctr + L_L3);
+}
+
+// The pages no other check accepted, one per lane (dense list): hashlittle2
+// with the page number (:147-155), then the final status and the corrupt count.
+__global__ __launch_bounds__(256) void k_sq_final(const uint8_t* __restrict__ pages, uint64_t ps, uint32_t first_pgno,
+                                                  const uint32_t* __restrict__ l3_l, uint8_t* __restrict__ status,
+                                                  unsigned long long* __restrict__ ctr) {
+	const uint64_t n = ctr[L_L3];
 	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (j >= ctr[0]) return;
-	const uint64_t i = crc_list[j];
-	if (crc_out[j] == ld32(pages + i * ps + ps - 4)) status[i] = 1;
-}
-
-__global__ void k_sq_xxh_classify(const uint8_t* __restrict__ pages, uint64_t ps, uint64_t count,
-                                  const uint8_t* __restrict__ status, uint32_t* __restrict__ xxh_list,
-                                  unsigned long long* __restrict__ ctr) {
-	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	const bool in = i < count;
-	bool want = false;
-	if (in && status[i] == kPending) want = (ld32(pages + i * ps + ps - 8) >> 24) == 0;
-	push(want, (uint32_t)i, xxh_list, &ctr[1]);
-}
-
-__global__ void k_sq_after_xxh(const uint8_t* __restrict__ pages, uint64_t ps, const uint32_t* __restrict__ xxh_list,
-                               const unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ xxh_out,
-                               uint8_t* __restrict__ status) {
-	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (j >= ctr[1]) return;
-	const uint64_t i = xxh_list[j];
-	const uint64_t h = xxh_out[j];
-	const uint8_t* t = pages + i * ps + ps - 8;
-	if (ld32(t) == (uint32_t)((h >> 32) & 0x00ffffffu) && ld32(t + 4) == (uint32_t)h) status[i] = 2;
-}
-
-// Undecided pages: hashlittle2 with the page number, then the final status
-// and the corrupt-page count.
-__global__ void k_sq_final(const uint8_t* __restrict__ pages, uint64_t ps, uint64_t count, uint32_t first_pgno,
-                           uint8_t* __restrict__ status, unsigned long long* __restrict__ ctr) {
-	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= count || status[i] != kPending) return;
-	const uint8_t* p = pages + i * ps;
-	uint32_t c = first_pgno + (uint32_t)i, b = 0x5ca1ab1eu;
-	hashlittle2(p, ps - 8, &c, &b);
-	const bool ok = c == ld32(p + ps - 8) && b == ld32(p + ps - 4);
-	status[i] = ok ? 3 : 0;
-	if (!ok) atomicAdd(&ctr[2], 1ull);
+	if ((uint64_t)blockIdx.x * blockDim.x >= n) return;
+	__shared__ uint32_t s_bad;
+	if (threadIdx.x == 0) s_bad = 0;
+	__syncthreads();
+	bool bad = false;
+	if (j < n) {
+		const uint32_t i = l3_l[j];
+		const uint8_t* p = pages + (uint64_t)i * ps;
+		uint32_t c = first_pgno + i, b = 0x5ca1ab1eu;
+		hashlittle2_a16(p, ps - 8, &c, &b);  // pages are 16-byte aligned (fdb_sqlite_verify_pages contract)
+		const bool ok = c == ld32(p + ps - 8) && b == ld32(p + ps - 4);
+		status[i] = ok ? 3 : 0;
+		bad = !ok;
+	}
+	count_bad(bad, &s_bad, &ctr[3]);
 }
 
 __global__ void k_store_bad(const unsigned long long* __restrict__ ctr, uint64_t* __restrict__ d_bad) {
-	*d_bad = ctr[2];
-}
-
-// CRC results indexed by page (page sizes other than 4 KiB: all pages were checksummed)
-__global__ void k_sq_after_crc_all(const uint8_t* __restrict__ pages, uint64_t ps, uint64_t count,
-                                   const uint32_t* __restrict__ crc_all, uint8_t* __restrict__ status) {
-	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= count) return;
-	const uint8_t* t = pages + i * ps + ps - 8;
-	if (ld32(t) == 0 && crc_all[i] == ld32(t + 4)) status[i] = 1;
+	*d_bad = ctr[3];
 }
 
 // ---------------------------------------------------------------------------
 // DiskQueue (4096-byte pages)
 // ---------------------------------------------------------------------------
-__global__ void k_dq_classify(const uint8_t* __restrict__ pages, uint64_t count, uint8_t* __restrict__ ok,
-                              uint32_t* __restrict__ v1_list, uint32_t* __restrict__ v2_list,
-                              unsigned long long* __restrict__ ctr) {
-	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	const bool in = i < count;
-	const uint32_t ver = in ? (ld32(pages + i * 4096 + 8) >> 16) : 0xFFFFu;  // implementationVersion, bytes 10..11
-	if (in) ok[i] = ver == 0 ? kPending : 0;
-	push(ver == 1, (uint32_t)i, v1_list, &ctr[0]);
-	push(ver == 2, (uint32_t)i, v2_list, &ctr[1]);
+// ctr[0] V1 list, ctr[1] V2 list, ctr[2] V0 (lookup3) list, ctr[3] failures.
+__global__ __launch_bounds__(kCB) void k_dq_classify(const uint8_t* __restrict__ pages, uint64_t count,
+                                                     uint8_t* __restrict__ ok, uint32_t* v1_l, uint32_t* v2_l,
+                                                     uint32_t* v0_l, unsigned long long* __restrict__ ctr) {
+	__shared__ Stage<3> S;
+	__shared__ uint32_t s_bad;
+	if (threadIdx.x == 0) s_bad = 0;
+	stage_init(S);
+	const uint64_t i0 = (uint64_t)blockIdx.x * kSpan;
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; ++k) {
+		const uint64_t i = i0 + k * kCB + threadIdx.x;
+		const bool in = i < count;
+		const uint32_t ver = in ? (ld32(pages + i * 4096 + 8) >> 16) : 0xFFFFu;  // implementationVersion, bytes 10..11
+		if (in) ok[i] = ver <= 2 ? kPending : 0;
+		stage_push(S, 0, in && ver == 1, (uint32_t)i);
+		stage_push(S, 1, in && ver == 2, (uint32_t)i);
+		stage_push(S, 2, in && ver == 0, (uint32_t)i);
+		const uint64_t m = __ballot(in && ver > 2);  // unknown versions fail (:1119)
+		if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(&s_bad, (uint32_t)__builtin_popcountll(m));
+	}
+	uint32_t* const lists[3] = {v1_l, v2_l, v0_l};
+	stage_flush(S, lists, ctr);
+	if (threadIdx.x == 0 && s_bad) atomicAdd(&ctr[3], (unsigned long long)s_bad);
 }
 
-__global__ void k_dq_compare(const uint8_t* __restrict__ pages, const uint32_t* __restrict__ v1_list,
-                             const uint32_t* __restrict__ v2_list, const unsigned long long* __restrict__ ctr,
-                             const uint32_t* __restrict__ crc_out, const uint64_t* __restrict__ xxh_out,
-                             uint8_t* __restrict__ ok) {
+__global__ __launch_bounds__(256) void k_dq_compare(const uint8_t* __restrict__ pages, const uint32_t* __restrict__ v1_l,
+                                                    const uint32_t* __restrict__ v2_l, const unsigned long long* __restrict__ ctr,
+                                                    const uint32_t* __restrict__ crc_out, const uint64_t* __restrict__ xxh_out,
+                                                    uint8_t* __restrict__ ok, unsigned long long* __restrict__ ctr_bad) {
 	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (j < ctr[0]) {
-		const uint64_t i = v1_list[j];
-		ok[i] = crc_out[j] == ld32(pages + i * 4096) ? 1 : 0;
+	const uint64_t n1 = ctr[0], n2 = ctr[1];
+	if ((uint64_t)blockIdx.x * blockDim.x >= (n1 > n2 ? n1 : n2)) return;
+	__shared__ uint32_t s_bad;
+	if (threadIdx.x == 0) s_bad = 0;
+	__syncthreads();
+	bool bad = false;
+	if (j < n1) {
+		const uint64_t i = v1_l[j];
+		const bool g = crc_out[j] == ld32(pages + i * 4096);
+		ok[i] = g ? 1 : 0;
+		bad = !g;
 	}
-	if (j < ctr[1]) {
-		const uint64_t i = v2_list[j];
-		ok[i] = xxh_out[j] == ld64(pages + i * 4096) ? 1 : 0;
+	const uint64_t m = __ballot(bad);
+	if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(&s_bad, (uint32_t)__builtin_popcountll(m));
+	bad = false;
+	if (j < n2) {
+		const uint64_t i = v2_l[j];
+		const bool g = xxh_out[j] == ld64(pages + i * 4096);
+		ok[i] = g ? 1 : 0;
+		bad = !g;
 	}
+	count_bad(bad, &s_bad, ctr_bad);
 }
 
-__global__ void k_dq_final(const uint8_t* __restrict__ pages, uint64_t count, uint8_t* __restrict__ ok,
-                           unsigned long long* __restrict__ ctr) {
-	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= count) return;
-	const uint8_t* p = pages + i * 4096;
-	bool good = ok[i] == 1;
-	if (ok[i] == kPending) {  // V0: hashlittle2 over [16, 4096) -> UID(c << 32 | b, 0xFDB)
+// V0 pages: hashlittle2 over [16, 4096) -> UID(c << 32 | b, 0xFDB)
+__global__ __launch_bounds__(256) void k_dq_final(const uint8_t* __restrict__ pages, const uint32_t* __restrict__ v0_l,
+                                                  uint8_t* __restrict__ ok, unsigned long long* __restrict__ ctr) {
+	const uint64_t n = ctr[2];
+	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if ((uint64_t)blockIdx.x * blockDim.x >= n) return;
+	__shared__ uint32_t s_bad;
+	if (threadIdx.x == 0) s_bad = 0;
+	__syncthreads();
+	bool bad = false;
+	if (j < n) {
+		const uint64_t i = v0_l[j];
+		const uint8_t* p = pages + i * 4096;
 		uint32_t c = 0x12345678u, b = 0xbeefabcdu;
-		hashlittle2(p + 16, 4080, &c, &b);
-		good = ld64(p) == (((uint64_t)c << 32) | b) && ld64(p + 8) == 0xFDBull;
+		hashlittle2_a16(p + 16, 4080, &c, &b);
+		const bool good = ld64(p) == (((uint64_t)c << 32) | b) && ld64(p + 8) == 0xFDBull;
 		ok[i] = good ? 1 : 0;
+		bad = !good;
 	}
-	if (!good) atomicAdd(&ctr[2], 1ull);
+	count_bad(bad, &s_bad, &ctr[3]);
 }
 
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 uint64_t workspace_bytes(uint64_t count) {
-	// counters, two u32 lists, u32 CRC results, u64 XXH3 results, and the
+	// counters, three u32 lists, u32 CRC results, u64 XXH3 results, and the
 	// general engine's workspace (page sizes other than 4 KiB)
-	return 64 + 4 * count + 4 * count + 4 * count + 8 * count + 64 + fdbcrc::varlen7_workspace_bytes(count, 0) + 16;
+	return 64 + 8 * count + 4 * count * 4 + 64 + fdbcrc::varlen7_workspace_bytes(count, 0) + 16;
 }
 
 struct Ws {
 	unsigned long long* ctr;
-	uint32_t *list_a, *list_b, *crc_out;
+	uint32_t *list_a, *list_b, *list_c, *crc_out;
 	uint64_t* xxh_out;
 	void* eng;
 };
@@ -240,32 +402,33 @@ static Ws carve(void* ws, uint64_t count) {
 	p += 4 * count;
 	w.list_b = reinterpret_cast<uint32_t*>(p);
 	p += 4 * count;
+	w.list_c = reinterpret_cast<uint32_t*>(p);
+	p += 4 * count;
 	w.crc_out = reinterpret_cast<uint32_t*>(p);
 	p += 4 * count;
 	w.eng = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
 	return w;
 }
 
-static unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
+static unsigned blocks(uint64_t n, uint64_t per = 256) { return (unsigned)((n + per - 1) / per); }
 
 int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t first_pgno, uint8_t* status,
                   uint64_t* d_bad, const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s) {
 	const Ws w = carve(ws, count);
 	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
-	k_sq_classify<<<blocks(count), 256, 0, s>>>(pages, ps, count, status, w.list_a, w.ctr);
-	const uint64_t* n_crc = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
-	const uint64_t* n_xxh = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
+	k_sq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, count, status, w.list_a, w.list_b, w.list_c, w.ctr);
+	const uint64_t* n_crc = reinterpret_cast<const uint64_t*>(&w.ctr[L_CRC]);
+	const uint64_t* n_xxh = reinterpret_cast<const uint64_t*>(&w.ctr[L_XXH]);
 	if (ps == 4096) {
 		if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n_crc, count, 0, 8, 0xFDBEEFDBu, w.crc_out, tabs,
 		                                     num_cus, s))
 			return -1;
-		k_sq_after_crc<<<blocks(count), 256, 0, s>>>(pages, ps, w.list_a, w.ctr, w.crc_out, status);
+		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, false, status, w.list_b, w.ctr);
 	} else {
 		// other page sizes: every page through the general fixed-stride engine
 		fdbcrc::launch_fixed_general(pages, ps, ps - 8, count, 0xFDBEEFDBu, nullptr, w.crc_out, tabs, num_cus, w.eng, s);
-		k_sq_after_crc_all<<<blocks(count), 256, 0, s>>>(pages, ps, count, w.crc_out, status);
+		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, true, status, w.list_b, w.ctr);
 	}
-	k_sq_xxh_classify<<<blocks(count), 256, 0, s>>>(pages, ps, count, status, w.list_b, w.ctr);
 	fdbxxh::XxhParams P{};
 	P.base = pages;
 	P.stride = ps;
@@ -275,8 +438,8 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 	P.idx = w.list_b;
 	P.d_count = n_xxh;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_sq_after_xxh<<<blocks(count), 256, 0, s>>>(pages, ps, w.list_b, w.ctr, w.xxh_out, status);
-	k_sq_final<<<blocks(count), 256, 0, s>>>(pages, ps, count, first_pgno, status, w.ctr);
+	k_sq_after_xxh<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_b, w.xxh_out, status, w.list_c, w.ctr);
+	k_sq_final<<<blocks(count), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, w.ctr);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
 	return 0;
 }
@@ -285,7 +448,7 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
                     const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s) {
 	const Ws w = carve(ws, count);
 	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
-	k_dq_classify<<<blocks(count), 256, 0, s>>>(pages, count, ok, w.list_a, w.list_b, w.ctr);
+	k_dq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, ok, w.list_a, w.list_b, w.list_c, w.ctr);
 	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
 	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
 	// V1: crc32c(0xfdbeefdb, bytes [4, 4096))
@@ -301,8 +464,8 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	P.idx = w.list_b;
 	P.d_count = n2;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_dq_compare<<<blocks(count), 256, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok);
-	k_dq_final<<<blocks(count), 256, 0, s>>>(pages, count, ok, w.ctr);
+	k_dq_compare<<<blocks(count), 256, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok, &w.ctr[3]);
+	k_dq_final<<<blocks(count), 256, 0, s>>>(pages, w.list_c, ok, w.ctr);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
 	return 0;
 }
