@@ -818,12 +818,15 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 // ---------------------------------------------------------------------------
 // v8 (experiment, -DFDBCRC_VARLEN=8): the same window slots, streamed like the page kernel
 // ---------------------------------------------------------------------------
-// Status: bit-exact (the full -m gpu suite passes with it), but slower than v7
-// on every shape measured (chunks 0.250 vs 0.230 ms, zipf 0.483 vs 0.299 ms,
-// 4 KiB buffers 0.380 vs 0.233 ms): the scalar cursor and the per-window
-// records sit between a unit's compute and the next unit's loads, and 118
-// SGPRs spill.  Kept for the next iteration (lane-parallel walk ahead of the
-// loads), not built by default.
+// Status: bit-exact (the full -m gpu suite passes with it), but not faster
+// than v7: 1 MiB buffers (almost all PLAIN units, the page kernel's loop)
+// 0.222 vs 0.213 ms, chunks 0.235 vs 0.216 ms, zipf 0.438 vs 0.296 ms, 4 KiB
+// buffers 0.354 vs 0.225 ms.  Scalar metadata loads removed the vmcnt(0)
+// drains that vector metadata loads caused (174 -> 15), yet the plain path
+// stays at v7's ~4.9 TB/s while the page kernel reads the same 1 GiB at
+// ~6 TB/s: hipcc still waits for half of the next unit's loads before each
+// compute (vmcnt(4) where vmcnt(8) would do).  Kept for the next iteration,
+// not built by default.
 // v7 keeps a 64-slot table per wave in vector registers (155 VGPRs: 12 waves
 // per CU, one 4 KiB pass in flight per wave) and runs at ~5 TB/s even on
 // large buffers.  v8 moves the control to the scalar unit so the streaming
@@ -916,61 +919,39 @@ __global__ __launch_bounds__(kV8Threads) void k_varlen8(const V7Params P_) {
 	}
 	const uint64_t j_first = j;
 
-	// ---- metadata batches: lane l of batch slot (kb & 1) holds buffer 64*kb + l ----
-	uint64_t b_off0 = 0, b_len0 = 0, b_off1 = 0, b_len1 = 0;
-	uint32_t b_s0 = 0, b_s1 = 0;
-	auto fetch = [&](uint64_t kbn, uint64_t& off, uint64_t& len, uint32_t& sd) __attribute__((always_inline)) {
-		const uint64_t i = kbn * 64 + (uint64_t)lane;
-		const uint64_t ic = i < count ? i : count - 1;
-		off = offsets ? gld64(&offsets[ic]) : ic * stride;
-		len = lengths ? gld64(&lengths[ic]) : length;
-		sd = ~(seeds ? gld32(&seeds[ic]) : seed);
-	};
-	uint64_t kb = j >> 6;
-	if (kb & 1) {
-		fetch(kb, b_off1, b_len1, b_s1);
-		fetch(kb + 1, b_off0, b_len0, b_s0);
-	} else {
-		fetch(kb, b_off0, b_len0, b_s0);
-		fetch(kb + 1, b_off1, b_len1, b_s1);
-	}
-
 	// ---- cursor (uniform) ----
+	// The cursor reads a buffer's offset/length/seed with SCALAR loads: the only
+	// vector loads in the streaming loop are the data loads, so the compiler's
+	// wait counting stays exact (vector metadata loads made it drain every load
+	// in flight -- vmcnt(0) -- at each use).
+	typedef __attribute__((address_space(4))) const uint64_t c_u64;
+	typedef __attribute__((address_space(4))) const uint32_t c_u32;
 	uint32_t W = 0, lo = 0, k0 = 0, zt = 0, s0 = 0;
 	uint64_t wb = 0, m = 0;
 	uint64_t rem = nslot;  // slots left to walk
-	auto enter = [&]() __attribute__((always_inline)) {   // geometry of buffer j; buffers without windows are skipped
+	auto enter = [&]() __attribute__((always_inline)) {  // geometry of buffer j; buffers without windows are skipped
 		for (;;) {
 			if (j >= count) {
 				W = 0;
 				return;
 			}
-			if ((j >> 6) != kb) {  // the next batch: the slot just left gets batch kb + 2
-				++kb;
-				if (kb & 1)
-					fetch(kb + 1, b_off0, b_len0, b_s0);
-				else
-					fetch(kb + 1, b_off1, b_len1, b_s1);
-			}
-			const int l = (int)(j & 63);
-			const bool odd = kb & 1;
-			const uint64_t off = odd ? rdlane64(b_off1, l) : rdlane64(b_off0, l);
-			const uint64_t len = odd ? rdlane64(b_len1, l) : rdlane64(b_len0, l);
+			const uint64_t off = offsets ? *((c_u64*)reinterpret_cast<uintptr_t>(offsets + j)) : j * stride;
+			const uint64_t len = lengths ? *((c_u64*)reinterpret_cast<uintptr_t>(lengths + j)) : length;
 			const Geo7 g = geo7(base + off, len);
-			if (rdfirst(g.W)) {
-				W = rdfirst(g.W);
-				lo = rdfirst(g.lo);
-				k0 = rdfirst(g.k0);
-				zt = rdfirst(g.zt);
-				wb = rdfirst64(g.A - g.lo);
-				s0 = rdfirst(odd ? rdlane(b_s1, l) : rdlane(b_s0, l));
+			if (g.W) {
+				W = g.W;
+				lo = g.lo;
+				k0 = g.k0;
+				zt = g.zt;
+				wb = g.A - g.lo;
+				s0 = ~(seeds ? *((c_u32*)reinterpret_cast<uintptr_t>(seeds + j)) : seed);
 				return;
 			}
-			j = rdfirst64(j + 1);
+			++j;
 		}
 	};
 	enter();
-	m = lo_s - rdfirst(gld32(&gs[j]));
+	m = lo_s - *((c_u32*)reinterpret_cast<uintptr_t>(gs + j));
 	// empty slots (past the range's end) load the last chunk of the range's first
 	// window, which always holds bytes of its buffer (windows end at E)
 	const uint64_t safe_wa = wb + 1024 * m;
@@ -1153,7 +1134,11 @@ __global__ __launch_bounds__(kV8Threads) void k_varlen8(const V7Params P_) {
 		if (plain) {  // two whole 4 KiB blocks of the open part
 			const uint32_t B0 = rdlane(R0, 0) ^ rdlane(R0, 16) ^ rdlane(R0, 32) ^ rdlane(R0, 48);
 			const uint32_t B1 = rdlane(R1, 0) ^ rdlane(R1, 16) ^ rdlane(R1, 32) ^ rdlane(R1, 48);
+#ifdef FDBCRC_V8_NOUMUL  // timing experiment only: wrong results
+			acc ^= B0 ^ B1;
+#else
 			acc = umul(T->block, umul(T->block, acc) ^ B0) ^ B1;
+#endif
 			return;
 		}
 		combine_pass(R0, q0);
@@ -1161,14 +1146,21 @@ __global__ __launch_bounds__(kV8Threads) void k_varlen8(const V7Params P_) {
 	};
 
 	const uint64_t nunit = (nslot + 7) >> 3;
+	// The explicit waits (vmcnt(8): the other unit's eight loads stay in flight)
+	// pin the wait-count state for the compiler, which otherwise drains half of
+	// the next unit's loads before every compute (the paths inside load_unit and
+	// the output flushes make its own count conservative).  A unit past the
+	// range's end has only empty slots: computing it is harmless.
 	for (uint64_t un = 0; un < nunit; un += 2) {
 		load_unit(u1, 8, plainB);
 		__builtin_amdgcn_sched_barrier(0);
+		__builtin_amdgcn_s_waitcnt(0x0F78);
 		compute_unit(u0, 0, plainA);
 		__builtin_amdgcn_sched_barrier(0);
 		load_unit(u0, 0, plainA);
 		__builtin_amdgcn_sched_barrier(0);
-		if (un + 1 < nunit) compute_unit(u1, 8, plainB);
+		__builtin_amdgcn_s_waitcnt(0x0F78);
+		compute_unit(u1, 8, plainB);
 		__builtin_amdgcn_sched_barrier(0);
 	}
 	if (nfin) flush();

@@ -1,9 +1,4 @@
 # development: one GPU step
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r2h
-timeout -k 10 300 python -u -m pytest tests/test_pagecheck.py tests/test_write_checker.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r2h/pytest_gpu.txt 2>&1; rc=$?
-tail -12 gpurun_out/r2h/pytest_gpu.txt | grep -E "PASS|FAIL|Error|passed|failed"
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python bench.py --workload sqlite-verify --steps 20 --cpu-seconds 0 > gpurun_out/r2h/bench_sqlite-verify.json || exit 1
-cut -c1-400 gpurun_out/r2h/bench_sqlite-verify.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r2h/prof -o sq -- python bench.py --workload sqlite-verify --steps 10 --cpu-seconds 0 --no-verify > gpurun_out/r2h/prof.log 2>&1 || exit 1
+for L in libfdb_crc32c libfdb_crc32c_v8; do echo "== $L"; FDBCRC_LIB=$PWD/foundationdb_amd/lib/$L.so timeout -k 10 120 python tools/probe_varlen.py "1 MiB" 16384 4096 zipf chunks 2>&1 | grep -v amdgpu.ids || exit 1; done
+FDBCRC_LIB=$PWD/foundationdb_amd/lib/libfdb_crc32c_v8.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread 2>&1 | tail -2

@@ -36,6 +36,7 @@ def run(name, lengths, align=256, reps=10):
           f"{lengths.sum() / ms / 1e6:8.1f} GB/s  {lengths.size / ms / 1e3:8.1f} Mbuf/s")
 
 
+run("1 MiB x 1024", [1 << 20] * 1024, 4096)
 run("4096 x 256K aligned", [4096] * (1 << 18), 4096)
 run("16384 x 64K", [16384] * (1 << 16), 4096)
 run("1024 x 1M", [1024] * (1 << 20), 1024)
