@@ -458,6 +458,51 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
 	return xxh3_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
 }
 
+uint64_t xxh3_gpu_chained_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes) {
+	DeviceState* st = nullptr;
+	if (device_state(&st)) return 0;
+	return fdbxxh::xxh3_chain_workspace_bytes(nsegs, nchains, total_bytes, fdbxxh::xxh3_nwave(st->num_cus));
+}
+
+int xxh3_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                              uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint64_t total_bytes,
+                              uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
+                              uint64_t workspace_bytes, void* stream) {
+	if (nchains == 0) return 0;
+	if (!d_out || !d_chain_starts || (nsegs && (!d_base || !d_seg_offsets || !d_seg_lengths)))
+		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_chained: null pointer");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	const uint64_t need = fdbxxh::xxh3_chain_workspace_bytes(nsegs, nchains, total_bytes, fdbxxh::xxh3_nwave(st->num_cus));
+	if (!d_workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_chained: workspace too small or misaligned");
+	if (fdbxxh::launch_xxh3_chained(static_cast<const uint8_t*>(d_base), d_seg_offsets, d_seg_lengths, nsegs,
+	                                d_chain_starts, nchains, total_bytes, seed, d_seeds, d_out, st->num_cus, d_workspace,
+	                                reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "xxh3_gpu_batch_chained: launch setup failed");
+	return check_launch("xxh3_gpu_batch_chained launch");
+}
+
+int xxh3_gpu_batch_chained(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                           uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint64_t total_bytes,
+                           uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
+	if (nchains == 0) return 0;
+	if (!d_out || !d_chain_starts || (nsegs && (!d_base || !d_seg_offsets || !d_seg_lengths)))
+		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_chained: null pointer");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
+	                              fdbxxh::xxh3_chain_workspace_bytes(nsegs, nchains, total_bytes,
+	                                                                 fdbxxh::xxh3_nwave(st->num_cus)),
+	                              &ws, &have, &hold))
+		return rc;
+	return xxh3_gpu_batch_chained_ws(d_base, d_seg_offsets, d_seg_lengths, nsegs, d_chain_starts, nchains, total_bytes,
+	                                 seed, d_seeds, d_out, ws, have, stream);
+}
+
 // ---- page verifiers (include/fdb_pagecheck.h) ---------------------------------
 
 uint64_t fdb_pagecheck_workspace_bytes(uint64_t count) { return fdbpc::workspace_bytes(count); }

@@ -1,0 +1,186 @@
+// One XXH3-64 per CHAIN of non-contiguous segments: a packet laid out over a
+// PacketBuffer chain (fdbrpc/FlowTransport.cpp:2025-2068: XXH3_64bits over one
+// buffer, or XXH3_64bits_reset/_update per buffer/_digest when the packet
+// spans several).  XXH3's stripes and its per-block scramble are sequential
+// over the message, so unlike CRC-32C (crc32c_chain.hip) the segment digests
+// cannot be combined: the segments are gathered, in order, into one staging
+// area on the device and the varlen engine hashes each chain's contiguous
+// range there.
+//
+//   k_seg_bsum / k_seg_bscan / k_seg_scan   exclusive prefix of the segment
+//                                           lengths (staging offsets)
+//   k_seg_gather                            one workgroup per segment copies
+//                                           it to its staging offset
+//   k_chain_ranges                          chain c = staging range
+//                                           [pre[starts[c]], pre[starts[c+1]])
+//   launch_xxh3                             the varlen engine over the ranges
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xxh3_device.h"
+
+namespace fdbxxh {
+
+constexpr unsigned kScanT = 1024, kScanPer = 4, kScanSpan = kScanT * kScanPer;
+
+__device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s_w) {
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+	if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+	__syncthreads();
+	uint64_t t = 0;
+	for (unsigned k = 0; k < blockDim.x / 64; ++k) t += s_w[k];
+	__syncthreads();
+	return t;
+}
+
+__global__ __launch_bounds__(kScanT) void k_seg_bsum(const uint64_t* __restrict__ len, uint64_t n,
+                                                     uint64_t* __restrict__ bsum) {
+	__shared__ uint64_t s_w[kScanT / 64];
+	uint64_t v = 0;
+	for (unsigned k = 0; k < kScanPer; ++k) {
+		const uint64_t i = (uint64_t)blockIdx.x * kScanSpan + k * kScanT + threadIdx.x;
+		v += i < n ? len[i] : 0;
+	}
+	const uint64_t t = block_sum(v, s_w);
+	if (threadIdx.x == 0) bsum[blockIdx.x] = t;
+}
+
+// exclusive scan of the block sums in place (one workgroup, any count)
+__global__ __launch_bounds__(kScanT) void k_seg_bscan(uint64_t* __restrict__ bsum, uint64_t nb) {
+	__shared__ uint64_t s_w[kScanT / 64];
+	__shared__ uint64_t s_carry;
+	if (threadIdx.x == 0) s_carry = 0;
+	__syncthreads();
+	const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	for (uint64_t c0 = 0; c0 < nb; c0 += kScanT) {
+		const uint64_t i = c0 + threadIdx.x;
+		const uint64_t v = i < nb ? bsum[i] : 0;
+		uint64_t inc = v;
+		for (int d = 1; d < 64; d <<= 1) {
+			const uint64_t y = __shfl_up(inc, d);
+			if (lane >= d) inc += y;
+		}
+		if (lane == 63) s_w[w] = inc;
+		__syncthreads();
+		uint64_t wb = 0, tot = 0;
+		for (int k = 0; k < (int)(kScanT / 64); ++k) {
+			wb += k < w ? s_w[k] : 0;
+			tot += s_w[k];
+		}
+		const uint64_t carry = s_carry;
+		if (i < nb) bsum[i] = carry + wb + inc - v;
+		__syncthreads();
+		if (threadIdx.x == 0) s_carry = carry + tot;
+		__syncthreads();
+	}
+}
+
+// pre[i] = exclusive prefix of len; pre[n] = total
+__global__ __launch_bounds__(kScanT) void k_seg_scan(const uint64_t* __restrict__ len, uint64_t n,
+                                                     const uint64_t* __restrict__ bsum, uint64_t* __restrict__ pre) {
+	__shared__ uint64_t s_w[kScanT / 64];
+	const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	const uint64_t i0 = (uint64_t)blockIdx.x * kScanSpan + (uint64_t)threadIdx.x * kScanPer;  // 4 consecutive per thread
+	uint64_t v[kScanPer], run = 0;
+	for (unsigned k = 0; k < kScanPer; ++k) {
+		v[k] = i0 + k < n ? len[i0 + k] : 0;
+		run += v[k];
+	}
+	uint64_t inc = run;
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint64_t y = __shfl_up(inc, d);
+		if (lane >= d) inc += y;
+	}
+	if (lane == 63) s_w[w] = inc;
+	__syncthreads();
+	uint64_t wb = 0;
+	for (int k = 0; k < w; ++k) wb += s_w[k];
+	uint64_t x = bsum[blockIdx.x] + wb + inc - run;
+	for (unsigned k = 0; k < kScanPer; ++k) {
+		if (i0 + k <= n) pre[i0 + k] = x;  // i0 + k == n writes the total
+		x += v[k];
+	}
+}
+
+// Segment j -> staging[pre[j], pre[j] + len[j]).  Bytes past `cap` are
+// dropped (the caller's total_bytes bound was wrong: results undefined, but no
+// write leaves the staging area).
+__global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                    const uint64_t* __restrict__ len, const uint64_t* __restrict__ pre,
+                                                    uint64_t nsegs, uint8_t* __restrict__ staging, uint64_t cap) {
+	for (uint64_t j = blockIdx.x; j < nsegs; j += gridDim.x) {
+		const uint8_t* src = base + off[j];
+		const uint64_t n = len[j], d = pre[j];
+		uint8_t* dst = staging + d;
+		const uint64_t lim = d >= cap ? 0 : (cap - d < n ? cap - d : n);
+		// 4-byte words where source and destination agree mod 4, bytes otherwise
+		const uint64_t mis = (reinterpret_cast<uintptr_t>(src) ^ reinterpret_cast<uintptr_t>(dst)) & 3;
+		uint64_t head = mis ? lim : (4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3;
+		if (head > lim) head = lim;
+		for (uint64_t k = threadIdx.x; k < head; k += blockDim.x) dst[k] = src[k];
+		if (!mis) {
+			const uint64_t nw = (lim - head) / 4;
+			const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src + head);
+			uint32_t* d4 = reinterpret_cast<uint32_t*>(dst + head);
+			for (uint64_t k = threadIdx.x; k < nw; k += blockDim.x) d4[k] = s4[k];
+			for (uint64_t k = head + 4 * nw + threadIdx.x; k < lim; k += blockDim.x) dst[k] = src[k];
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void k_chain_ranges(const uint64_t* __restrict__ starts, uint64_t nchains,
+                                                      const uint64_t* __restrict__ pre, uint64_t* __restrict__ ch_off,
+                                                      uint64_t* __restrict__ ch_len) {
+	const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (c >= nchains) return;
+	const uint64_t a = pre[starts[c]], b = pre[starts[c + 1]];
+	ch_off[c] = a;
+	ch_len[c] = b - a;
+}
+
+static uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
+
+uint64_t xxh3_chain_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes, uint64_t nwave) {
+	const uint64_t nb = nsegs / kScanSpan + 1;  // the scan covers nsegs + 1 entries (pre[nsegs] = total)
+	return al16(8 * (nb + 1)) + al16(8 * (nsegs + 1)) + 2 * al16(8 * nchains) + al16(total_bytes + 16) +
+	       al16(xxh3_workspace_bytes(nchains ? nchains : 1, nwave));
+}
+
+int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint64_t* seg_len, uint64_t nsegs,
+                        const uint64_t* starts, uint64_t nchains, uint64_t total_bytes, uint64_t seed,
+                        const uint64_t* seeds, uint64_t* out, int num_cus, void* ws, hipStream_t s) {
+	const uint64_t nb = nsegs / kScanSpan + 1;
+	uint8_t* p = static_cast<uint8_t*>(ws);
+	uint64_t* bsum = reinterpret_cast<uint64_t*>(p);
+	p += al16(8 * (nb + 1));
+	uint64_t* pre = reinterpret_cast<uint64_t*>(p);
+	p += al16(8 * (nsegs + 1));
+	uint64_t* ch_off = reinterpret_cast<uint64_t*>(p);
+	p += al16(8 * nchains);
+	uint64_t* ch_len = reinterpret_cast<uint64_t*>(p);
+	p += al16(8 * nchains);
+	uint8_t* staging = p;
+	p += al16(total_bytes + 16);
+	void* eng = p;
+	if (nsegs) {
+		k_seg_bsum<<<(unsigned)nb, kScanT, 0, s>>>(seg_len, nsegs, bsum);
+		k_seg_bscan<<<1, kScanT, 0, s>>>(bsum, nb);
+		k_seg_scan<<<(unsigned)nb, kScanT, 0, s>>>(seg_len, nsegs, bsum, pre);
+		const uint64_t g = nsegs < 65536 ? nsegs : 65536;
+		k_seg_gather<<<(unsigned)g, 256, 0, s>>>(base, seg_off, seg_len, pre, nsegs, staging, total_bytes);
+	} else if (hipMemsetAsync(pre, 0, 8, s) != hipSuccess) {
+		return -1;
+	}
+	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, pre, ch_off, ch_len);
+	XxhParams P{};
+	P.base = staging;
+	P.offsets = ch_off;
+	P.lengths = ch_len;
+	P.count = nchains;
+	P.seed = seed;
+	P.seeds = seeds;
+	P.out = out;
+	return launch_xxh3(P, num_cus, eng, s);
+}
+
+}  // namespace fdbxxh

@@ -28,6 +28,8 @@ def _lib():
         L.xxh3_gpu_varlen_workspace_bytes.argtypes = [u64]
         L.xxh3_gpu_batch_varlen_ws.restype = ctypes.c_int
         L.xxh3_gpu_batch_varlen_ws.argtypes = [vp, vp, vp, u64, u64, vp, vp, vp, u64, vp]
+        L.xxh3_gpu_batch_chained.restype = ctypes.c_int
+        L.xxh3_gpu_batch_chained.argtypes = [vp, vp, vp, u64, vp, u64, u64, u64, vp, vp, vp]
         _bound = True
     return L
 
@@ -83,4 +85,34 @@ def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=Non
                                                  _vp(seeds), _vp(out), _vp(workspace),
                                                  workspace.numel() * workspace.element_size(), _stream_handle(stream))
     _check(rc, "xxh3_gpu_batch_varlen")
+    return out
+
+
+def batch_chained(buf, seg_offsets, seg_lengths, chain_starts, total_bytes=None, seed=0, seeds=None, out=None,
+                  stream=None):
+    """XXH3-64 of each chain of segments (xxh3_gpu_batch_chained): chain c is the
+    concatenation of segments [chain_starts[c], chain_starts[c+1]) -- a packet
+    over a PacketBuffer chain (fdbrpc/FlowTransport.cpp:2025-2068).
+    `total_bytes` bounds the sum of the segment lengths (default: computed,
+    which synchronises the stream once)."""
+    _require_device(buf, "buf")
+    _require_device(seg_offsets, "seg_offsets", buf.device, I64)
+    _require_device(seg_lengths, "seg_lengths", buf.device, I64)
+    _require_device(chain_starts, "chain_starts", buf.device, I64)
+    nsegs = seg_offsets.numel()
+    if seg_lengths.numel() != nsegs:
+        raise CRC32CError("seg_offsets and seg_lengths differ in size")
+    nchains = max(chain_starts.numel() - 1, 0)
+    if total_bytes is None:
+        total_bytes = int(seg_lengths.sum().item()) if nsegs else 0
+    if out is None:
+        out = torch.empty(nchains, dtype=torch.uint64, device=buf.device)
+    _require_device(out, "out", buf.device, U64, nchains)
+    if seeds is not None:
+        _require_device(seeds, "seeds", buf.device, U64, nchains)
+    with torch.cuda.device(buf.device):
+        rc = _lib().xxh3_gpu_batch_chained(_vp(buf), _vp(seg_offsets), _vp(seg_lengths), nsegs, _vp(chain_starts),
+                                           nchains, int(total_bytes), seed & 0xFFFFFFFFFFFFFFFF, _vp(seeds), _vp(out),
+                                           _stream_handle(stream))
+    _check(rc, "xxh3_gpu_batch_chained")
     return out

@@ -47,6 +47,25 @@ int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, cons
                              uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
                              uint64_t workspace_bytes, void* stream);
 
+/* Chains: d_out[c] = XXH3_64bits_withSeed(concatenation of segments
+ * [d_chain_starts[c], d_chain_starts[c+1]), d_seeds ? d_seeds[c] : seed) --
+ * a packet spread over a PacketBuffer chain, which FlowTransport hashes with
+ * XXH3_64bits_reset / _update per buffer / _digest
+ * (fdbrpc/FlowTransport.cpp:2025-2068).  Segment j is the d_seg_lengths[j]
+ * bytes at d_base + d_seg_offsets[j]; d_chain_starts holds nchains + 1
+ * non-decreasing values <= nsegs.  The segments are gathered on the device
+ * into a staging area of `total_bytes` (the caller's bound on the sum of the
+ * segment lengths: a smaller bound leaves the digests undefined, never writes
+ * outside the workspace), then hashed per chain. */
+int xxh3_gpu_batch_chained(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                           uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint64_t total_bytes,
+                           uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* stream);
+uint64_t xxh3_gpu_chained_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes);
+int xxh3_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                              uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint64_t total_bytes,
+                              uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
+                              uint64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

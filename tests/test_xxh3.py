@@ -183,3 +183,43 @@ def test_gpu_empty_and_workspace(cuda):
     ws = torch.empty(X.varlen_workspace_bytes(n), dtype=torch.uint8, device=cuda)
     got = host(X.batch_varlen(d, i64(offs, cuda), i64(lens, cuda), workspace=ws))
     assert np.array_equal(got, O.xxh3_batch_varlen(h, offs, lens))
+
+
+@pytest.mark.gpu
+def test_gpu_xxh3_chained_packet_buffers(cuda):
+    """XXH3-64 of packets spread over PacketBuffer chains (fdbrpc/FlowTransport.cpp:2025-2068):
+    chains of 0..40 segments of 0..5000 bytes, any alignment, scattered through
+    a buffer, uniform and per-chain seeds, against the reference's own
+    flow/xxhash.c over each chain's concatenated bytes."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    rng = np.random.default_rng(2043)
+    h = O.splitmix64((32 << 20) // 8, 0x2043).view(np.uint8)
+    d = torch.from_numpy(h).to(cuda)
+    offs, lens, starts = [], [], [0]
+    for c in range(3000):
+        k = int(rng.choice([0, 1, 1, 1, 2, 3, 5, 17, 40]))
+        offs += list(rng.integers(0, h.size - 5000, k))
+        lens += list(rng.integers(0, 5000, k))
+        starts.append(len(offs))
+    offs[:4] = [0, 1, 3, 5]  # tiny, unaligned ones too
+    lens[:4] = [1, 2, 0, 250]
+    cat = lambda c: b"".join(h[o:o + l].tobytes() for o, l in zip(offs[starts[c]:starts[c + 1]], lens[starts[c]:starts[c + 1]]))
+    t = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device=cuda)
+    got = X.batch_chained(d, t(offs), t(lens), t(starts)).cpu().numpy().view(np.uint64)
+    want = np.array([O.ref_xxh3_64(cat(c)) for c in range(len(starts) - 1)], dtype=np.uint64)
+    assert np.array_equal(got, want)
+    seeds = rng.integers(0, 2**63, len(starts) - 1, dtype=np.int64)
+    got = X.batch_chained(d, t(offs), t(lens), t(starts), seeds=torch.from_numpy(seeds).to(cuda)).cpu().numpy().view(np.uint64)
+    want = np.array([O.ref_xxh3_64(cat(c), int(seeds[c])) for c in range(len(starts) - 1)], dtype=np.uint64)
+    assert np.array_equal(got, want)
+    # more than one scan block of segments (4096 per block), and no segments at all
+    n = 9000
+    o2, l2 = rng.integers(0, h.size - 300, n), rng.integers(0, 300, n)
+    s2 = np.arange(0, n + 1, 3)
+    got = X.batch_chained(d, t(o2), t(l2), t(s2)).cpu().numpy().view(np.uint64)
+    cat2 = lambda c: b"".join(h[o:o + l].tobytes() for o, l in zip(o2[s2[c]:s2[c + 1]], l2[s2[c]:s2[c + 1]]))
+    assert all(int(got[c]) == O.ref_xxh3_64(cat2(c)) for c in range(0, len(s2) - 1, 7))
+    e = torch.zeros(0, dtype=torch.int64, device=cuda)
+    got = X.batch_chained(d, e, e, t([0, 0, 0]), seed=9).cpu().numpy().view(np.uint64)
+    assert list(got) == [O.ref_xxh3_64(b"", 9)] * 2
