@@ -571,6 +571,264 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 }
 
 // ---------------------------------------------------------------------------
+// Variable-length batches (packets, chained staging ranges): the row layout of
+// k_xxh3_rows, each 16-lane row walking its own sequence of buffers.  The
+// planner gives the wave whole buffers balanced by bytes; short ones (<= 240 B)
+// go first, one lane each.  The long ones are handed to the rows dynamically:
+// whenever a row has loaded its buffer's last block, it takes the next long
+// buffer of a 64-buffer POOL (lengths/offsets in lanes, a uniform bitmask of
+// the unclaimed long buffers; picks are v_readlane), so the four rows stay busy
+// until the wave's range is exhausted whatever the lengths.  Every data load is
+// unconditional: a row without work reads the planner's workspace (1 KiB,
+// discarded), and lanes whose stripe is unused in a final block read the last
+// 64 bytes (the last-stripe lanes' line).  Offsets are arbitrary: the
+// `dwordx4` loads are unaligned (gfx950 runs with unaligned global access
+// enabled).  A pool refill waits for the loads in flight: once per 64 buffers.
+// ---------------------------------------------------------------------------
+typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
+typedef __attribute__((address_space(1))) const u64x2u g_u64x2u;
+
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int j) {
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+	return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t rdfirst64v(uint64_t v) {
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+	return ((uint64_t)hi << 32) | lo;
+}
+
+struct VStep {
+	uint64_t v[4][2];
+	uint64_t len, buf, seed;  // this row's buffer
+	uint32_t blk;             // block loaded
+	bool act;                 // row has a buffer
+	bool any;                 // some row has one (uniform)
+};
+
+template <bool SEEDS>
+__global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
+	const int lane = threadIdx.x & 63;
+	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
+	const uint64_t wpb = blockDim.x >> 6;
+	const uint64_t w = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const uint64_t begin = rdfirst64v(P.wave_first[w]);
+	uint64_t end = rdfirst64v(P.wave_first[w + 1]);
+	end = end < P.count ? end : P.count;
+	if (begin >= end) return;
+	const uint64_t base = reinterpret_cast<uint64_t>(P.base);
+	const uint64_t* __restrict__ lengths = P.lengths;
+	const uint64_t* __restrict__ offsets = P.offsets;
+	const uint64_t* __restrict__ seeds = P.seeds;
+	uint64_t* __restrict__ out = P.out;
+	const uint64_t seed0 = P.seed;
+
+	// ---- short buffers: one lane each
+	for (uint64_t b0 = begin; b0 < end; b0 += 64) {
+		const uint64_t i = b0 + lane;
+		if (i < end) {
+			const uint64_t len = lengths[i];
+			if (len <= 240) out[i] = xxh3_short(base + offsets[i], len, SEEDS ? seeds[i] : seed0);
+		}
+	}
+
+	// ---- long buffers: rows
+	const uint64_t dummy = reinterpret_cast<uint64_t>(P.wave_first);
+	// Two pool banks: picks come from A; B is refilled only at the top of a
+	// half-iteration, so a pick never waits for a load.
+	uint64_t am = 0, bm = 0, ab = 0, bb = 0, pnext = begin;
+	uint64_t alen = 0, aoff = 0, aseed = 0, blen = 0, boff = 0, bseed = 0;
+	auto fill_b = [&]() __attribute__((always_inline)) {
+		while (bm == 0 && pnext < end) {
+			bb = rdfirst64v(pnext);  // keep the pool cursor in SGPRs
+			pnext = bb + 64;
+			const uint64_t i = bb + lane;
+			const bool in = i < end;
+			blen = in ? lengths[i] : 0;
+			boff = in ? offsets[i] : 0;
+			if (SEEDS) bseed = in ? seeds[i] : 0;
+			bm = __ballot(blen > 240);
+		}
+		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): bank B complete
+	};
+	auto refill = [&]() __attribute__((always_inline)) {
+		if (am == 0) {
+			if (bm == 0) fill_b();
+			am = bm;
+			ab = bb;
+			alen = blen;
+			aoff = boff;
+			aseed = bseed;
+			bm = 0;
+		}
+		if (bm == 0 && pnext < end) fill_b();
+	};
+	// load cursor of this lane's row (row-uniform)
+	uint64_t lp = dummy, llen = 1024, lbuf = 0, lseed = seed0;
+	uint32_t lblk = 0, lnblk = 0;
+	bool lact = false;
+
+	auto grab = [&]() __attribute__((always_inline)) {
+		uint64_t need = __ballot(l == 0 && lblk == lnblk);
+		while (need != 0) {
+			const int rr = __builtin_ctzll(need) >> 4;
+			need &= need - 1;
+			if (am == 0) {
+				if (bm == 0) break;  // nothing loaded: idle until the next refill
+				am = bm;
+				ab = bb;
+				alen = blen;
+				aoff = boff;
+				aseed = bseed;
+				bm = 0;
+			}
+			const int j = __builtin_ctzll(am);
+			am &= am - 1;
+			const uint64_t len = rdlane64(alen, j), off = rdlane64(aoff, j);
+			const uint64_t sd = SEEDS ? rdlane64(aseed, j) : seed0;
+			if (r == rr) {
+				llen = len;
+				lp = base + off;
+				lblk = 0;
+				lnblk = (uint32_t)((len - 1) >> 10) + 1;
+				lbuf = ab + j;
+				lseed = sd;
+				lact = true;
+			}
+		}
+		if (lblk == lnblk) {  // no buffer for this row: read the dummy KiB
+			lact = false;
+			lp = dummy;
+			llen = 1024;
+			lblk = 0;
+			lnblk = 1;
+		}
+	};
+	auto load = [&](VStep& S) __attribute__((always_inline)) {
+		grab();
+		const uint64_t nfull = (llen - 1) >> 10;
+		const uint32_t ns = (uint32_t)(((llen - 1) - (nfull << 10)) >> 6);
+		const bool fin = lblk == nfull;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint32_t s = g + 4 * i;
+			const bool tail = fin && (s == 15 || s >= ns);
+			const uint64_t a = tail ? lp + llen - 64 + 16 * k : lp + ((uint64_t)lblk << 10) + 64 * s + 16 * k;
+			const u64x2u x = __builtin_nontemporal_load((g_u64x2u*)a);
+			S.v[i][0] = x[0];
+			S.v[i][1] = x[1];
+		}
+		S.len = llen;
+		S.buf = lbuf;
+		S.seed = lseed;
+		S.blk = lblk;
+		S.act = lact;
+		S.any = __ballot(lact) != 0;
+		++lblk;
+	};
+
+	// Results collect in lanes (rx = hash, ri = buffer index, rn used) and
+	// leave together: a store's source registers may not be rewritten until it
+	// has completed, and in-order vmcnt would make that a wait for every load in
+	// flight, so stores happen once per 56+ buffers rather than per buffer.
+	uint64_t rx = 0, ri = 0;
+	uint32_t rn = 0;
+	auto flush = [&]() __attribute__((always_inline)) {
+		if ((uint32_t)lane < rn) out[ri] = rx;
+		rn = 0;
+		// wait here, on the rare flush path, so that no later register write
+		// has to wait for the store on the common path
+		__builtin_amdgcn_s_waitcnt(0x0F70);
+	};
+	RowKeys K = row_keys(lane, seed0);
+	uint64_t a0 = 0, a1 = 0;
+	auto compute = [&](const VStep& S) __attribute__((always_inline)) {
+		const uint64_t nfull = (S.len - 1) >> 10;
+		const uint32_t ns = (uint32_t)(((S.len - 1) - (nfull << 10)) >> 6);
+		const bool fin = S.blk == nfull;
+		if (SEEDS && __ballot(S.blk == 0 && S.act) != 0) K = row_keys(lane, S.seed);
+		if (S.blk == 0) {
+			a0 = k == 0 ? P32_3 : (k == 1 ? P64_2 : (k == 2 ? P64_4 : P64_5));
+			a1 = k == 0 ? P64_1 : (k == 1 ? P64_3 : (k == 2 ? P32_2 : P32_1));
+		}
+		uint64_t d0 = 0, d1 = 0;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint32_t s = g + 4 * i;
+			const bool last = fin && s == 15;
+			const bool on = !fin || s < ns || last;
+			const uint64_t x0 = S.v[i][0] ^ (last ? K.l0 : K.k0[i]);
+			const uint64_t x1 = S.v[i][1] ^ (last ? K.l1 : K.k1[i]);
+			const uint64_t c0 = S.v[i][1] + (uint64_t)(uint32_t)x0 * (x0 >> 32);
+			const uint64_t c1 = S.v[i][0] + (uint64_t)(uint32_t)x1 * (x1 >> 32);
+			d0 += on ? c0 : 0;
+			d1 += on ? c1 : 0;
+		}
+		uint32_t lo0 = (uint32_t)d0, hi0 = (uint32_t)(d0 >> 32), lo1 = (uint32_t)d1, hi1 = (uint32_t)(d1 >> 32);
+		add_dpp<0x124>(lo0, hi0);
+		add_dpp<0x124>(lo1, hi1);
+		add_dpp<0x128>(lo0, hi0);
+		add_dpp<0x128>(lo1, hi1);
+		a0 += ((uint64_t)hi0 << 32) | lo0;
+		a1 += ((uint64_t)hi1 << 32) | lo1;
+		const uint64_t m = mulfold(a0 ^ K.g0, a1 ^ K.g1);
+		uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+		add_dpp<0xB1>(lo, hi);
+		add_dpp<0x4E>(lo, hi);
+		const uint64_t h = xxh3_aval(S.len * P64_1 + (((uint64_t)hi << 32) | lo));
+		if (!fin) {
+			a0 = ((a0 ^ (a0 >> 47)) ^ K.c0) * P32_1;
+			a1 = ((a1 ^ (a1 >> 47)) ^ K.c1) * P32_1;
+		}
+		uint64_t done = __ballot(l == 0 && fin && S.act);
+		while (done != 0) {
+			const int src = __builtin_ctzll(done);
+			done &= done - 1;
+			const uint64_t hv = rdlane64(h, src), iv = rdlane64(S.buf, src);
+			rx = (uint32_t)lane == rn ? hv : rx;
+			ri = (uint32_t)lane == rn ? iv : ri;
+			++rn;
+		}
+		if (rn > 56) flush();
+	};
+
+	// Two steps per half-iteration, the other half's two steps in flight; the
+	// halves alternate register sets (no copies of data in flight).
+	// s0/s1 start as idle steps (nothing loaded), so no data load precedes the
+	// loop and every load lands in the loop's own registers.
+	VStep s0, s1, t0, t1;
+#pragma unroll
+	for (int i = 0; i < 4; ++i) s0.v[i][0] = s0.v[i][1] = s1.v[i][0] = s1.v[i][1] = 0;
+	s0.len = s1.len = 1024;
+	s0.buf = s1.buf = 0;
+	s0.seed = s1.seed = seed0;
+	s0.blk = s1.blk = 0;
+	s0.act = s1.act = false;
+	s0.any = s1.any = false;
+	for (;;) {
+		if (!s0.any && !s1.any && am == 0 && bm == 0 && pnext >= end) break;
+		refill();
+		load(t0);
+		load(t1);
+		__builtin_amdgcn_sched_barrier(0);
+		compute(s0);
+		compute(s1);
+		__builtin_amdgcn_sched_barrier(0);
+		if (!t0.any && !t1.any && am == 0 && bm == 0 && pnext >= end) break;
+		refill();
+		load(s0);
+		load(s1);
+		__builtin_amdgcn_sched_barrier(0);
+		compute(t0);
+		compute(t1);
+		__builtin_amdgcn_sched_barrier(0);
+	}
+	flush();
+}
+
+// ---------------------------------------------------------------------------
 // Varlen planning: whole buffers per wave, balanced by bytes.  Wave w takes
 // the buffers whose start lies in [w*Q, (w+1)*Q) of the concatenated stream.
 // ---------------------------------------------------------------------------
@@ -661,7 +919,12 @@ int xxh3_blocks_per_cu() {
 		int a = 0, b = 0;
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xxh3<true>, 256, 0) != hipSuccess) a = 4;
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_xxh3<false>, 256, 0) != hipSuccess) b = 4;
-		const int m = a < b ? a : b;
+		int c = 0, d = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, k_xxh3_vrows<false>, 256, 0) != hipSuccess) c = 3;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&d, k_xxh3_vrows<true>, 256, 0) != hipSuccess) d = 3;
+		int m = a < b ? a : b;
+		m = m < c ? m : c;
+		m = m < d ? m : d;
 		return m < 1 ? 1 : m;
 	}();
 	return n;
@@ -682,6 +945,16 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		k_xscan<<<1, 1024, 0, stream>>>(tiles, ntile, nwave);
 		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(P.lengths, P.count, tiles, ntile, wave_first, nwave);
 		P.wave_first = wave_first;
+#ifndef FDBXXH_VROWS
+#define FDBXXH_VROWS 1
+#endif
+#if FDBXXH_VROWS
+		if (P.seeds)
+			k_xxh3_vrows<true><<<(unsigned)grid, 256, 0, stream>>>(P);
+		else
+			k_xxh3_vrows<false><<<(unsigned)grid, 256, 0, stream>>>(P);
+		return 0;
+#endif
 	}
 	if (!P.offsets && P.length > 240 && (mis & 7) == 0) {
 		// fixed-length pages: four per wave in lockstep

@@ -1,3 +1,5 @@
 # development: one GPU step
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_xxh3.py -m gpu -x -v --timeout 120 --timeout-method thread 2>&1 | grep -E "PASS|FAIL|Error|passed|failed|assert" | tail -15
+mkdir -p gpurun_out
+timeout -k 10 200 python -u tools/probe_xxh3.py 2>&1 | tee gpurun_out/step_probe.log
+FDBCRC_LIB=foundationdb_amd/lib/libfdb_crc32c_xold.so timeout -k 10 200 python -u tools/probe_xxh3.py 2>&1 | tee gpurun_out/step_probe_old.log

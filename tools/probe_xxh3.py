@@ -41,3 +41,5 @@ run("256 x 1M", [256] * (1 << 20), 256)
 run("64 x 1M", [64] * (1 << 20), 64)
 run("zipf", W.zipf_lengths(), 256)
 run("chunks", W.chunk_lengths(), 4096)
+run("zipf unaligned", W.zipf_lengths(), 1)
+run("1500 x 512K unaligned", [1500] * (1 << 19), 1)
