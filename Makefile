@@ -25,7 +25,7 @@ CXXFLAGS := -O3 -fPIC -std=c++17 -Wall -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 TU_LIB := foundationdb_amd/lib/libfdb_crc32c_testutil.so
 TU_SRCS := $(wildcard foundationdb_amd/testutil/*.hip)
 
-all: $(LIB) $(TU_LIB) oracle
+all: $(LIB) $(TU_LIB) $(DBG_LIB) oracle
 
 $(TU_LIB): $(TU_SRCS) foundationdb_amd/testutil/fdb_crc32c_testutil.h
 	@mkdir -p $(dir $(TU_LIB))
@@ -52,12 +52,19 @@ oracle:
 	$(MAKE) -C oracle
 
 # bounds-checked build for kernel debugging (foundationdb_amd/lib/libfdb_crc32c_debug.so)
+# (built by default: the GPU suite replays route batches against it)
 DBG_LIB := foundationdb_amd/lib/libfdb_crc32c_debug.so
-debug: $(HIP_SRCS) $(CPP_SRCS) $(HDRS)
+DBG_OBJS := $(patsubst $(CSRC)/%.hip,build/dbg/%.hip.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,build/dbg/%.cpp.o,$(CPP_SRCS))
+build/dbg/crc32c_kernels.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+build/dbg/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build/dbg
-	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) -DFDBCRC_DEBUG -c $$f -o build/dbg/$$(basename $$f).o || exit 1; done
-	for f in $(CPP_SRCS); do $(CXX) $(CXXFLAGS) -DFDBCRC_DEBUG -c $$f -o build/dbg/$$(basename $$f).o || exit 1; done
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(DBG_LIB) build/dbg/*.o
+	$(HIPCC) $(HIPFLAGS) -DFDBCRC_DEBUG -c $< -o $@
+build/dbg/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build/dbg
+	$(CXX) $(CXXFLAGS) -DFDBCRC_DEBUG -c $< -o $@
+$(DBG_LIB): $(DBG_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+debug: $(DBG_LIB)
 
 # ASan + UBSan build of the host code (reference: cmake/ConfigureCompiler.cmake:5-12):
 # every .cpp instrumented, the device objects as in the product; load it with
@@ -74,7 +81,7 @@ $(ASAN_LIB): $(HIP_OBJS) $(ASAN_OBJS)
 asan: $(ASAN_LIB)
 
 clean:
-	rm -rf build $(LIB) $(TU_LIB) $(ASAN_LIB)
+	rm -rf build $(LIB) $(TU_LIB) $(ASAN_LIB) $(DBG_LIB)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean debug asan

@@ -30,35 +30,53 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // LDS fill: slice4 (1024 words) to all 32 columns, lane tables to their column.
-// Any block size: each round keeps kPer global loads per thread in flight
-// (one round for blocks of 768 or more threads).  Every entry of the image is
-// written: a kernel must never depend on what an earlier kernel left in LDS.
+// Every entry of the image is written (a kernel must never depend on what an
+// earlier kernel left in LDS), for any block size.  Threads write consecutive
+// 16-byte quads of the image (ds_write_b128, conflict-free): the transposed
+// order -- one thread writing a table word's 32 replicas -- puts all lanes of
+// a write on the same banks and cost ~15 us per launch.  The loads of a round
+// are all issued before its writes.
 __device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t) {
-	constexpr uint32_t kSlice = 1024, kLane = 64 * 128;
-	constexpr uint32_t kCompact = kSlice + kLane;  // 9216 words
-	constexpr uint32_t kPer = 12;                  // 12 x 768 = 9216
+	typedef __attribute__((address_space(1))) const uint32_t g_u32;
+	auto gl = [](const uint32_t* p) -> uint32_t { return *((g_u32*)reinterpret_cast<uintptr_t>(p)); };
 	const uint32_t* s4 = &t->slice4[0][0];
 	const uint32_t* ln = &t->lane[0][0][0];
-	for (uint32_t q0 = 0; q0 < kCompact; q0 += kPer * blockDim.x) {
+	constexpr uint32_t kSliceQ = 0x20000 / 16;  // quads of the two slicing regions
+	constexpr uint32_t kLaneQ = 0x8000 / 16;    // quads of the lane tables
+	constexpr uint32_t kPer = 8;
+	u32x4* q4 = reinterpret_cast<u32x4*>(lds);
+	// slicing regions: word W = region*16384 + (idx*2 + (k&1))*32 + col holds
+	// slice4[2*region + (k&1)][idx]; a quad's four words share one value
+	for (uint32_t Q0 = 0; Q0 < kSliceQ; Q0 += kPer * blockDim.x) {
 		uint32_t v[kPer];
 #pragma unroll
 		for (uint32_t i = 0; i < kPer; ++i) {
-			const uint32_t q = q0 + threadIdx.x + i * blockDim.x;
-			v[i] = q < kSlice ? s4[q] : (q < kCompact ? ln[q - kSlice] : 0u);
+			const uint32_t Q = Q0 + threadIdx.x + i * blockDim.x;
+			const uint32_t W = 4 * (Q < kSliceQ ? Q : 0);
+			const uint32_t pair = (W & 16383u) >> 5;
+			v[i] = gl(s4 + (((W >> 14) * 2 + (pair & 1)) << 8) + (pair >> 1));
 		}
 #pragma unroll
 		for (uint32_t i = 0; i < kPer; ++i) {
-			const uint32_t q = q0 + threadIdx.x + i * blockDim.x;
-			if (q < kSlice) {  // slice4[k][idx], k = 0..3 -> T3,T2 | T1,T0 regions
-				const uint32_t k = q >> 8, idx = q & 255;
-				uint32_t* d = lds + (kS4Off / 4) + (k >> 1) * 16384 + (idx * 2 + (k & 1)) * 32;
+			const uint32_t Q = Q0 + threadIdx.x + i * blockDim.x;
+			if (Q < kSliceQ) q4[(kS4Off / 16) + Q] = u32x4{v[i], v[i], v[i], v[i]};
+		}
+	}
+	// lane tables: word V = half*4096 + nv*32 + (l & 31) holds lane[l][nv] (l = 32*half + (l & 31))
+	for (uint32_t Q0 = 0; Q0 < kLaneQ; Q0 += 2 * blockDim.x) {
+		u32x4 v[2];
 #pragma unroll
-				for (int c = 0; c < 32; ++c) d[c] = v[i];
-			} else if (q < kCompact) {
-				const uint32_t r = q - kSlice;
-				const uint32_t l = r >> 7, nv = r & 127;
-				lds[(kS4LaneOff / 4) + (l >> 5) * 4096 + nv * 32 + (l & 31)] = v[i];
-			}
+		for (uint32_t i = 0; i < 2; ++i) {
+			const uint32_t Q = Q0 + threadIdx.x + i * blockDim.x;
+			const uint32_t V = 4 * (Q < kLaneQ ? Q : 0);
+			const uint32_t nv = (V >> 5) & 127u, l = (V >> 12) * 32 + (V & 31u);
+#pragma unroll
+			for (uint32_t e = 0; e < 4; ++e) v[i][e] = gl(ln + (l + e) * 128 + nv);
+		}
+#pragma unroll
+		for (uint32_t i = 0; i < 2; ++i) {
+			const uint32_t Q = Q0 + threadIdx.x + i * blockDim.x;
+			if (Q < kLaneQ) q4[(kS4LaneOff / 16) + Q] = v[i];
 		}
 	}
 	__syncthreads();

@@ -21,6 +21,8 @@ struct DevTables {
 	uint32_t carryw[64][16][8][16];  // x^(8*(1024*(k+1) - z)): a register carried into a table -> its
 	                                 // buffer's end at slot k
 	uint32_t chunkpow[256][8][16];   // x^(8*16*(255-c)): 16-byte chunk c of a pass block to the block's end
+	// big-buffer block route: block k (from the buffer's end) -> the buffer's end
+	uint32_t bpow[2][256][8][16];    // [0][j]: x^(8*4096*j), [1][j]: x^(8*4096*256*j)
 };
 
 // Build the tables on the host (crc32c_tables.cpp).
@@ -59,6 +61,27 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 int launch_chain_fold(const uint64_t* starts, uint64_t nchains, const uint64_t* lengths, const uint32_t* segcrc,
                       uint32_t seed, const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus,
                       hipStream_t stream);
+// Big-buffer block route (crc32c_kernels.hip): buffers the varlen prep kernel
+// routed to 4 KiB blocks aligned to their end.  Entry q of the route's list
+// (in buffer order) is buffer eidx[q]: its blocks are [es[q], es[q+1]) of the
+// route (hdr[2] blocks, hdr[3] entries in total), eE[q] is its end rounded up
+// to 16 bytes, elot[q] = lo/16 | k0 << 8 | t << 12 (lo: bytes of its first
+// block before its first 16-byte chunk, k0: its start mod 16, t: bytes from
+// its end to eE) and esd[q] = ~seed.  out[] starts at ~0 (prep); every block
+// XORs in its raw register weighted to the buffer's end.
+struct BigParams {
+	const uint64_t* hdr;
+	const uint32_t* es;
+	const uint64_t* eE;
+	const uint32_t* eidx;
+	const uint32_t* elot;
+	const uint32_t* esd;
+	uint32_t* out;
+	uint32_t* ctr;  // kPageCtrWords per workgroup, zeroed by prep
+	const DevTables* tabs;
+};
+constexpr uint64_t kBigMax = 256ull << 20;  // largest span routed (block index from the end < 65536)
+int launch_bigblocks(const BigParams& P, int num_cus, hipStream_t stream);
 int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out, hipStream_t stream);
 
 }  // namespace fdbcrc

@@ -228,6 +228,321 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 }
 
 // ---------------------------------------------------------------------------
+// Big-buffer block route (buffers the varlen prep routed here, crc32c_varlen.hip)
+// ---------------------------------------------------------------------------
+// A routed buffer [P0, P1) is cut into nb 4 KiB BLOCKS aligned to its
+// 16-byte-rounded end E: block k (counted from the end) is
+// [E - 4096(k+1), E - 4096k).  The blocks of all routed buffers, in buffer
+// order, stream exactly like 4 KiB pages (k_pages4k: same loads, swizzle,
+// register chains, lane fold, dynamic per-workgroup grabs).  Edges, in the
+// load layout before the swizzle (uniform branches, first/last block only):
+//   * the first block's chunks before A = P0 & ~15 are not loaded (their
+//     addresses clamp to A) and hold zeros -- leading zeros are free;
+//   * in the lead chunk the bytes below P0 are zeroed and ~seed is XORed in
+//     at P0 (append_hw's pre-inversion, crc32c.cpp:197); what spills past the
+//     chunk goes into the next chunk, or into the register at the block end;
+//   * in the last chunk the t = E - P1 bytes after the buffer are zeroed.
+// Every block's raw register R is weighted to the buffer's end and XORed
+// into out[] (prep stored ~0 there: the final inversion):
+//     out ^= R * x^(8*4096*k) * x^(-8t)
+//
+// Block -> buffer: each wave keeps a WINDOW of 64 consecutive route entries
+// in its lanes; the owner of block b is the last entry whose first block is
+// <= b (one ballot).  The window only moves forward (a wave's grabs
+// increase) and is refilled when a grab passes its end.  The registers of a
+// store group's 64 blocks (increasing block order, so a buffer's blocks sit
+// in adjacent lanes) are weighted lane-parallel (global nibble tables),
+// XOR-reduced per buffer (segmented scan) and leave with one atomicXor per
+// buffer part.
+//
+// Lane and register of the 16-byte chunk at block offset o in the load
+// layout (make_ctx, load_block): lane 32h + 16q + r, register ka | kb << 1.
+__device__ __forceinline__ void chunk_slot(uint32_t o, uint32_t& ln, uint32_t& ri) {
+	ln = 32 * ((o >> 4) & 1) + 16 * ((o >> 5) & 1) + ((o >> 6) & 15);
+	ri = ((o >> 11) & 1) | (((o >> 10) & 1) << 1);
+}
+template <int U>
+__global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
+	typedef __attribute__((address_space(1))) const uint64_t g_u64;
+	typedef __attribute__((address_space(1))) const uint32_t g_u32;
+	auto gl32 = [](const uint32_t* p) -> uint32_t { return *((g_u32*)reinterpret_cast<uintptr_t>(p)); };
+	auto gl64 = [](const uint64_t* p) -> uint64_t { return *((g_u64*)reinterpret_cast<uintptr_t>(p)); };
+	const uint64_t count = rdfirst64(gl64(P.hdr + 2));  // blocks
+	if (count == 0) return;
+	const uint64_t nbig = rdfirst64(gl64(P.hdr + 3));   // entries
+	constexpr uint32_t C = 2 * U;   // blocks per grab
+	constexpr uint32_t F = 64 / C;  // grabs per store group
+	__shared__ uint32_t lds[kLdsBytesB / 4];
+	const DevTables* __restrict__ T = P.tabs;
+	const LaneCtx c = make_ctx();
+	const uint32_t lane = (uint32_t)c.lane;
+	const uint32_t col4 = (lane & 31) * 4;
+	const uint32_t c4 = col4 | 0x10000u;
+	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
+	const uint32_t wpb = blockDim.x >> 6;
+	const uint32_t wi = rdfirst(threadIdx.x >> 6);
+	const uint64_t ngrab = (count + C - 1) / C;
+	const uint64_t per = (ngrab + gridDim.x - 1) / gridDim.x;
+	const uint64_t g0 = (uint64_t)blockIdx.x * per;
+	const uint64_t g1 = g0 + per < ngrab ? g0 + per : ngrab;
+	uint32_t* const my_ctr = P.ctr + kPageCtrWords * blockIdx.x;
+	const uint32_t last = (uint32_t)(count - 1);
+
+	// ---- window of route entries [wj, wj + 64) ----------------------------
+	uint64_t wj = 0;
+	uint32_t ws = 0, wI = 0, wL = 0, wS = 0, wend = 0;  // first block (~0: none), output index, lo | k0 | t, ~seed
+	uint64_t wE = 0;                                   // 16-byte-rounded end
+	auto load_window = [&](uint64_t j0) {
+		const uint64_t q = j0 + lane;
+		const uint64_t qc = q < nbig ? q : nbig - 1;  // clamped: every load is unconditional
+		const uint32_t s = gl32(P.es + qc);
+		wE = gl64(P.eE + qc);
+		wI = gl32(P.eidx + qc);
+		wL = gl32(P.elot + qc);
+		wS = gl32(P.esd + qc);
+		const uint64_t qe = j0 + 64 < nbig ? j0 + 64 : nbig - 1;
+		const uint32_t se = gl32(P.es + qe);
+		ws = q < nbig ? s : (q == nbig ? (uint32_t)count : ~0u);
+		wend = j0 + 64 < nbig ? rdfirst(se) : (uint32_t)count;
+		wj = j0;
+	};
+	// the entry holding block b: the last q with es[q] <= b (64-ary narrowing)
+	auto find = [&](uint32_t b) -> uint64_t {
+		uint64_t q0 = 0, n = nbig;  // es[q0] <= b
+		while (n > 64) {
+			const uint64_t stp = (n + 63) >> 6;
+			const uint64_t k = (uint64_t)lane * stp;
+			const uint32_t v = gl32(P.es + q0 + (k < n ? k : 0));
+			const bool le = k < n && v <= b;
+			const uint64_t cnt = __builtin_popcountll(__ballot(le));
+			q0 += (cnt - 1) * stp;
+			n = n - (cnt - 1) * stp < stp ? n - (cnt - 1) * stp : stp;
+		}
+		const uint32_t v = gl32(P.es + q0 + (lane < n ? lane : 0));
+		const bool le = lane < n && v <= b;
+		return q0 + __builtin_popcountll(__ballot(le)) - 1;
+	};
+
+	// ---- per-grab metadata (wave-uniform) ----------------------------------
+	struct Meta {
+		uint64_t a[C];    // block address
+		uint32_t kt[C];   // block index from the buffer's end | t << 16 | (first block: k0 << 20 | lo/16 << 24)
+		uint32_t sd[C];   // first block: ~seed, else 0
+		uint32_t idx[C];  // output index (~0: no block, result discarded)
+	};
+	auto meta_of = [&](uint64_t g, Meta& M) {
+		const uint64_t bf = g * C;
+		if (bf >= count) {  // nothing left: clamped duplicates of a block in the window, discarded
+			const uint64_t a0 = rdlane64(wE, 0) - 4096;
+#pragma unroll
+			for (uint32_t j = 0; j < C; ++j) {
+				M.a[j] = a0;
+				M.kt[j] = 0;
+				M.sd[j] = 0;
+				M.idx[j] = ~0u;
+			}
+			return;
+		}
+		const uint32_t b0 = (uint32_t)bf;
+		const uint32_t bl = bf + C - 1 < count ? b0 + C - 1 : last;
+		while (bl >= wend) {
+			const uint32_t adv = b0 < wend ? (uint32_t)__builtin_popcountll(__ballot(ws <= b0)) - 1u : 64u;
+			load_window(wj + adv);
+		}
+		const int e0 = (int)__builtin_popcountll(__ballot(ws <= b0)) - 1;
+		const uint32_t se0 = rdlane(ws, e0);
+		const uint32_t sn0 = e0 < 63 ? rdlane(ws, e0 + 1) : wend;
+		if (bl < sn0) {  // the whole grab in one buffer (the common case): one lookup
+			const uint32_t m0 = b0 - se0;
+			const uint32_t k0 = sn0 - se0 - 1 - m0;
+			const uint32_t lot = rdlane(wL, e0), ix = rdlane(wI, e0);
+			const uint64_t a0 = rdlane64(wE, e0) - 4096ull * (k0 + 1);
+			const uint32_t t16 = (lot >> 12) << 16;
+#pragma unroll
+			for (uint32_t j = 0; j < C; ++j) {
+				// blocks past the batch's last one: duplicates of it (in this same
+				// buffer), their results discarded
+				const bool valid = b0 + j <= last;
+				M.a[j] = a0 + 4096ull * (valid ? j : last - b0);
+				M.kt[j] = (k0 - j) | t16;
+				M.sd[j] = 0;
+				M.idx[j] = valid ? ix : ~0u;
+			}
+			if (m0 == 0) {  // ... starting at its first block
+				M.kt[0] |= ((lot & 0xF00u) << 12) | ((lot & 0xFFu) << 24);
+				M.sd[0] = rdlane(wS, e0);
+			}
+			return;
+		}
+#pragma unroll
+		for (uint32_t j = 0; j < C; ++j) {
+			const bool valid = b0 + j <= last;
+			const uint32_t b = valid ? b0 + j : last;
+			const int e = (int)__builtin_popcountll(__ballot(ws <= b)) - 1;
+			const uint32_t se = rdlane(ws, e);
+			const uint32_t sn = e < 63 ? rdlane(ws, e + 1) : wend;
+			const uint32_t m = b - se;             // block index from the buffer's start
+			const uint32_t k = sn - se - 1 - m;    // ... from its end
+			const uint32_t lot = rdlane(wL, e);
+			M.a[j] = rdlane64(wE, e) - 4096ull * (k + 1);
+			M.kt[j] = k | ((lot >> 12) << 16) | (m == 0 ? ((lot & 0xF00u) << 12) | ((lot & 0xFFu) << 24) : 0u);
+			M.sd[j] = m == 0 ? rdlane(wS, e) : 0u;
+			M.idx[j] = valid ? rdlane(wI, e) : ~0u;
+		}
+	};
+	auto load_u = [&](Block (&u)[U], const Meta& M, uint32_t j0) {
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) {
+			const uint8_t* blk = reinterpret_cast<const uint8_t*>(M.a[j0 + j]);
+			const uint32_t lo = (M.kt[j0 + j] >> 24) << 4;
+			// load k = 2kb + ka reads block bytes ld_off + 2048ka + 1024kb
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				uint32_t off = c.ld_off + 2048u * (k & 1) + 1024u * (k >> 1);
+				off = off > lo ? off : lo;
+				u[j].r[k] = ld16(blk + off);
+			}
+		}
+	};
+	auto crc_u = [&](Block (&u)[U], const Meta& M, uint32_t j0, uint32_t (&crc)[U]) {
+		uint32_t spill[U];
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) {
+			const uint32_t kt = M.kt[j0 + j], sd = M.sd[j0 + j];
+			spill[j] = 0;
+			if ((kt >> 20) | sd) {  // first block
+				const uint32_t lo = (kt >> 24) << 4, k0 = (kt >> 20) & 15u;
+#pragma unroll
+				for (int k = 0; k < 4; ++k) {  // chunks before the lead chunk
+					const bool z = c.ld_off + 2048u * (k & 1) + 1024u * (k >> 1) < lo;
+#pragma unroll
+					for (int d = 0; d < 4; ++d) u[j].r[k][d] = z ? 0u : u[j].r[k][d];
+				}
+				const Masks mk = edge_masks(k0, 16u, sd);
+				uint32_t ln, ri;
+				chunk_slot(lo, ln, ri);
+				const bool lead_lane = lane == ln;
+#pragma unroll
+				for (uint32_t k = 0; k < 4; ++k) {
+					const bool on = lead_lane && k == ri;
+#pragma unroll
+					for (int d = 0; d < 4; ++d) u[j].r[k][d] = on ? ((u[j].r[k][d] & mk.lm[d]) ^ mk.inj[d]) : u[j].r[k][d];
+				}
+				// ~seed past the lead chunk: into the next chunk, or the register at the block end
+				const bool in_blk = lo + 16 < 4096;
+				chunk_slot((lo + 16) & 4095u, ln, ri);
+				const bool sp_lane = in_blk && lane == ln;
+#pragma unroll
+				for (uint32_t k = 0; k < 4; ++k) u[j].r[k][0] ^= (sp_lane && k == ri) ? mk.spill : 0u;
+				spill[j] = in_blk ? 0u : mk.spill;
+			}
+			const uint32_t t = (kt >> 16) & 15u;
+			if ((kt & 0xFFFFu) == 0 && t) {  // last block: the bytes after the buffer (lane 63, register 3)
+				const Masks mt = edge_masks(0u, 16u - t, 0u);
+#pragma unroll
+				for (int d = 0; d < 4; ++d) u[j].r[3][d] &= lane == 63 ? mt.tm[d] : ~0u;
+			}
+		}
+		uint32_t sd[U];
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) sd[j] = ~0u;  // no register at the block start: ~sd = 0
+		unit_crc_b<U, false, true>(lds, c.lane, c4, c_lane, u, sd, crc, 0, 0);
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) crc[j] ^= spill[j];
+	};
+
+	uint32_t mine = 0, mkt = 0, midx = ~0u;  // lane f*C + j: block j of the group's f-th grab
+	auto store = [&]() {
+		const uint32_t k = mkt & 0xFFFFu, t = (mkt >> 16) & 15u;
+		uint32_t w = vmul_tab(T->bpow[0][k & 255u], mine);
+		if (__ballot(k >= 256u)) w = vmul_tab(T->bpow[1][k >> 8], w);
+		w = vmul_tab(T->inv_z[t], w);
+		// segmented inclusive XOR over runs of equal output index
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const uint32_t y = (uint32_t)__shfl_up((int)w, d);
+			const uint32_t yi = (uint32_t)__shfl_up((int)midx, d);
+			if ((int)lane >= d && yi == midx) w ^= y;
+		}
+		const uint32_t ni = (uint32_t)__shfl_down((int)midx, 1);
+		if (midx != ~0u && (lane == 63 || ni != midx)) atomicXor(P.out + midx, w);
+		midx = ~0u;
+	};
+
+	auto clampg = [&](uint64_t g) { return g < g1 ? g : ngrab; };  // ngrab: nothing left
+	auto request = [&]() -> uint32_t {
+		uint32_t r = 0;
+		if (lane == 0) r = atomicAdd(my_ctr, 1u);
+		return r;
+	};
+	uint64_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
+	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
+	load_window(find(g0 * C < count ? (uint32_t)(g0 * C) : last));
+	Meta MA, MB;
+	meta_of(gA, MA);
+	meta_of(gB, MB);
+	Block u0[U], u1[U];
+	load_u(u0, MA, 0);  // in flight during the LDS fill
+	fill_lds_b(lds, T);
+	uint32_t f = 0;
+	// one grab: X is its metadata, Y the next grab's (its first unit is
+	// loaded here), rebuilt for the grab after it
+	auto step = [&](Meta& X, Meta& Y) {
+		const uint32_t l0 = f * C;
+		uint32_t crc[U];
+		load_u(u1, X, U);
+		__builtin_amdgcn_sched_barrier(0);
+		crc_u(u0, X, 0, crc);
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) {
+			const bool me = lane == l0 + j;
+			mine = me ? crc[j] : mine;
+			mkt = me ? X.kt[j] : mkt;
+			midx = me ? X.idx[j] : midx;
+		}
+		__builtin_amdgcn_sched_barrier(0);
+		load_u(u0, Y, 0);  // the next grab's first unit
+		__builtin_amdgcn_sched_barrier(0);
+		crc_u(u1, X, U, crc);
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) {
+			const bool me = lane == l0 + U + j;
+			mine = me ? crc[j] : mine;
+			mkt = me ? X.kt[U + j] : mkt;
+			midx = me ? X.idx[U + j] : midx;
+		}
+		__builtin_amdgcn_sched_barrier(0);
+		gA = gB;
+		gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
+		req = request();
+		meta_of(gB, X);
+		if (++f == F) {
+			store();
+			f = 0;
+		}
+	};
+	// two grabs per iteration: the metadata registers swap roles instead of
+	// being copied
+	while (gA < ngrab) {
+		step(MA, MB);
+		if (gA >= ngrab) break;
+		step(MB, MA);
+	}
+	if (f) store();
+	// every request of every wave has returned: the counter goes back to zero
+	__builtin_amdgcn_s_waitcnt(0);
+	__syncthreads();
+	if (threadIdx.x == 0) *my_ctr = 0;
+}
+
+int launch_bigblocks(const BigParams& P, int num_cus, hipStream_t stream) {
+	// the block count lives on the device: one workgroup per CU, waves
+	// without a grab leave at once
+	k_bigblocks<FDBCRC_PU><<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 // At most one workgroup per CU, and at least one grab per wave.
@@ -281,6 +596,20 @@ int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32
 	    pages, stride, max_count, seed, nullptr, out, tabs, ctr, h, t, idx, d_count);
 	return 0;
 }
+
+#ifdef FDBCRC_DEBUG
+// Debug builds: this file's copy of the load window (crc32c_common.h keeps one
+// per translation unit), set and read together with the varlen file's.
+__global__ void k_dbg_set_pages(unsigned long long lo, unsigned long long hi) {
+	g_dbg[0] = lo; g_dbg[1] = hi;
+	for (int k = 2; k < 8; ++k) g_dbg[k] = 0;
+}
+__global__ void k_dbg_get_pages(unsigned long long* out) {
+	for (int k = 0; k < 8; ++k) out[k] = g_dbg[k];
+}
+void dbg_set_pages(uint64_t lo, uint64_t hi) { k_dbg_set_pages<<<1, 1>>>(lo, hi); }
+void dbg_get_pages(uint64_t* d_out8) { k_dbg_get_pages<<<1, 1>>>(reinterpret_cast<unsigned long long*>(d_out8)); }
+#endif
 
 __global__ void k_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* __restrict__ seeds,
                              uint32_t* __restrict__ out) {

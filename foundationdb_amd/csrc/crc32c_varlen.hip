@@ -8,6 +8,7 @@
 // crc32c_combine.  The design (v7) is described where its kernels start below.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "crc32c_common.h"
 
@@ -244,18 +245,23 @@ __device__ __forceinline__ void keep_below7(uint32_t k1, uint32_t (&tm)[4]) {
 }
 struct Geo7 {
 	uint64_t A;    // P0 & ~15
-	uint32_t W;    // windows (0: shorter than 16 bytes)
+	uint32_t W;    // windows (0: shorter than 16 bytes, small, or routed to blocks)
 	uint32_t lo;   // bytes of window 0 before A (multiple of 16, < 1024)
 	uint32_t k0;   // P0 % 16
 	uint32_t zt;   // E - P1
+	uint32_t nb;   // 4 KiB blocks of the big-buffer route (0: not routed)
 };
-__device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len) {
+// bigmin: spans of at least this many bytes (up to kBigMax) go to the block
+// route (crc32c_kernels.hip, k_bigblocks); 0 disables it.
+__device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len, uint64_t bigmin = 0) {
 	Geo7 g;
 	const uint64_t P1 = P0 + len;
 	const uint64_t E = (P1 + 15) & ~uint64_t(15);
 	g.A = P0 & ~uint64_t(15);
 	const uint64_t span = E - g.A;
-	g.W = (len >= 16 && span > kSmallSpan) ? (uint32_t)((span + 1023) >> 10) : 0u;
+	const bool big = bigmin && len >= 16 && span >= bigmin && span <= kBigMax;
+	g.nb = big ? (uint32_t)((span + 4095) >> 12) : 0u;
+	g.W = (!big && len >= 16 && span > kSmallSpan) ? (uint32_t)((span + 1023) >> 10) : 0u;
 	g.lo = (uint32_t)(1024 * (uint64_t)g.W - span) & 1023u;
 	g.k0 = (uint32_t)(P0 & 15);
 	g.zt = (uint32_t)(E - P1);
@@ -281,30 +287,58 @@ struct V7Params {
 	uint32_t* ctr;             // per workgroup: slot ranges grabbed (FDBCRC_V7_RANGES > 1)
 	const DevTables* tabs;
 	uint32_t qalign;           // slots per wave rounded to a multiple of this (power of two)
+	// big-buffer block route (bigmin = 0: off; hdr[2] blocks and hdr[3] entries in total)
+	uint64_t bigmin;
+	uint64_t* bsum;            // per tile: blocks of its routed buffers (like tsum)
+	uint64_t* nsum;            // per tile: routed buffers
+	uint32_t* es;              // per entry: first block
+	uint64_t* eE;              // per entry: 16-byte-rounded end
+	uint32_t* eidx;            // per entry: buffer index
+	uint32_t* elot;            // per entry: lo / 16 | k0 << 8 | t << 12
+	uint32_t* esd;             // per entry: ~seed
+	uint32_t* bctr;            // block kernel grab counters (zeroed here)
+	uint32_t nbctr;            // ... words
 };
 __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_t& off, uint64_t& len) {
 	off = P.offsets ? P.offsets[i] : i * P.stride;
 	len = P.lengths ? P.lengths[i] : P.length;
 }
 __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
-	__shared__ uint64_t part[4];
+	__shared__ uint64_t part[3][4];
 	const uint64_t i = (uint64_t)blockIdx.x * kTileW + threadIdx.x;
-	uint64_t W = 0;
+	uint64_t W = 0, B = 0, N = 0;
 	if (i < P.count) {
 		uint64_t off, len;
 		v7_buffer(P, i, off, len);
-		W = geo7(reinterpret_cast<uint64_t>(P.base) + off, len).W;
+		const Geo7 g = geo7(reinterpret_cast<uint64_t>(P.base) + off, len, P.bigmin);
+		W = g.W;
+		B = g.nb;
+		N = g.nb ? 1 : 0;
 	}
-	for (int o = 32; o > 0; o >>= 1) W += __shfl_xor(W, o);
-	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = W;
+	for (int o = 32; o > 0; o >>= 1) {
+		W += __shfl_xor(W, o);
+		B += __shfl_xor(B, o);
+		N += __shfl_xor(N, o);
+	}
+	if ((threadIdx.x & 63) == 0) {
+		part[0][threadIdx.x >> 6] = W;
+		part[1][threadIdx.x >> 6] = B;
+		part[2][threadIdx.x >> 6] = N;
+	}
 	__syncthreads();
-	if (threadIdx.x == 0) P.tsum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+	if (threadIdx.x == 0) {
+		P.tsum[blockIdx.x] = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+		if (P.bigmin) {
+			P.bsum[blockIdx.x] = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+			P.nsum[blockIdx.x] = part[2][0] + part[2][1] + part[2][2] + part[2][3];
+		}
+	}
 }
 
 __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	__shared__ uint32_t s4[4][256];  // slice4 tables (no bank replication: this kernel is not LDS-bound)
-	__shared__ uint32_t wsum[4];
-	__shared__ uint64_t s_pre[4];
+	__shared__ uint32_t wsum[3][4];
+	__shared__ uint64_t s_pre[3][4];
 	const DevTables* T = P.tabs;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -314,42 +348,84 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	if (tile == 0)
 		for (uint64_t k = threadIdx.x; k < P.nwave / kV7RangesPerBlock; k += 256) P.ctr[k] = 0;
 #endif
-	// exclusive slot prefix of this tile: the sum of all earlier tile sums,
-	// read in parallel by the whole block (no inter-block waiting)
-	uint64_t pre = 0;
+	if (tile == 0)
+		for (uint32_t k = threadIdx.x; k < P.nbctr; k += 256) P.bctr[k] = 0;
+	// exclusive prefixes of this tile (window slots, route blocks, route
+	// entries): the sums of all earlier tiles, read in parallel by the whole
+	// block (no inter-block waiting)
+	uint64_t pre = 0, preB = 0, preN = 0;
 	if (P.scanned) {
-		pre = threadIdx.x == 0 ? P.tsum[tile] : 0;
+		if (threadIdx.x == 0) {
+			pre = P.tsum[tile];
+			if (P.bigmin) {
+				preB = P.bsum[tile];
+				preN = P.nsum[tile];
+			}
+		}
 	} else if (P.selfsum) {
 		for (uint64_t j = threadIdx.x; j < (uint64_t)tile * kTileW; j += blockDim.x) {
 			uint64_t o, l;
 			v7_buffer(P, j, o, l);
-			pre += geo7(reinterpret_cast<uint64_t>(P.base) + o, l).W;
+			const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o, l, P.bigmin);
+			pre += gj.W;
+			preB += gj.nb;
+			preN += gj.nb ? 1u : 0u;
 		}
 	} else {
-		for (uint32_t k = threadIdx.x; k < tile; k += blockDim.x) pre += P.tsum[k];
+		for (uint32_t k = threadIdx.x; k < tile; k += blockDim.x) {
+			pre += P.tsum[k];
+			if (P.bigmin) {
+				preB += P.bsum[k];
+				preN += P.nsum[k];
+			}
+		}
 	}
-	for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
-	if (lane == 0) s_pre[wv] = pre;
+	for (int o = 32; o > 0; o >>= 1) {
+		pre += __shfl_xor(pre, o);
+		preB += __shfl_xor(preB, o);
+		preN += __shfl_xor(preN, o);
+	}
+	if (lane == 0) {
+		s_pre[0][wv] = pre;
+		s_pre[1][wv] = preB;
+		s_pre[2][wv] = preN;
+	}
 	const uint64_t i = (uint64_t)tile * kTileW + threadIdx.x;
 	const bool ok = i < P.count;
 	uint64_t off = 0, len = 0;
 	if (ok) v7_buffer(P, i, off, len);
 	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
-	const Geo7 g = geo7(P0, len);
-	const uint32_t W = ok ? g.W : 0u;
-	uint32_t incl = W;
+	const Geo7 g = geo7(P0, len, P.bigmin);
+	const uint32_t W = ok ? g.W : 0u, B = ok ? g.nb : 0u, N = (ok && g.nb) ? 1u : 0u;
+	uint32_t incl = W, inclB = B, inclN = N;
 	for (int d = 1; d < 64; d <<= 1) {
 		const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-		if (lane >= d) incl += y;
+		const uint32_t yB = (uint32_t)__shfl_up((int)inclB, d);
+		const uint32_t yN = (uint32_t)__shfl_up((int)inclN, d);
+		if (lane >= d) {
+			incl += y;
+			inclB += yB;
+			inclN += yN;
+		}
 	}
-	if (lane == 63) wsum[wv] = incl;
+	if (lane == 63) {
+		wsum[0][wv] = incl;
+		wsum[1][wv] = inclB;
+		wsum[2][wv] = inclN;
+	}
 	__syncthreads();
-	uint32_t inwave = 0, agg = 0;
+	uint32_t inwave = 0, agg = 0, inB = 0, aggB = 0, inN = 0, aggN = 0;
 	for (int k = 0; k < 4; ++k) {
-		inwave += k < wv ? wsum[k] : 0u;
-		agg += wsum[k];
+		inwave += k < wv ? wsum[0][k] : 0u;
+		agg += wsum[0][k];
+		inB += k < wv ? wsum[1][k] : 0u;
+		aggB += wsum[1][k];
+		inN += k < wv ? wsum[2][k] : 0u;
+		aggN += wsum[2][k];
 	}
-	const uint32_t excl = (uint32_t)(s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3]);
+	const uint32_t excl = (uint32_t)(s_pre[0][0] + s_pre[0][1] + s_pre[0][2] + s_pre[0][3]);
+	const uint64_t exclB = s_pre[1][0] + s_pre[1][1] + s_pre[1][2] + s_pre[1][3];
+	const uint64_t exclN = s_pre[2][0] + s_pre[2][1] + s_pre[2][2] + s_pre[2][3];
 	if (threadIdx.x == 0) {
 		P.incl[tile] = (uint64_t)excl + agg;
 		if (tile + 1 == P.ntile) {
@@ -358,12 +434,28 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 			q = q < P.qalign ? P.qalign : (q + P.qalign - 1) & ~uint64_t(P.qalign - 1);
 			P.hdr[0] = total;
 			P.hdr[1] = q;
+			P.hdr[2] = exclB + aggB;
+			P.hdr[3] = exclN + aggN;
 		}
 	}
 	if (!ok) return;
 	const uint32_t gi = excl + inwave + incl - W;
 	P.gs[i] = gi;
 	const uint32_t s0 = ~(P.seeds ? P.seeds[i] : P.seed);
+	if (g.nb) {
+		// block route: the buffer's entry; out[] starts at ~0 (the final
+		// inversion) and every block XORs its weighted register in
+		const uint64_t q = exclN + inN + inclN - 1;
+		const uint64_t E = (P0 + len + 15) & ~uint64_t(15);
+		const uint32_t lo = (uint32_t)(4096ull * g.nb - (E - g.A));
+		P.es[q] = (uint32_t)(exclB + inB + inclB - B);
+		P.eE[q] = E;
+		P.eidx[q] = (uint32_t)i;
+		P.elot[q] = (lo >> 4) | (g.k0 << 8) | (g.zt << 12);
+		P.esd[q] = s0;
+		P.out[i] = ~0u;
+		return;
+	}
 	if (!W) {
 		if (len < 16) {  // byte-serial
 			uint32_t r = s0;
@@ -456,12 +548,15 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	const uint32_t col4 = (lane & 31) * 4;
 	const uint32_t c4 = col4 | 0x10000u;
 	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
-	fill_lds_b(lds, T);
 	const uint64_t wpb = blockDim.x >> 6;
 	typedef __attribute__((address_space(1))) const uint64_t g_u64;
 	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
 	const uint64_t total = rdfirst64(hp[0]), Qs = rdfirst64(hp[1]);
 	const uint64_t r_base = (uint64_t)blockIdx.x * kV7RangesPerBlock;
+	// no slots for this workgroup (e.g. every buffer went to the block route):
+	// leave before the table fill
+	if (r_base * Qs >= total) return;
+	fill_lds_b(lds, T);
 	uint64_t w = r_base + rdfirst(threadIdx.x >> 6);
 	for (;;) {
 	const uint64_t lo_s64 = w * Qs;
@@ -511,7 +606,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			g = P.gs[j];
 			cl = P.cl[j];
 		}
-		const Geo7 ge = geo7(reinterpret_cast<uint64_t>(P.base) + off, len);
+		const Geo7 ge = geo7(reinterpret_cast<uint64_t>(P.base) + off, len, P.bigmin);
 		const uint32_t W = ok ? ge.W : 0u;
 		B_bi0 = bi0;
 		B_wb = ge.A - ge.lo;
@@ -776,11 +871,20 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	}
 }
 
+#ifndef FDBCRC_BIGMIN
+#define FDBCRC_BIGMIN 4096  // smallest span (bytes) sent to the block route; 0 disables it
+#endif
+static_assert(FDBCRC_BIGMIN == 0 || FDBCRC_BIGMIN >= 4096, "the route's edge terms assume distinct lead and tail chunks");
+
+static uint64_t al16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 	nwave = nwave > 16 * 1024 ? nwave : 16 * 1024;  // covers any launch geometry up to 1024 CUs
 	nwave *= FDBCRC_V7_RANGES;                      // virtual waves: one per slot range
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
-	return 16 + 16 * (ntile + 1) + 4 * nwave + 8 * count + 256 * nwave + 4 * nwave + 64;
+	return 64 + 32 * (ntile + 1) + al16(4 * nwave + 8 * count) + 256 * nwave + 4 * nwave + 64  // window route
+	       + 16 * (ntile + 1) + 8 * count + 4 * al16(4 * count)                                    // block route
+	       + 4 * nwave;                                                                            // its counters
 }
 
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
@@ -794,14 +898,40 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
 	P.seed = seed; P.seeds = seeds; P.out = out; P.tabs = tabs;
 	P.ntile = ntile; P.nwave = nwave; P.qalign = 4;
-	P.hdr = reinterpret_cast<uint64_t*>(wp);
-	P.tsum = reinterpret_cast<uint64_t*>(wp + 16);
+	// block route: output indices are 32-bit there.  FDBCRC_BIGMIN in the
+	// environment (development: route threshold experiments) overrides the
+	// built-in threshold; values below 4096 are raised to it, 0 disables.
+	static const uint64_t bigmin_env = [] {
+		const char* e = getenv("FDBCRC_BIGMIN");
+		if (!e) return (uint64_t)FDBCRC_BIGMIN;
+		const uint64_t v = strtoull(e, nullptr, 0);
+		return v == 0 ? 0 : (v < 4096 ? 4096 : v);
+	}();
+	P.bigmin = count < 0xFFFFFFFFull ? bigmin_env : 0;
+	P.hdr = reinterpret_cast<uint64_t*>(wp);      // [0..3]; [4..7]: k_scan scratch of the route's tile sums
+	P.tsum = reinterpret_cast<uint64_t*>(wp + 64);
 	P.incl = P.tsum + ntile + 1;
-	uint32_t* wave_tile = reinterpret_cast<uint32_t*>(P.incl + ntile + 1);  // k_scan output (unused here)
+	P.bsum = P.incl + ntile + 1;
+	P.nsum = P.bsum + ntile + 1;
+	uint32_t* wave_tile = reinterpret_cast<uint32_t*>(P.nsum + ntile + 1);  // k_scan output (unused here)
 	P.gs = wave_tile + nwave;
 	P.cl = P.gs + count;
 	P.dummy = P.cl + count;
 	P.ctr = P.dummy + 64 * nwave;
+	uint8_t* rp = reinterpret_cast<uint8_t*>(P.ctr + nwave) + 64;
+	rp = reinterpret_cast<uint8_t*>(al16(reinterpret_cast<uint64_t>(rp)));
+	P.eE = reinterpret_cast<uint64_t*>(rp);
+	rp += 8 * count;
+	P.es = reinterpret_cast<uint32_t*>(rp);
+	rp += al16(4 * count);
+	P.eidx = reinterpret_cast<uint32_t*>(rp);
+	rp += al16(4 * count);
+	P.elot = reinterpret_cast<uint32_t*>(rp);
+	rp += al16(4 * count);
+	P.esd = reinterpret_cast<uint32_t*>(rp);
+	rp += al16(4 * count);
+	P.bctr = reinterpret_cast<uint32_t*>(rp);
+	P.nbctr = (uint32_t)(kPageCtrWords * grid);
 	// tile prefixes: each prep block sums its predecessors (up to 8192 tiles);
 	// larger batches scan the tile sums first; batches of at most 8 tiles
 	// skip the count kernel (a prep block counts its predecessors' windows
@@ -809,8 +939,20 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.scanned = ntile > 8192;
 	P.selfsum = ntile <= kSelfSumTiles;
 	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
-	if (P.scanned) k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4);
+	if (P.scanned) {
+		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4);
+		if (P.bigmin) {  // scratch header and wave map (one wave)
+			k_scan<<<1, 1024, 0, stream>>>(P.bsum, ntile, reinterpret_cast<uint32_t*>(P.hdr + 6), 1, P.hdr + 4, 4, 4);
+			k_scan<<<1, 1024, 0, stream>>>(P.nsum, ntile, reinterpret_cast<uint32_t*>(P.hdr + 6), 1, P.hdr + 4, 4, 4);
+		}
+	}
 	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	if (P.bigmin) {
+		BigParams B{};
+		B.hdr = P.hdr; B.es = P.es; B.eE = P.eE; B.eidx = P.eidx; B.elot = P.elot; B.esd = P.esd;
+		B.out = out; B.ctr = P.bctr; B.tabs = tabs;
+		launch_bigblocks(B, num_cus, stream);
+	}
 	k_varlen7<<<(unsigned)grid, FDBCRC_V7_THREADS, 0, stream>>>(P);
 	return 0;
 }
@@ -1239,14 +1381,29 @@ __global__ void k_dbg_get(unsigned long long* out) {
 }  // namespace fdbcrc
 
 #ifdef FDBCRC_DEBUG
-// Debug builds only (make debug): allowed window for varlen data loads, and
-// readback of [lo, hi, violations, first bad address, site, ...].
+// Debug builds only (make debug): allowed window for the data loads of the
+// varlen engine and the block route (lo = hi = 0: no checking), and readback
+// of [lo, hi, violations, first bad address, site, ...] over both.
+namespace fdbcrc {
+void dbg_set_pages(uint64_t lo, uint64_t hi);
+void dbg_get_pages(uint64_t* d_out8);
+}
 extern "C" int crc32c_debug_bounds(uint64_t lo, uint64_t hi) {
 	fdbcrc::k_dbg_set<<<1, 1>>>(lo, hi);
+	fdbcrc::dbg_set_pages(lo, hi);
 	return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
 extern "C" int crc32c_debug_read(uint64_t* d_out8) {
+	uint64_t a[8], b[8];
 	fdbcrc::k_dbg_get<<<1, 1>>>(reinterpret_cast<unsigned long long*>(d_out8));
-	return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
+	if (hipMemcpy(a, d_out8, 64, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+	fdbcrc::dbg_get_pages(d_out8);
+	if (hipMemcpy(b, d_out8, 64, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+	if (!a[2]) {
+		a[3] = b[3];
+		a[4] = b[4];
+	}
+	a[2] += b[2];
+	return hipMemcpy(d_out8, a, 64, hipMemcpyHostToDevice) == hipSuccess ? 0 : -3;
 }
 #endif
