@@ -1,6 +1,7 @@
 // C ABI for the batched engine (declarations and contracts: include/fdb_crc32c.h).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -31,6 +32,8 @@ struct StreamState {
 	uint64_t ws_bytes = 0;
 	uint32_t* ctr = nullptr;  // page-kernel grab counters
 	uint64_t ctr_bytes = 0;
+	uint64_t* hst_h = nullptr;  // varlen route statistics of the stream's last batch (host-mapped)
+	uint64_t* hst_d = nullptr;  // ... its device address
 };
 
 struct DeviceState {
@@ -124,6 +127,37 @@ int stream_workspace(DeviceState* st, hipStream_t s, uint64_t need, void** ws, u
 	return 0;
 }
 
+// Route of the stream's next varlen batch from the span statistics its last
+// batch left (prep writes them into host-mapped memory; read without any
+// synchronisation: a stale or torn value only costs speed, never
+// correctness).  Caller holds the stream's lock.  Falls back to kRouteBoth.
+int stream_route(DeviceState* st, hipStream_t s, uint64_t** hstat) {
+	StreamState* ss = stream_state(st, s);
+	if (!ss->hst_h) {
+		void* h = nullptr;
+		void* d = nullptr;
+		if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess) {
+			*hstat = nullptr;
+			return kRouteBoth;
+		}
+		memset(h, 0, 64);
+		if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+			(void)hipHostFree(h);
+			*hstat = nullptr;
+			return kRouteBoth;
+		}
+		ss->hst_h = static_cast<uint64_t*>(h);
+		ss->hst_d = static_cast<uint64_t*>(d);
+	}
+	*hstat = ss->hst_d;
+	static const int forced = [] {  // development: FDBCRC_ROUTE=0|1|2 pins the route
+		const char* e = getenv("FDBCRC_ROUTE");
+		return e ? atoi(e) : -1;
+	}();
+	if (forced >= kRouteBoth && forced <= kRouteBlocks) return forced;
+	return route_for_stats(ss->hst_h);
+}
+
 int check_launch(const char* what) {
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, what, e);
@@ -175,6 +209,7 @@ int release_stream(hipStream_t stream) {
 	hipError_t e = hipStreamSynchronize(stream);
 	if (ss->ws) (void)hipFree(ss->ws);
 	if (ss->ctr) (void)hipFree(ss->ctr);
+	if (ss->hst_h) (void)hipHostFree(ss->hst_h);
 	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "hipStreamSynchronize(release)", e);
 	return 0;
 }
@@ -303,9 +338,9 @@ uint64_t crc32c_gpu_varlen_workspace_bytes(uint64_t count) {
 	return varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16);
 }
 
-int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
-                               uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
-                               uint64_t workspace_bytes, void* stream) {
+static int batch_varlen_impl(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                             uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
+                             uint64_t workspace_bytes, void* stream, int route, uint64_t* hstat) {
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths || !d_base)
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
@@ -318,12 +353,20 @@ int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, co
 	debug_window_varlen(d_base, d_offsets, d_lengths, count);
 #endif
 	launch_varlen(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, seed, d_seeds, d_out, st->tables,
-	              st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream));
+	              st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream), route, hstat);
 #ifdef FDBCRC_DEBUG
 	(void)hipDeviceSynchronize();
 	debug_report("batch_varlen");
 #endif
 	return check_launch("crc32c_gpu_batch_varlen launch");
+}
+
+// Caller-owned workspace: no library state, so both routes run.
+int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                               uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
+                               uint64_t workspace_bytes, void* stream) {
+	return batch_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, d_workspace, workspace_bytes,
+	                         stream, kRouteBoth, nullptr);
 }
 
 int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
@@ -339,7 +382,9 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
 	                              varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have, &hold))
 		return rc;
-	return crc32c_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
+	uint64_t* hstat = nullptr;
+	const int route = stream_route(st, reinterpret_cast<hipStream_t>(stream), &hstat);
+	return batch_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream, route, hstat);
 }
 
 // ---- grouped chains ------------------------------------------------------------

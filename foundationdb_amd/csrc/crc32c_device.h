@@ -22,7 +22,7 @@ struct DevTables {
 	                                 // buffer's end at slot k
 	uint32_t chunkpow[256][8][16];   // x^(8*16*(255-c)): 16-byte chunk c of a pass block to the block's end
 	// big-buffer block route: block k (from the buffer's end) -> the buffer's end
-	uint32_t bpow[2][256][8][16];    // [0][j]: x^(8*4096*j), [1][j]: x^(8*4096*256*j)
+	uint32_t bpow[4][256][8][16];    // [i][j]: x^(8*4096*j*256^i)
 };
 
 // Build the tables on the host (crc32c_tables.cpp).
@@ -43,10 +43,25 @@ int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32
                              uint64_t max_count, uint32_t h, uint32_t t, uint32_t seed, uint32_t* out,
                              const DevTables* tabs, int num_cus, hipStream_t stream);
 // Variable-length engine (crc32c_varlen.hip).  ws: varlen_workspace_bytes().
+// route: which streaming kernels run.  kRouteBoth: spans of 4 KiB or more on
+// 4 KiB blocks (k_bigblocks), the rest on 1 KiB window slots (k_varlen7);
+// kRouteWindows: windows only; kRouteBlocks: blocks only.  Every route gives
+// the same checksums; it only decides speed (and which launches a batch pays).
+// hstat (host-mapped, may be null) receives the first 256 buffers' bytes by
+// span class: [0] 128 B < span < 4 KiB, [1] 4 KiB - 16 KiB, [2] 16 KiB and
+// more (route_for_stats() turns them into the next batch's route: blocks
+// when 16 KiB+ spans hold most bytes -- alone if no span is under 4 KiB --,
+// else windows).
+enum : int { kRouteBoth = 0, kRouteWindows = 1, kRouteBlocks = 2 };
+inline int route_for_stats(const volatile uint64_t* s) {
+	const uint64_t win = s[0], mid = s[1], large = s[2];
+	if (large == 0 || large < win + mid) return kRouteWindows;  // (nothing windowed at all: windows, the cheaper launch)
+	return win == 0 ? kRouteBlocks : kRouteBoth;
+}
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
-                  hipStream_t stream);
+                  hipStream_t stream, int route = kRouteBoth, uint64_t* hstat = nullptr);
 // Fixed stride, any length/alignment (same engine, same workspace size as varlen).
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
                          const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
@@ -55,7 +70,7 @@ int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, 
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
-                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream);
+                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat);
 // Grouped chains (crc32c_chain.hip): out[c] = fold of segments [starts[c], starts[c+1])
 // whose independent registers segcrc[j] = crc32c_append(0xffffffff, segment j).
 int launch_chain_fold(const uint64_t* starts, uint64_t nchains, const uint64_t* lengths, const uint32_t* segcrc,
@@ -80,7 +95,7 @@ struct BigParams {
 	uint32_t* ctr;  // kPageCtrWords per workgroup, zeroed by prep
 	const DevTables* tabs;
 };
-constexpr uint64_t kBigMax = 256ull << 20;  // largest span routed (block index from the end < 65536)
+constexpr uint64_t kBigMax = 1ull << 40;  // spans routed are below this (block index from the end < 2^28)
 int launch_bigblocks(const BigParams& P, int num_cus, hipStream_t stream);
 int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out, hipStream_t stream);
 

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 //   * in the last chunk the t = E - P1 bytes after the buffer are zeroed.
 // Every block's raw register R is weighted to the buffer's end and XORed
 // into out[] (prep stored ~0 there: the final inversion):
-//     out ^= R * x^(8*4096*k) * x^(-8t)
+//     out ^= R * x^(8*4096*k) * x^(-8t)          (k < 2^28: spans under 1 TiB)
 //
 // Block -> buffer: each wave keeps a WINDOW of 64 consecutive route entries
 // in its lanes; the owner of block b is the last entry whose first block is
@@ -326,18 +326,22 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	// ---- per-grab metadata (wave-uniform) ----------------------------------
 	struct Meta {
 		uint64_t a[C];    // block address
-		uint32_t kt[C];   // block index from the buffer's end | t << 16 | (first block: k0 << 20 | lo/16 << 24)
+		uint32_t kt[C];   // block index from the buffer's end | t << 28
+		uint32_t ek[C];   // first block: lo/16 | k0 << 8, else 0
 		uint32_t sd[C];   // first block: ~seed, else 0
 		uint32_t idx[C];  // output index (~0: no block, result discarded)
 	};
 	auto meta_of = [&](uint64_t g, Meta& M) {
 		const uint64_t bf = g * C;
-		if (bf >= count) {  // nothing left: clamped duplicates of a block in the window, discarded
+		if (bf >= count) {  // nothing left: duplicates of the window's first entry's last block, discarded
 			const uint64_t a0 = rdlane64(wE, 0) - 4096;
+			// a buffer of one block starts lo bytes into it: its loads clamp there
+			const uint32_t lo16 = rdlane(ws, 1) - rdlane(ws, 0) == 1 ? rdlane(wL, 0) & 0xFFu : 0u;
 #pragma unroll
 			for (uint32_t j = 0; j < C; ++j) {
 				M.a[j] = a0;
 				M.kt[j] = 0;
+				M.ek[j] = lo16;
 				M.sd[j] = 0;
 				M.idx[j] = ~0u;
 			}
@@ -357,19 +361,20 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 			const uint32_t k0 = sn0 - se0 - 1 - m0;
 			const uint32_t lot = rdlane(wL, e0), ix = rdlane(wI, e0);
 			const uint64_t a0 = rdlane64(wE, e0) - 4096ull * (k0 + 1);
-			const uint32_t t16 = (lot >> 12) << 16;
+			const uint32_t t28 = (lot >> 12) << 28;
 #pragma unroll
 			for (uint32_t j = 0; j < C; ++j) {
 				// blocks past the batch's last one: duplicates of it (in this same
 				// buffer), their results discarded
 				const bool valid = b0 + j <= last;
 				M.a[j] = a0 + 4096ull * (valid ? j : last - b0);
-				M.kt[j] = (k0 - j) | t16;
+				M.kt[j] = (k0 - j) | t28;
+				M.ek[j] = 0;
 				M.sd[j] = 0;
 				M.idx[j] = valid ? ix : ~0u;
 			}
 			if (m0 == 0) {  // ... starting at its first block
-				M.kt[0] |= ((lot & 0xF00u) << 12) | ((lot & 0xFFu) << 24);
+				M.ek[0] = lot & 0xFFFu;
 				M.sd[0] = rdlane(wS, e0);
 			}
 			return;
@@ -385,7 +390,8 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 			const uint32_t k = sn - se - 1 - m;    // ... from its end
 			const uint32_t lot = rdlane(wL, e);
 			M.a[j] = rdlane64(wE, e) - 4096ull * (k + 1);
-			M.kt[j] = k | ((lot >> 12) << 16) | (m == 0 ? ((lot & 0xF00u) << 12) | ((lot & 0xFFu) << 24) : 0u);
+			M.kt[j] = k | ((lot >> 12) << 28);
+			M.ek[j] = m == 0 ? lot & 0xFFFu : 0u;
 			M.sd[j] = m == 0 ? rdlane(wS, e) : 0u;
 			M.idx[j] = valid ? rdlane(wI, e) : ~0u;
 		}
@@ -394,7 +400,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 #pragma unroll
 		for (uint32_t j = 0; j < U; ++j) {
 			const uint8_t* blk = reinterpret_cast<const uint8_t*>(M.a[j0 + j]);
-			const uint32_t lo = (M.kt[j0 + j] >> 24) << 4;
+			const uint32_t lo = (M.ek[j0 + j] & 0xFFu) << 4;
 			// load k = 2kb + ka reads block bytes ld_off + 2048ka + 1024kb
 #pragma unroll
 			for (int k = 0; k < 4; ++k) {
@@ -408,10 +414,10 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		uint32_t spill[U];
 #pragma unroll
 		for (uint32_t j = 0; j < U; ++j) {
-			const uint32_t kt = M.kt[j0 + j], sd = M.sd[j0 + j];
+			const uint32_t kt = M.kt[j0 + j], ek = M.ek[j0 + j], sd = M.sd[j0 + j];
 			spill[j] = 0;
-			if ((kt >> 20) | sd) {  // first block
-				const uint32_t lo = (kt >> 24) << 4, k0 = (kt >> 20) & 15u;
+			if (ek | sd) {  // first block
+				const uint32_t lo = (ek & 0xFFu) << 4, k0 = ek >> 8;
 #pragma unroll
 				for (int k = 0; k < 4; ++k) {  // chunks before the lead chunk
 					const bool z = c.ld_off + 2048u * (k & 1) + 1024u * (k >> 1) < lo;
@@ -436,8 +442,8 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 				for (uint32_t k = 0; k < 4; ++k) u[j].r[k][0] ^= (sp_lane && k == ri) ? mk.spill : 0u;
 				spill[j] = in_blk ? 0u : mk.spill;
 			}
-			const uint32_t t = (kt >> 16) & 15u;
-			if ((kt & 0xFFFFu) == 0 && t) {  // last block: the bytes after the buffer (lane 63, register 3)
+			const uint32_t t = kt >> 28;
+			if ((kt & 0xFFFFFFFu) == 0 && t) {  // last block: the bytes after the buffer (lane 63, register 3)
 				const Masks mt = edge_masks(0u, 16u - t, 0u);
 #pragma unroll
 				for (int d = 0; d < 4; ++d) u[j].r[3][d] &= lane == 63 ? mt.tm[d] : ~0u;
@@ -453,9 +459,11 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 
 	uint32_t mine = 0, mkt = 0, midx = ~0u;  // lane f*C + j: block j of the group's f-th grab
 	auto store = [&]() {
-		const uint32_t k = mkt & 0xFFFFu, t = (mkt >> 16) & 15u;
+		const uint32_t k = mkt & 0xFFFFFFFu, t = mkt >> 28;
 		uint32_t w = vmul_tab(T->bpow[0][k & 255u], mine);
-		if (__ballot(k >= 256u)) w = vmul_tab(T->bpow[1][k >> 8], w);
+		if (__ballot(k >= (1u << 8))) w = vmul_tab(T->bpow[1][(k >> 8) & 255u], w);
+		if (__ballot(k >= (1u << 16))) w = vmul_tab(T->bpow[2][(k >> 16) & 255u], w);
+		if (__ballot(k >= (1u << 24))) w = vmul_tab(T->bpow[3][k >> 24], w);
 		w = vmul_tab(T->inv_z[t], w);
 		// segmented inclusive XOR over runs of equal output index
 #pragma unroll

@@ -34,10 +34,8 @@ void build_dev_tables(DevTables* t) {
 			mul_tables_nibble(xpow8(1024u * (d + 1) - z), t->carryw[d][z]);
 		}
 	for (int c = 0; c < 256; ++c) mul_tables_nibble(xpow8(16u * (255 - c)), t->chunkpow[c]);
-	for (int j = 0; j < 256; ++j) {
-		mul_tables_nibble(xpow8(4096ull * j), t->bpow[0][j]);
-		mul_tables_nibble(xpow8(4096ull * 256 * j), t->bpow[1][j]);
-	}
+	for (int i = 0; i < 4; ++i)
+		for (int j = 0; j < 256; ++j) mul_tables_nibble(xpow8((4096ull * j) << (8 * i)), t->bpow[i][j]);
 	for (int m = 0; m < 64; ++m) {
 		// x^(8*2^m) by repeated squaring of x^8
 		uint32_t c = kOne >> 8;

@@ -15,13 +15,14 @@
 namespace fdbcrc {
 
 // ---------------------------------------------------------------------------
-// tile scan (batches of more than 8192 tiles)
+// tile scan (batches of more than kScanTiles tiles)
 // ---------------------------------------------------------------------------
 // quantum: ceil(total / nwave), at least qmin, rounded up to a multiple of qalign
 __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, uint64_t ntile,
                                                uint32_t* __restrict__ wave_tile, uint64_t nwave,
                                                uint64_t* __restrict__ hdr, uint64_t qmin = 4096,
-                                               uint64_t qalign = 64) {
+                                               uint64_t qalign = 64, uint64_t* __restrict__ aux0 = nullptr,
+                                               uint64_t* __restrict__ aux1 = nullptr) {
 	constexpr uint32_t C = 8192;  // tiles per LDS chunk
 	__shared__ uint64_t buf[C];
 	__shared__ uint64_t wsum[16];
@@ -98,6 +99,48 @@ __global__ __launch_bounds__(1024) void k_scan(uint64_t* __restrict__ prefix, ui
 		prefix[ntile] = total;
 		hdr[0] = total;
 		hdr[1] = q;
+	}
+	// the block route's tile sums (blocks, entries): plain exclusive scans
+	for (int a = 0; a < 2; ++a) {
+		uint64_t* arr = a == 0 ? aux0 : aux1;
+		if (!arr) continue;
+		__syncthreads();
+		if (t == 0) carry_s = 0;
+		for (uint64_t c0 = 0; c0 < ntile; c0 += C) {
+			const uint32_t n = (uint32_t)(ntile - c0 < C ? ntile - c0 : C);
+			__syncthreads();
+			for (uint32_t k = t; k < n; k += blockDim.x) buf[k] = arr[c0 + k];
+			__syncthreads();
+			const uint32_t r0 = t * (C / 1024);
+			uint64_t run = 0;
+			for (uint32_t k = 0; k < C / 1024; ++k) {
+				const uint32_t idx = r0 + k;
+				const uint64_t x = idx < n ? buf[idx] : 0;
+				if (idx < n) buf[idx] = run;
+				run += x;
+			}
+			uint64_t inc = run;
+			for (int o = 1; o < 64; o <<= 1) {
+				const uint64_t y = __shfl_up(inc, o);
+				if ((int)lane >= o) inc += y;
+			}
+			if (lane == 63) wsum[w] = inc;
+			__syncthreads();
+			uint64_t wbase = 0, ctot = 0;
+			for (uint32_t k = 0; k < 16; ++k) {
+				wbase += k < w ? wsum[k] : 0;
+				ctot += wsum[k];
+			}
+			const uint64_t excl = carry_s + wbase + inc - run;
+			for (uint32_t k = 0; k < C / 1024; ++k) {
+				const uint32_t idx = r0 + k;
+				if (idx < n) buf[idx] += excl;
+			}
+			__syncthreads();
+			for (uint32_t k = t; k < n; k += blockDim.x) arr[c0 + k] = buf[k];
+			__syncthreads();
+			if (t == 0) carry_s += ctot;
+		}
 	}
 }
 
@@ -214,6 +257,10 @@ constexpr uint32_t kTileW = 256;
 #endif
 constexpr uint64_t kV7RangesPerBlock = (FDBCRC_V7_THREADS / 64) * FDBCRC_V7_RANGES;
 constexpr uint64_t kSelfSumTiles = 8;
+#ifndef FDBCRC_SCAN_TILES
+#define FDBCRC_SCAN_TILES 8192
+#endif
+constexpr uint64_t kScanTiles = FDBCRC_SCAN_TILES;
 #ifndef FDBCRC_SMALL_SPAN
 #define FDBCRC_SMALL_SPAN 128
 #endif
@@ -251,7 +298,7 @@ struct Geo7 {
 	uint32_t zt;   // E - P1
 	uint32_t nb;   // 4 KiB blocks of the big-buffer route (0: not routed)
 };
-// bigmin: spans of at least this many bytes (up to kBigMax) go to the block
+// bigmin: spans of at least this many bytes (below kBigMax) go to the block
 // route (crc32c_kernels.hip, k_bigblocks); 0 disables it.
 __device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len, uint64_t bigmin = 0) {
 	Geo7 g;
@@ -259,7 +306,7 @@ __device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len, uint64_t bigmin 
 	const uint64_t E = (P1 + 15) & ~uint64_t(15);
 	g.A = P0 & ~uint64_t(15);
 	const uint64_t span = E - g.A;
-	const bool big = bigmin && len >= 16 && span >= bigmin && span <= kBigMax;
+	const bool big = bigmin && len >= 16 && span >= bigmin && span < kBigMax;
 	g.nb = big ? (uint32_t)((span + 4095) >> 12) : 0u;
 	g.W = (!big && len >= 16 && span > kSmallSpan) ? (uint32_t)((span + 1023) >> 10) : 0u;
 	g.lo = (uint32_t)(1024 * (uint64_t)g.W - span) & 1023u;
@@ -298,6 +345,7 @@ struct V7Params {
 	uint32_t* esd;             // per entry: ~seed
 	uint32_t* bctr;            // block kernel grab counters (zeroed here)
 	uint32_t nbctr;            // ... words
+	uint64_t* hstat;           // route statistics of tile 0 (host-mapped, may be null): RouteStat
 };
 __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_t& off, uint64_t& len) {
 	off = P.offsets ? P.offsets[i] : i * P.stride;
@@ -339,6 +387,7 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	__shared__ uint32_t s4[4][256];  // slice4 tables (no bank replication: this kernel is not LDS-bound)
 	__shared__ uint32_t wsum[3][4];
 	__shared__ uint64_t s_pre[3][4];
+	__shared__ uint64_t s_stat[4][3];
 	const DevTables* T = P.tabs;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -372,11 +421,24 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 			preN += gj.nb ? 1u : 0u;
 		}
 	} else {
-		for (uint32_t k = threadIdx.x; k < tile; k += blockDim.x) {
-			pre += P.tsum[k];
-			if (P.bigmin) {
-				preB += P.bsum[k];
-				preN += P.nsum[k];
+		// eight tile sums per thread in flight at once (one load latency per
+		// 2048 predecessor tiles, not one per 256)
+		for (uint32_t k0 = threadIdx.x; k0 < tile; k0 += 8 * blockDim.x) {
+			uint64_t v[8], vB[8], vN[8];
+#pragma unroll
+			for (uint32_t u = 0; u < 8; ++u) {
+				const uint32_t k = k0 + u * blockDim.x;
+				const uint32_t kc = k < tile ? k : 0;
+				v[u] = gld64(P.tsum + kc);
+				vB[u] = P.bigmin ? gld64(P.bsum + kc) : 0;
+				vN[u] = P.bigmin ? gld64(P.nsum + kc) : 0;
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < 8; ++u) {
+				const bool in = k0 + u * blockDim.x < tile;
+				pre += in ? v[u] : 0;
+				preB += in ? vB[u] : 0;
+				preN += in ? vN[u] : 0;
 			}
 		}
 	}
@@ -397,6 +459,17 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
 	const Geo7 g = geo7(P0, len, P.bigmin);
 	const uint32_t W = ok ? g.W : 0u, B = ok ? g.nb : 0u, N = (ok && g.nb) ? 1u : 0u;
+	if (tile == 0 && P.hstat) {  // the first 256 buffers' bytes by span class, for the host's next route choice
+		const uint64_t span = ok && len >= 16 ? ((P0 + len + 15) & ~uint64_t(15)) - (P0 & ~uint64_t(15)) : 0;
+		uint64_t c[3] = {span > kSmallSpan && span < 4096 ? len : 0, span >= 4096 && span < 16384 ? len : 0,
+		                 span >= 16384 ? len : 0};
+#pragma unroll
+		for (int k = 0; k < 3; ++k)
+			for (int o = 32; o > 0; o >>= 1) c[k] += __shfl_xor(c[k], o);
+		if (lane == 0)
+#pragma unroll
+			for (int k = 0; k < 3; ++k) s_stat[wv][k] = c[k];
+	}
 	uint32_t incl = W, inclB = B, inclN = N;
 	for (int d = 1; d < 64; d <<= 1) {
 		const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
@@ -427,6 +500,8 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	const uint64_t exclB = s_pre[1][0] + s_pre[1][1] + s_pre[1][2] + s_pre[1][3];
 	const uint64_t exclN = s_pre[2][0] + s_pre[2][1] + s_pre[2][2] + s_pre[2][3];
 	if (threadIdx.x == 0) {
+		if (tile == 0 && P.hstat)
+			for (int k = 0; k < 3; ++k) P.hstat[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
 		P.incl[tile] = (uint64_t)excl + agg;
 		if (tile + 1 == P.ntile) {
 			const uint64_t total = (uint64_t)excl + agg;
@@ -495,7 +570,6 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		return;
 	}
 	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
-	if (!P.cl) return;  // v8 masks the lead chunk and injects the seed itself
 	// lead term: the lead chunk's bytes below k0 (read only when the buffer
 	// starts inside its chunk) with the register ~seed injected at k0, carried
 	// to the end of the pass block (chunkpow).  The garbage after the buffer's
@@ -889,7 +963,7 @@ uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
-                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream) {
+                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat) {
 	const uint64_t grid = (uint64_t)num_cus;
 	const uint64_t nwave = grid * kV7RangesPerBlock;  // one virtual wave per slot range
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
@@ -907,7 +981,14 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 		const uint64_t v = strtoull(e, nullptr, 0);
 		return v == 0 ? 0 : (v < 4096 ? 4096 : v);
 	}();
-	P.bigmin = count < 0xFFFFFFFFull ? bigmin_env : 0;
+	// kRouteBoth: spans from bigmin up go to the blocks, the rest to windows;
+	// kRouteWindows: no block launch; kRouteBlocks: every windowed span goes to
+	// the blocks and the window kernel is not launched
+	P.bigmin = count >= 0xFFFFFFFFull || route == kRouteWindows ? 0
+	           : route == kRouteBlocks                          ? kSmallSpan + 1
+	                                                            : bigmin_env;
+	if (route == kRouteBlocks && P.bigmin == 0) route = kRouteWindows;
+	P.hstat = hstat;
 	P.hdr = reinterpret_cast<uint64_t*>(wp);      // [0..3]; [4..7]: k_scan scratch of the route's tile sums
 	P.tsum = reinterpret_cast<uint64_t*>(wp + 64);
 	P.incl = P.tsum + ntile + 1;
@@ -932,20 +1013,18 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	rp += al16(4 * count);
 	P.bctr = reinterpret_cast<uint32_t*>(rp);
 	P.nbctr = (uint32_t)(kPageCtrWords * grid);
-	// tile prefixes: each prep block sums its predecessors (up to 8192 tiles);
+	// tile prefixes: each prep block sums its predecessors (up to kScanTiles tiles);
 	// larger batches scan the tile sums first; batches of at most 8 tiles
 	// skip the count kernel (a prep block counts its predecessors' windows
 	// itself: one launch less, which is most of a small batch's latency)
-	P.scanned = ntile > 8192;
+	// (summing the predecessors costs each prep block O(tile) loads: past
+	// kScanTiles tiles one scan block is cheaper)
+	P.scanned = ntile > kScanTiles;
 	P.selfsum = ntile <= kSelfSumTiles;
 	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
-	if (P.scanned) {
-		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4);
-		if (P.bigmin) {  // scratch header and wave map (one wave)
-			k_scan<<<1, 1024, 0, stream>>>(P.bsum, ntile, reinterpret_cast<uint32_t*>(P.hdr + 6), 1, P.hdr + 4, 4, 4);
-			k_scan<<<1, 1024, 0, stream>>>(P.nsum, ntile, reinterpret_cast<uint32_t*>(P.hdr + 6), 1, P.hdr + 4, 4, 4);
-		}
-	}
+	if (P.scanned)
+		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4, P.bigmin ? P.bsum : nullptr,
+		                               P.bigmin ? P.nsum : nullptr);
 	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.bigmin) {
 		BigParams B{};
@@ -953,386 +1032,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 		B.out = out; B.ctr = P.bctr; B.tabs = tabs;
 		launch_bigblocks(B, num_cus, stream);
 	}
-	k_varlen7<<<(unsigned)grid, FDBCRC_V7_THREADS, 0, stream>>>(P);
-	return 0;
-}
-
-// ---------------------------------------------------------------------------
-// v8 (experiment, -DFDBCRC_VARLEN=8): the same window slots, streamed like the page kernel
-// ---------------------------------------------------------------------------
-// Status: bit-exact (the full -m gpu suite passes with it), but not faster
-// than v7: 1 MiB buffers (almost all PLAIN units, the page kernel's loop)
-// 0.222 vs 0.213 ms, chunks 0.235 vs 0.216 ms, zipf 0.438 vs 0.296 ms, 4 KiB
-// buffers 0.354 vs 0.225 ms.  Scalar metadata loads removed the vmcnt(0)
-// drains that vector metadata loads caused (174 -> 15), yet the plain path
-// stays at v7's ~4.9 TB/s while the page kernel reads the same 1 GiB at
-// ~6 TB/s: hipcc still waits for half of the next unit's loads before each
-// compute (vmcnt(4) where vmcnt(8) would do).  Kept for the next iteration,
-// not built by default.
-// v7 keeps a 64-slot table per wave in vector registers (155 VGPRs: 12 waves
-// per CU, one 4 KiB pass in flight per wave) and runs at ~5 TB/s even on
-// large buffers.  v8 moves the control to the scalar unit so the streaming
-// loop is the page kernel's: 1024-thread blocks (16 waves per CU, <= 128
-// VGPRs), two passes computed together (ILP 2) while the next two are in
-// flight -- 8 KiB per wave.
-//
-//  * A scalar CURSOR walks the wave's slot range [lo_s, hi_s) window by
-//    window: buffer j, window m, geometry from the buffer's offset/length
-//    (read with v_readlane from a 64-buffer metadata BATCH held in VGPRs; two
-//    batches, the next one loading while the cursor is in the current one).
-//    Buffers without windows (finished by prep) are skipped.
-//  * For every slot the cursor writes a RECORD into lane q of four record
-//    VGPRs (flags, buffer index, seed, windows remaining): the computing unit
-//    reads them back with v_readlane one unit later.  Lanes 0..7 / 8..15
-//    belong to the two units in flight.
-//  * The lead window zeroes its chunks before the buffer's first chunk (their
-//    loads are clamped to that chunk), masks the bytes before P0 and injects
-//    ~seed at P0 (crc32c.cpp:197: leading zeros are free); the last window
-//    masks the bytes after P1 in lane 63's chunk.  No prep-side edge terms.
-//  * Combining is scalar and per pass: the 16-lane team sums S_t (block
-//    layout, S_t = Rw_t * x^(8*1024*(3-t))) of one buffer add up normalised to
-//    the pass block's end; a buffer open across passes is carried by one
-//    multiply by x^(8*4096); a buffer finishing at team t is multiplied by
-//    x^(-8*(1024*(3-t) + zt)) (table corr).  Finished checksums collect in
-//    lanes and leave 64 at a time (plain stores; atomicXor for the parts of
-//    buffers split between waves, out[] zeroed by prep).
-constexpr uint32_t kV8Threads = 1024;
-constexpr uint32_t r8_VALID = 1u << 0;
-constexpr uint32_t r8_LEAD = 1u << 1;    // window 0: chunks before lo zeroed, seed injected at k0
-constexpr uint32_t r8_LAST = 1u << 2;    // the buffer's last window: tail mask zt, finish
-constexpr uint32_t r8_PSTART = 1u << 3;  // first window of the buffer's part in this wave
-constexpr uint32_t r8_PEND = 1u << 4;    // last slot of the wave, the buffer continues (rec_r: windows left)
-constexpr uint32_t r8_LO = 8;            // lo / 16 (6 bits)
-constexpr uint32_t r8_K0 = 16;           // P0 % 16 (4 bits)
-constexpr uint32_t r8_ZT = 20;           // trailing zeros (4 bits)
-
-// v in lane `lane` of `old` (uniform v and lane): a compare and a select
-__device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t lane, uint32_t old) {
-	return (threadIdx.x & 63) == lane ? v : old;
-}
-
-__global__ __launch_bounds__(kV8Threads) void k_varlen8(const V7Params P_) {
-	__shared__ uint32_t lds[kLdsBytesB / 4];
-	// kernel arguments as plain locals: the lambdas below capture by reference,
-	// and a captured struct would be copied to scratch (every use a VGPR load)
-	const DevTables* __restrict__ const T = P_.tabs;
-	const uint64_t count = P_.count, stride = P_.stride, length = P_.length;
-	const uint64_t* __restrict__ const offsets = P_.offsets;
-	const uint64_t* __restrict__ const lengths = P_.lengths;
-	const uint32_t* __restrict__ const seeds = P_.seeds;
-	const uint32_t seed = P_.seed;
-	const uint32_t* __restrict__ const gs = P_.gs;
-	uint32_t* const out = P_.out;
-	uint32_t* const dummy_base = P_.dummy;
-	const uint64_t* const hdr = P_.hdr;
-	const uint8_t* const pbase = P_.base;
-	typedef __attribute__((address_space(1))) const uint64_t g_u64;
-	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(hdr);
-	const uint64_t total = rdfirst64(hp[0]), Qs = rdfirst64(hp[1]);
-	const uint64_t w = (uint64_t)blockIdx.x * (kV8Threads / 64) + rdfirst(threadIdx.x >> 6);
-	const uint64_t lo_s = w * Qs;
-	if (lo_s >= total) {  // no slots: take part in the LDS fill's barrier and leave
-		fill_lds_b(lds, T);
-		return;
-	}
-	const uint64_t nslot = lo_s + Qs < total ? Qs : total - lo_s;
-	const LaneCtx c = make_ctx();
-	const int lane = c.lane;
-	const uint32_t col4 = (lane & 31) * 4;
-	const uint32_t c4 = col4 | 0x10000u;
-	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
-	const uint64_t base = reinterpret_cast<uint64_t>(pbase);
-
-	// ---- the buffer holding slot lo_s: the largest j with gs[j] <= lo_s (buffers
-	// without windows share the first slot of the next windowed buffer) ----
-	uint64_t j = 0;
-	{
-		uint64_t a = 0, n = count;  // answer in [a, a + n)
-		while (n > 1) {
-			const uint64_t stp = (n + 63) >> 6;
-			const uint64_t k = (uint64_t)lane * stp;
-			bool le = false;
-			if (k < n && k > 0) le = gld32(&gs[a + k]) <= (uint32_t)lo_s;
-			const uint64_t cnt = __builtin_popcountll(__ballot(le));
-			a += cnt * stp;
-			n = (cnt + 1) * stp <= n ? stp : n - cnt * stp;
-		}
-		j = rdfirst64(a);
-	}
-	const uint64_t j_first = j;
-
-	// ---- cursor (uniform) ----
-	// The cursor reads a buffer's offset/length/seed with SCALAR loads: the only
-	// vector loads in the streaming loop are the data loads, so the compiler's
-	// wait counting stays exact (vector metadata loads made it drain every load
-	// in flight -- vmcnt(0) -- at each use).
-	typedef __attribute__((address_space(4))) const uint64_t c_u64;
-	typedef __attribute__((address_space(4))) const uint32_t c_u32;
-	uint32_t W = 0, lo = 0, k0 = 0, zt = 0, s0 = 0;
-	uint64_t wb = 0, m = 0;
-	uint64_t rem = nslot;  // slots left to walk
-	auto enter = [&]() __attribute__((always_inline)) {  // geometry of buffer j; buffers without windows are skipped
-		for (;;) {
-			if (j >= count) {
-				W = 0;
-				return;
-			}
-			const uint64_t off = offsets ? *((c_u64*)reinterpret_cast<uintptr_t>(offsets + j)) : j * stride;
-			const uint64_t len = lengths ? *((c_u64*)reinterpret_cast<uintptr_t>(lengths + j)) : length;
-			const Geo7 g = geo7(base + off, len);
-			if (g.W) {
-				W = g.W;
-				lo = g.lo;
-				k0 = g.k0;
-				zt = g.zt;
-				wb = g.A - g.lo;
-				s0 = ~(seeds ? *((c_u32*)reinterpret_cast<uintptr_t>(seeds + j)) : seed);
-				return;
-			}
-			++j;
-		}
-	};
-	enter();
-	m = lo_s - *((c_u32*)reinterpret_cast<uintptr_t>(gs + j));
-	// empty slots (past the range's end) load the last chunk of the range's first
-	// window, which always holds bytes of its buffer (windows end at E)
-	const uint64_t safe_wa = wb + 1024 * m;
-	bool at_start = true;
-
-	uint32_t rec_f = 0, rec_j = 0, rec_s = 0, rec_r = 0;
-	// one window into record lane q; returns its address and the clamp of its loads
-	auto walk1 = [&](uint32_t q, uint64_t& wa, uint32_t& clamp) __attribute__((always_inline)) {
-		if (rem == 0 || W == 0) {
-			rec_f = wrlane(0u, q, rec_f);
-			wa = safe_wa;
-			clamp = 1008;
-			return;
-		}
-		const bool last = m + 1 == W;
-		// zt in every record: a part that ends with the wave (PEND) is moved to
-		// the buffer's end too, so it drops the same trailing zeros
-		const uint32_t f = r8_VALID | (m == 0 ? (r8_LEAD | ((lo >> 4) << r8_LO) | (k0 << r8_K0)) : 0u) |
-		                   ((m == 0 || at_start) ? r8_PSTART : 0u) | (last ? r8_LAST : 0u) | (zt << r8_ZT) |
-		                   ((rem == 1 && !last) ? r8_PEND : 0u);
-		rec_f = wrlane(f, q, rec_f);
-		rec_j = wrlane((uint32_t)(j - j_first), q, rec_j);
-		rec_s = wrlane(s0, q, rec_s);
-		rec_r = wrlane((uint32_t)(W - m - 1), q, rec_r);
-		wa = wb + 1024 * m;
-		clamp = m == 0 ? lo : 0u;
-		at_start = false;
-		--rem;
-		if (last) {
-			++j;
-			m = 0;
-			enter();
-		} else {
-			++m;
-		}
-	};
-
-	Block u0[2], u1[2];
-	// a unit: two passes of four windows; load k of a pass fetches team {0,2,1,3}[k].
-	// PLAIN unit: eight interior windows of one buffer whose part is already
-	// open (not its first or last window, not the wave's last slot): contiguous
-	// 8 KiB, no records, no masks, combined as two 4 KiB blocks.
-	auto load_unit = [&](Block (&u)[2], uint32_t q0, bool& plain) __attribute__((always_inline)) {
-		plain = rem > 8 && W != 0 && !at_start && m > 0 && m + 8 < W;
-		if (plain) {
-			const uint64_t wa0 = wb + 1024 * m;
-			m += 8;
-			rem -= 8;
-#pragma unroll
-			for (int p = 0; p < 2; ++p)
-#pragma unroll
-				for (int k = 0; k < 4; ++k) {
-					const int t = ((k & 1) << 1) | (k >> 1);
-					u[p].r[k] = ld16(reinterpret_cast<const uint8_t*>(wa0 + 4096 * p + 1024 * t + c.ld_off));
-				}
-			return;
-		}
-#pragma unroll
-		for (int p = 0; p < 2; ++p) {
-			uint64_t wa[4];
-			uint32_t cl[4];
-#pragma unroll
-			for (int t = 0; t < 4; ++t) walk1(q0 + 4 * p + t, wa[t], cl[t]);
-#pragma unroll
-			for (int k = 0; k < 4; ++k) {
-				const int t = ((k & 1) << 1) | (k >> 1);
-				const uint32_t off = c.ld_off > cl[t] ? c.ld_off : cl[t];
-				u[p].r[k] = ld16(reinterpret_cast<const uint8_t*>(wa[t] + off));
-			}
-		}
-	};
-	bool plainA = false, plainB = false;
-	load_unit(u0, 0, plainA);
-	fill_lds_b(lds, T);
-
-	// ---- combine state (uniform) ----
-	uint32_t acc = 0;
-	bool open = false, part_mid = false;  // part_mid: the open part began after the buffer's window 0
-	uint32_t mine = 0, myidx = 0, mysplit = 0;  // finished checksums: lane k holds the k-th
-	uint32_t nfin = 0;
-	uint32_t* const dummy = dummy_base + w * 64;
-	auto flush = [&]() __attribute__((always_inline)) {  // unconditional vector memory operations (dummy targets)
-		bool have = (uint32_t)lane < nfin;
-#ifdef FDBCRC_DEBUG
-		if (have && j_first + myidx >= count) {
-			if (atomicAdd(&g_dbg[2], 1ull) == 0) {
-				g_dbg[3] = j_first + myidx;
-				g_dbg[4] = 10;
-			}
-			have = false;
-		}
-#endif
-		const bool sp = have && mysplit;
-		*((have && !sp) ? out + j_first + myidx : dummy + lane) = mine;
-		atomicXor(sp ? out + j_first + myidx : dummy + lane, sp ? mine : 0u);
-		nfin = 0;
-	};
-	auto emit = [&](uint32_t jr, uint32_t v, bool split) __attribute__((always_inline)) {
-		mine = wrlane(v, nfin, mine);
-		myidx = wrlane(jr, nfin, myidx);
-		mysplit = wrlane(split ? 1u : 0u, nfin, mysplit);
-		if (++nfin == 64) flush();
-	};
-	auto combine_pass = [&](uint32_t R, uint32_t q0) __attribute__((always_inline)) {
-		if (open) acc = umul(T->block, acc);  // to this pass block's end
-#pragma unroll
-		for (int t = 0; t < 4; ++t) {
-			const uint32_t f = rdlane(rec_f, (int)(q0 + t));
-			if (!(f & r8_VALID)) continue;
-			uint32_t S = rdlane(R, 16 * t);
-			if (f & r8_PSTART) {
-				acc = 0;
-				part_mid = !(f & r8_LEAD);
-			}
-			// the seed's bytes past the lead chunk when that chunk ends the window:
-			// an XOR into the register at the window's end
-			if ((f & r8_LEAD) && ((f >> r8_LO) & 63u) == 63u && ((f >> r8_K0) & 15u) > 12u) {
-				const uint32_t kk = (f >> r8_K0) & 15u;
-				S ^= mul_xpow(T, rdlane(rec_s, (int)(q0 + t)) >> (8 * (16 - kk)), 1024 * (3 - t));
-			}
-			acc ^= S;
-			open = true;
-			if (f & (r8_LAST | r8_PEND)) {
-				uint32_t v = umul(T->corr[t][(f >> r8_ZT) & 15u], acc);
-				if (f & r8_PEND) v = mul_xpow(T, v, 1024 * (uint64_t)rdlane(rec_r, (int)(q0 + t)));
-				const bool split = part_mid || (f & r8_PEND);
-				emit(rdlane(rec_j, (int)(q0 + t)), part_mid ? v : ~v, split);  // window 0's part inverts
-				open = false;
-			}
-		}
-	};
-	auto compute_unit = [&](Block (&u)[2], uint32_t q0, bool plain) __attribute__((always_inline)) {
-		// edge masks: lead windows (chunks before lo, the lead chunk with the seed
-		// injected, the seed's spill into the next chunk) and last windows
-#pragma unroll
-		for (int p = 0; p < 2 && !plain; ++p) {
-			uint32_t fl[4];
-			uint32_t any = 0;
-#pragma unroll
-			for (int t = 0; t < 4; ++t) {
-				fl[t] = rdlane(rec_f, (int)(q0 + 4 * p + t));
-				any |= fl[t];
-			}
-			if (any & (r8_LEAD | r8_LAST)) {
-#pragma unroll
-				for (int k = 0; k < 4; ++k) {
-					const int t = ((k & 1) << 1) | (k >> 1);
-					const uint32_t f = fl[t];
-					if (f & r8_LEAD) {
-						const uint32_t lo16 = ((f >> r8_LO) & 63u) << 4, kk = (f >> r8_K0) & 15u;
-						const Masks mk = edge_masks(kk, 16u, rdlane(rec_s, (int)(q0 + 4 * p + t)));
-						const bool z = c.ld_off < lo16, ld = c.ld_off == lo16, sp = c.ld_off == lo16 + 16;
-#pragma unroll
-						for (int d = 0; d < 4; ++d) {
-							uint32_t v = z ? 0u : u[p].r[k][d];
-							v = ld ? ((v & mk.lm[d]) ^ mk.inj[d]) : v;
-							v ^= (sp && d == 0) ? mk.spill : 0u;
-							u[p].r[k][d] = v;
-						}
-					}
-					if ((f & r8_LAST) && ((f >> r8_ZT) & 15u)) {
-						uint32_t km[4];
-						keep_below7(16u - ((f >> r8_ZT) & 15u), km);
-#pragma unroll
-						for (int d = 0; d < 4; ++d) u[p].r[k][d] &= lane == 63 ? km[d] : ~0u;
-					}
-				}
-			}
-		}
-		unswizzle(u[0]);
-		unswizzle(u[1]);
-		uint32_t x0 = u[0].r[0][0], x1 = u[1].r[0][0];
-#pragma unroll
-		for (int wd = 0; wd < 16; ++wd) {
-			x0 = word_step4_next(lds, x0, wd < 15 ? u[0].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u, c4);
-			x1 = word_step4_next(lds, x1, wd < 15 ? u[1].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u, c4);
-		}
-		const uint32_t R0 = row_xor(mul_nibbles(lds, x0, c_lane));
-		const uint32_t R1 = row_xor(mul_nibbles(lds, x1, c_lane));
-		if (plain) {  // two whole 4 KiB blocks of the open part
-			const uint32_t B0 = rdlane(R0, 0) ^ rdlane(R0, 16) ^ rdlane(R0, 32) ^ rdlane(R0, 48);
-			const uint32_t B1 = rdlane(R1, 0) ^ rdlane(R1, 16) ^ rdlane(R1, 32) ^ rdlane(R1, 48);
-#ifdef FDBCRC_V8_NOUMUL  // timing experiment only: wrong results
-			acc ^= B0 ^ B1;
-#else
-			acc = umul(T->block, umul(T->block, acc) ^ B0) ^ B1;
-#endif
-			return;
-		}
-		combine_pass(R0, q0);
-		combine_pass(R1, q0 + 4);
-	};
-
-	const uint64_t nunit = (nslot + 7) >> 3;
-	// The explicit waits (vmcnt(8): the other unit's eight loads stay in flight)
-	// pin the wait-count state for the compiler, which otherwise drains half of
-	// the next unit's loads before every compute (the paths inside load_unit and
-	// the output flushes make its own count conservative).  A unit past the
-	// range's end has only empty slots: computing it is harmless.
-	for (uint64_t un = 0; un < nunit; un += 2) {
-		load_unit(u1, 8, plainB);
-		__builtin_amdgcn_sched_barrier(0);
-		__builtin_amdgcn_s_waitcnt(0x0F78);
-		compute_unit(u0, 0, plainA);
-		__builtin_amdgcn_sched_barrier(0);
-		load_unit(u0, 0, plainA);
-		__builtin_amdgcn_sched_barrier(0);
-		__builtin_amdgcn_s_waitcnt(0x0F78);
-		compute_unit(u1, 8, plainB);
-		__builtin_amdgcn_sched_barrier(0);
-	}
-	if (nfin) flush();
-}
-
-int launch_varlen8(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
-                   uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
-                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream) {
-	const uint64_t grid = (uint64_t)num_cus;
-	const uint64_t nwave = grid * (kV8Threads / 64);
-	const uint64_t ntile = (count + kTileW - 1) / kTileW;
-	uint8_t* wp = static_cast<uint8_t*>(ws);
-	V7Params P{};
-	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
-	P.seed = seed; P.seeds = seeds; P.out = out; P.tabs = tabs;
-	P.ntile = ntile; P.nwave = nwave; P.qalign = 8;
-	P.hdr = reinterpret_cast<uint64_t*>(wp);
-	P.tsum = reinterpret_cast<uint64_t*>(wp + 16);
-	P.incl = P.tsum + ntile + 1;
-	uint32_t* wave_tile = reinterpret_cast<uint32_t*>(P.incl + ntile + 1);
-	P.gs = wave_tile + nwave;
-	P.cl = nullptr;  // no prep-side lead terms
-	P.dummy = P.gs + 2 * count;
-	P.ctr = P.dummy + 64 * nwave;
-	P.scanned = ntile > 8192;
-	P.selfsum = ntile <= kSelfSumTiles;
-	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
-	if (P.scanned) k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 8, 8);
-	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
-	k_varlen8<<<(unsigned)grid, kV8Threads, 0, stream>>>(P);
+	if (route != kRouteBlocks) k_varlen7<<<(unsigned)grid, FDBCRC_V7_THREADS, 0, stream>>>(P);
 	return 0;
 }
 
@@ -1341,31 +1041,21 @@ int launch_varlen8(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 // ---------------------------------------------------------------------------
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) { return varlen7_workspace_bytes(count, nwave); }
 
-// Streaming kernel: v7 (default) or the v8 experiment (-DFDBCRC_VARLEN=8: correct,
-// measured slower -- DESIGN.md §3.2)
-#ifndef FDBCRC_VARLEN
-#define FDBCRC_VARLEN 7
-#endif
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
-                  hipStream_t stream) {
-#if FDBCRC_VARLEN == 8
-	return launch_varlen8(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream);
-#else
-	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream);
-#endif
+                  hipStream_t stream, int route, uint64_t* hstat) {
+	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream, route,
+	                      hstat);
 }
 
 // Fixed stride, any length and alignment: the same engine with metadata
-// computed on the fly.
+// computed on the fly.  The length is known here, so is the route: 16 KiB
+// or more (blocks waste at most 20 %) goes to the blocks, the rest to windows.
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
                          const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                          hipStream_t stream) {
-#if FDBCRC_VARLEN == 8
-	return launch_varlen8(base, nullptr, nullptr, stride, length, count, seed, seeds, out, tabs, num_cus, ws, stream);
-#else
-	return launch_varlen7(base, nullptr, nullptr, stride, length, count, seed, seeds, out, tabs, num_cus, ws, stream);
-#endif
+	return launch_varlen7(base, nullptr, nullptr, stride, length, count, seed, seeds, out, tabs, num_cus, ws, stream,
+	                      length >= 16384 ? kRouteBlocks : kRouteWindows, nullptr);
 }
 
 #ifdef FDBCRC_DEBUG
