@@ -143,7 +143,7 @@ def _spot_check(buf, offsets, lengths, seed, got, n=512):
 
 
 class VarLen:
-    kernel_name = "fdbcrc::k_varlen7 (+ k_v7count, k_v7prep)"
+    kernel_name = "varlen engine: fdbcrc::k_v7count + k_v7prep + the batch's route (k_bigblocks 4 KiB blocks and/or k_varlen7 1 KiB windows)"
 
     def __init__(self, dev, rank, lengths, align, desc, seed=0, metric=None, shape=None):
         self.dev, self.seed = dev, seed
@@ -193,7 +193,7 @@ class HostChunks:
     """configs[4], host-to-host: backup chunks in pinned host memory, checksummed
     through the pinned H2D -> kernel -> D2H pipeline (4 streams, 64 MiB segments).
     The rate includes both PCIe copies; it is PCIe-bound by design."""
-    kernel_name = "host pipeline (H2D + fdbcrc::k_varlen7 + D2H)"
+    kernel_name = "host pipeline (H2D + varlen engine + D2H)"
     metric = "host-to-host CRC32C GiB/s on 4 KiB-1 MiB chunk batches (pinned H2D + kernel + D2H); % of PCIe peak"
     host_timed = True
     pcie_peak_gbs = 63.0  # PCIe Gen5 x16 per direction, MI355X_MICROARCH.md
