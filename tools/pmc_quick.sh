@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmq
 for m in ${MODES:-chunks}; do
-  timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmq/$m -o sq -- python tools/pmc_probe.py $m > gpurun_out/pmq/$m.log 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc ${PMC:-GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAVE_CYCLES} --kernel-trace --output-format csv -d gpurun_out/pmq/$m -o sq -- python tools/pmc_probe.py $m > gpurun_out/pmq/$m.log 2>&1 || exit 1
   python - "$m" <<'PY'
 import csv, collections, glob, sys
 m = sys.argv[1]
