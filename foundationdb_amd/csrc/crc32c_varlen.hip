@@ -179,6 +179,18 @@ __device__ __forceinline__ uint32_t chain64_b(const uint32_t* lds, uint32_t s, c
 }
 __device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return (uint32_t)__shfl_up((int)v, d); }
 
+// Inclusive prefix sum of a 32-bit value over the wave on DPP (row shifts,
+// then the row broadcasts of lanes 15 and 31): six VALU adds, no LDS traffic.
+__device__ __forceinline__ uint32_t scan_add(uint32_t v) {
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+	v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+	return v;
+}
+
 // Inclusive prefix sum of a 64-bit value over the wave.
 __device__ __forceinline__ uint64_t scan64(uint64_t v, int lane) {
 #pragma unroll
@@ -352,33 +364,31 @@ __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_
 	len = P.lengths ? P.lengths[i] : P.length;
 }
 __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
-	__shared__ uint64_t part[3][4];
+	__shared__ uint32_t part[3][4];
 	const uint64_t i = (uint64_t)blockIdx.x * kTileW + threadIdx.x;
-	uint64_t W = 0, B = 0, N = 0;
+	uint32_t W = 0, B = 0, N = 0;
 	if (i < P.count) {
 		uint64_t off, len;
 		v7_buffer(P, i, off, len);
 		const Geo7 g = geo7(reinterpret_cast<uint64_t>(P.base) + off, len, P.bigmin);
 		W = g.W;
 		B = g.nb;
-		N = g.nb ? 1 : 0;
+		N = g.nb ? 1u : 0u;
 	}
-	for (int o = 32; o > 0; o >>= 1) {
-		W += __shfl_xor(W, o);
-		B += __shfl_xor(B, o);
-		N += __shfl_xor(N, o);
-	}
-	if ((threadIdx.x & 63) == 0) {
+	W = scan_add(W);
+	B = scan_add(B);
+	N = scan_add(N);
+	if ((threadIdx.x & 63) == 63) {
 		part[0][threadIdx.x >> 6] = W;
 		part[1][threadIdx.x >> 6] = B;
 		part[2][threadIdx.x >> 6] = N;
 	}
 	__syncthreads();
 	if (threadIdx.x == 0) {
-		P.tsum[blockIdx.x] = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+		P.tsum[blockIdx.x] = (uint64_t)part[0][0] + part[0][1] + part[0][2] + part[0][3];
 		if (P.bigmin) {
-			P.bsum[blockIdx.x] = part[1][0] + part[1][1] + part[1][2] + part[1][3];
-			P.nsum[blockIdx.x] = part[2][0] + part[2][1] + part[2][2] + part[2][3];
+			P.bsum[blockIdx.x] = (uint64_t)part[1][0] + part[1][1] + part[1][2] + part[1][3];
+			P.nsum[blockIdx.x] = (uint64_t)part[2][0] + part[2][1] + part[2][2] + part[2][3];
 		}
 	}
 }
@@ -386,13 +396,21 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	__shared__ uint32_t s4[4][256];  // slice4 tables (no bank replication: this kernel is not LDS-bound)
 	__shared__ uint32_t wsum[3][4];
-	__shared__ uint64_t s_pre[3][4];
+	__shared__ uint32_t s_pre[3][4];
 	__shared__ uint64_t s_stat[4][3];
 	const DevTables* T = P.tabs;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
 	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = T->slice4[k][threadIdx.x];
 	const uint32_t tile = blockIdx.x;
+	// this thread's buffer: its metadata and seed loads go out first, so their
+	// latency overlaps the tile-prefix loads below
+	const uint64_t i = (uint64_t)tile * kTileW + threadIdx.x;
+	const bool ok = i < P.count;
+	uint64_t off = 0, len = 0;
+	v7_buffer(P, ok ? i : P.count - 1, off, len);
+	const uint32_t sdv = P.seeds ? P.seeds[ok ? i : P.count - 1] : P.seed;
+	if (!ok) len = 0;
 #if FDBCRC_V7_RANGES > 1
 	if (tile == 0)
 		for (uint64_t k = threadIdx.x; k < P.nwave / kV7RangesPerBlock; k += 256) P.ctr[k] = 0;
@@ -401,14 +419,15 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		for (uint32_t k = threadIdx.x; k < P.nbctr; k += 256) P.bctr[k] = 0;
 	// exclusive prefixes of this tile (window slots, route blocks, route
 	// entries): the sums of all earlier tiles, read in parallel by the whole
-	// block (no inter-block waiting)
-	uint64_t pre = 0, preB = 0, preN = 0;
+	// block (no inter-block waiting).  Every total is below 2^32 (the engine's
+	// slot limit), so the sums are 32-bit.
+	uint32_t pre = 0, preB = 0, preN = 0;
 	if (P.scanned) {
 		if (threadIdx.x == 0) {
-			pre = P.tsum[tile];
+			pre = (uint32_t)P.tsum[tile];
 			if (P.bigmin) {
-				preB = P.bsum[tile];
-				preN = P.nsum[tile];
+				preB = (uint32_t)P.bsum[tile];
+				preN = (uint32_t)P.nsum[tile];
 			}
 		}
 	} else if (P.selfsum) {
@@ -424,38 +443,32 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		// eight tile sums per thread in flight at once (one load latency per
 		// 2048 predecessor tiles, not one per 256)
 		for (uint32_t k0 = threadIdx.x; k0 < tile; k0 += 8 * blockDim.x) {
-			uint64_t v[8], vB[8], vN[8];
+			uint32_t v[8], vB[8], vN[8];
 #pragma unroll
 			for (uint32_t u = 0; u < 8; ++u) {
 				const uint32_t k = k0 + u * blockDim.x;
 				const uint32_t kc = k < tile ? k : 0;
-				v[u] = gld64(P.tsum + kc);
-				vB[u] = P.bigmin ? gld64(P.bsum + kc) : 0;
-				vN[u] = P.bigmin ? gld64(P.nsum + kc) : 0;
+				v[u] = (uint32_t)gld64(P.tsum + kc);
+				vB[u] = P.bigmin ? (uint32_t)gld64(P.bsum + kc) : 0u;
+				vN[u] = P.bigmin ? (uint32_t)gld64(P.nsum + kc) : 0u;
 			}
 #pragma unroll
 			for (uint32_t u = 0; u < 8; ++u) {
 				const bool in = k0 + u * blockDim.x < tile;
-				pre += in ? v[u] : 0;
-				preB += in ? vB[u] : 0;
-				preN += in ? vN[u] : 0;
+				pre += in ? v[u] : 0u;
+				preB += in ? vB[u] : 0u;
+				preN += in ? vN[u] : 0u;
 			}
 		}
 	}
-	for (int o = 32; o > 0; o >>= 1) {
-		pre += __shfl_xor(pre, o);
-		preB += __shfl_xor(preB, o);
-		preN += __shfl_xor(preN, o);
-	}
+	pre = rdlane(scan_add(pre), 63);
+	preB = rdlane(scan_add(preB), 63);
+	preN = rdlane(scan_add(preN), 63);
 	if (lane == 0) {
 		s_pre[0][wv] = pre;
 		s_pre[1][wv] = preB;
 		s_pre[2][wv] = preN;
 	}
-	const uint64_t i = (uint64_t)tile * kTileW + threadIdx.x;
-	const bool ok = i < P.count;
-	uint64_t off = 0, len = 0;
-	if (ok) v7_buffer(P, i, off, len);
 	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
 	const Geo7 g = geo7(P0, len, P.bigmin);
 	const uint32_t W = ok ? g.W : 0u, B = ok ? g.nb : 0u, N = (ok && g.nb) ? 1u : 0u;
@@ -470,17 +483,7 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 #pragma unroll
 			for (int k = 0; k < 3; ++k) s_stat[wv][k] = c[k];
 	}
-	uint32_t incl = W, inclB = B, inclN = N;
-	for (int d = 1; d < 64; d <<= 1) {
-		const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-		const uint32_t yB = (uint32_t)__shfl_up((int)inclB, d);
-		const uint32_t yN = (uint32_t)__shfl_up((int)inclN, d);
-		if (lane >= d) {
-			incl += y;
-			inclB += yB;
-			inclN += yN;
-		}
-	}
+	const uint32_t incl = scan_add(W), inclB = scan_add(B), inclN = scan_add(N);
 	if (lane == 63) {
 		wsum[0][wv] = incl;
 		wsum[1][wv] = inclB;
@@ -496,9 +499,9 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		inN += k < wv ? wsum[2][k] : 0u;
 		aggN += wsum[2][k];
 	}
-	const uint32_t excl = (uint32_t)(s_pre[0][0] + s_pre[0][1] + s_pre[0][2] + s_pre[0][3]);
-	const uint64_t exclB = s_pre[1][0] + s_pre[1][1] + s_pre[1][2] + s_pre[1][3];
-	const uint64_t exclN = s_pre[2][0] + s_pre[2][1] + s_pre[2][2] + s_pre[2][3];
+	const uint32_t excl = s_pre[0][0] + s_pre[0][1] + s_pre[0][2] + s_pre[0][3];
+	const uint32_t exclB = s_pre[1][0] + s_pre[1][1] + s_pre[1][2] + s_pre[1][3];
+	const uint32_t exclN = s_pre[2][0] + s_pre[2][1] + s_pre[2][2] + s_pre[2][3];
 	if (threadIdx.x == 0) {
 		if (tile == 0 && P.hstat)
 			for (int k = 0; k < 3; ++k) P.hstat[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
@@ -509,14 +512,14 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 			q = q < P.qalign ? P.qalign : (q + P.qalign - 1) & ~uint64_t(P.qalign - 1);
 			P.hdr[0] = total;
 			P.hdr[1] = q;
-			P.hdr[2] = exclB + aggB;
-			P.hdr[3] = exclN + aggN;
+			P.hdr[2] = (uint64_t)exclB + aggB;
+			P.hdr[3] = (uint64_t)exclN + aggN;
 		}
 	}
 	if (!ok) return;
 	const uint32_t gi = excl + inwave + incl - W;
 	P.gs[i] = gi;
-	const uint32_t s0 = ~(P.seeds ? P.seeds[i] : P.seed);
+	const uint32_t s0 = ~sdv;
 	if (g.nb) {
 		// block route: the buffer's entry; out[] starts at ~0 (the final
 		// inversion) and every block XORs its weighted register in
