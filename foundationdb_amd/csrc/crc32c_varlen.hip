@@ -672,17 +672,23 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	uint32_t B_cl;
 	uint32_t Gb1 = 0;       // wave-relative end of the batch's slots
 	uint64_t p_shift = 0;   // bytes from the end of the wave's last window to its buffer's end
+	// The metadata of the next 64-buffer batch is loaded one batch ahead: when
+	// build() consumes it, the loads have long returned, so they never make the
+	// table build wait for the data loads in flight (vmcnt is in order).
+	uint64_t pf_off = 0, pf_len = 0;
+	uint32_t pf_g = 0, pf_cl = 0;
+	auto prefetch = [&](uint64_t bi0) {  // unconditional, clamped into the batch
+		const uint64_t j = bi0 + lane < P.count ? bi0 + lane : P.count - 1;
+		v7_buffer(P, j, pf_off, pf_len);
+		pf_g = gld32(P.gs + j);
+		pf_cl = gld32(P.cl + j);
+	};
 	auto build = [&]() {
 		const uint64_t bi0 = nb_bi0;
 		const uint64_t j = bi0 + lane;
 		const bool ok = j < P.count;
-		uint64_t off = 0, len = 0;
-		uint32_t g = 0xFFFFFFFFu, cl = 0;
-		if (ok) {
-			v7_buffer(P, j, off, len);
-			g = P.gs[j];
-			cl = P.cl[j];
-		}
+		const uint64_t off = pf_off, len = ok ? pf_len : 0;
+		const uint32_t g = ok ? pf_g : 0xFFFFFFFFu, cl = ok ? pf_cl : 0u;
 		const Geo7 ge = geo7(reinterpret_cast<uint64_t>(P.base) + off, len, P.bigmin);
 		const uint32_t W = ok ? ge.W : 0u;
 		B_bi0 = bi0;
@@ -692,15 +698,12 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		B_f = ge.lo | (ge.zt << k7_ZT);
 		B_cl = cl;
 		nb_bi0 = bi0 + 64;
-		// end of the slots of this batch (pieces are in order; W = 0 pieces add nothing)
-		const uint32_t e = ok ? g + W : 0u;
-		uint32_t emax = e;
-#pragma unroll
-		for (int d = 32; d > 0; d >>= 1) {
-			const uint32_t y = (uint32_t)__shfl_xor((int)emax, d);
-			emax = y > emax ? y : emax;
-		}
-		emax = rdfirst(emax);
+		prefetch(nb_bi0 < P.count ? nb_bi0 : bi0);
+		// end of the slots of this batch: g + W is non-decreasing over the
+		// batch's buffers (pieces are in order; W = 0 pieces add nothing), so it
+		// is the last buffer's
+		const uint64_t nv = P.count - bi0;
+		const uint32_t emax = rdlane(g + W, nv < 64 ? (int)nv - 1 : 63);
 		Gb1 = (emax > hi_s ? hi_s : emax) - lo_s;
 		if (emax < lo_s) Gb1 = 0;
 		more = nb_bi0 < P.count && emax < hi_s;
@@ -924,6 +927,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	t1.S = 0;
 	t1.em = ~0ull;
 	phase1(t1, 0);
+	prefetch(nb_bi0);
 	build();
 	uint32_t sb = 0;
 	uint32_t f0 = build_table(t0, 0);
