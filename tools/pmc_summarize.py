@@ -14,23 +14,40 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(mode, kernel_substrs):
-    """Per counter: the sum over the step's kernels (every kernel whose name
-    holds one of kernel_substrs) of that kernel's mean value per launch."""
-    agg = collections.defaultdict(list)
-    durs = collections.defaultdict(list)
+    """Per counter: its total over the step's kernels (every kernel whose name
+    holds one of kernel_substrs) per step.  A step may run a kernel only
+    sometimes (the varlen engine picks its route per batch, from the previous
+    batch's statistics), so each pass is cut into steps by its most-launched
+    kernel, the first step (the route not yet adapted) is dropped, and the
+    totals of the remaining dispatches are divided by their step count."""
+    sums = collections.defaultdict(float)
+    dur = 0.0
+    npass = 0
+    launches = 0
     for f in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "pmc", mode, "*_counter_collection.csv"))):
-        for r in csv.DictReader(open(f)):
-            if any(k in r["Kernel_Name"] for k in kernel_substrs):
-                agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
-        for t in csv.DictReader(open(f.replace("counter_collection", "kernel_trace"))):
-            if any(k in t["Kernel_Name"] for k in kernel_substrs):
-                durs[t["Kernel_Name"]].append((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) * 1e-9)
-    mean = collections.defaultdict(float)
-    for (_, counter), v in agg.items():
-        mean[counter] += sum(v) / len(v)
-    dur = sum(sum(v) / len(v) for v in durs.values())
-    launches = max(len(v) for v in durs.values())
-    return dict(mean), dur, launches
+        rows = [r for r in csv.DictReader(open(f)) if any(k in r["Kernel_Name"] for k in kernel_substrs)]
+        trace = [t for t in csv.DictReader(open(f.replace("counter_collection", "kernel_trace")))
+                 if any(k in t["Kernel_Name"] for k in kernel_substrs)]
+        if not rows:
+            continue
+        per_kernel = collections.defaultdict(set)
+        for r in rows:
+            per_kernel[r["Kernel_Name"]].add(int(r["Dispatch_Id"]))
+        marker = max(per_kernel.values(), key=len)
+        ids = sorted(marker)
+        cut = ids[1] if len(ids) > 1 else ids[0]
+        steps = len(ids) - 1 if len(ids) > 1 else 1
+        counters = collections.defaultdict(float)
+        for r in rows:
+            if int(r["Dispatch_Id"]) >= cut:
+                counters[r["Counter_Name"]] += float(r["Counter_Value"])
+        for c, v in counters.items():
+            sums[c] += v / steps
+        dur += sum((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) * 1e-9 for t in trace
+                   if int(t["Dispatch_Id"]) >= cut) / steps
+        npass += 1
+        launches = max(launches, steps)
+    return dict(sums), dur / max(npass, 1), launches
 
 
 def main(mode="pages4k", workload="pages4k", kernel=("k_pages4k",), algorithmic=(1 << 20) * 4100, units=1 << 20):
