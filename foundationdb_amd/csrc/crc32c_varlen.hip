@@ -268,7 +268,10 @@ constexpr uint32_t kTileW = 256;
 #define FDBCRC_V7_RANGES 1
 #endif
 constexpr uint64_t kV7RangesPerBlock = (FDBCRC_V7_THREADS / 64) * FDBCRC_V7_RANGES;
-constexpr uint64_t kSelfSumTiles = 8;
+#ifndef FDBCRC_SELFSUM_TILES
+#define FDBCRC_SELFSUM_TILES 8
+#endif
+constexpr uint64_t kSelfSumTiles = FDBCRC_SELFSUM_TILES;
 #ifndef FDBCRC_SCAN_TILES
 #define FDBCRC_SCAN_TILES 8192
 #endif
@@ -431,13 +434,24 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 			}
 		}
 	} else if (P.selfsum) {
-		for (uint64_t j = threadIdx.x; j < (uint64_t)tile * kTileW; j += blockDim.x) {
-			uint64_t o, l;
-			v7_buffer(P, j, o, l);
-			const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o, l, P.bigmin);
-			pre += gj.W;
-			preB += gj.nb;
-			preN += gj.nb ? 1u : 0u;
+		// the predecessors' geometry recomputed here, eight buffers per thread
+		// in flight at once
+		const uint64_t n = (uint64_t)tile * kTileW;
+		for (uint64_t j0 = threadIdx.x; j0 < n; j0 += 8 * blockDim.x) {
+			uint64_t o[8], l[8];
+#pragma unroll
+			for (uint32_t u = 0; u < 8; ++u) {
+				const uint64_t j = j0 + u * blockDim.x;
+				v7_buffer(P, j < n ? j : 0, o[u], l[u]);
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < 8; ++u) {
+				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o[u], l[u], P.bigmin);
+				const bool in = j0 + u * blockDim.x < n;
+				pre += in ? gj.W : 0u;
+				preB += in ? gj.nb : 0u;
+				preN += in && gj.nb ? 1u : 0u;
+			}
 		}
 	} else {
 		// eight tile sums per thread in flight at once (one load latency per

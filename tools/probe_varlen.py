@@ -48,5 +48,7 @@ run("small: 4096 x 1000", [4096] * 1000, 4096, reps=200)
 run("small: 1500 x 10000", [1500] * 10000, 2048, reps=200)
 run("small: 600 x 2000", [600] * 2000, 1024, reps=200)
 run("chunks", W.chunk_lengths(), 4096)
+run("16 KiB x 8K", [16384] * 8192, 4096)
+run("2 KiB x 16K", [2048] * 16384, 2048, reps=50)
 run("one route buffer 100000", [100000], 4096, reps=200)
 run("route 64 KiB x 16K", [65536] * (1 << 14), 4096)
