@@ -290,12 +290,15 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
 	return ((uint64_t)shfl32((uint32_t)(v >> 32), src) << 32) | shfl32((uint32_t)v, src);
 }
 // Inclusive prefix XOR over the wave.
+// (DPP row shifts and row broadcasts, like scan_add: no LDS round trips)
 __device__ __forceinline__ uint32_t scanx(uint32_t v, int lane) {
-#pragma unroll
-	for (int d = 1; d < 64; d <<= 1) {
-		const uint32_t y = shup(v, d);
-		if (lane >= d) v ^= y;
-	}
+	(void)lane;
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
 	return v;
 }
 // Byte mask of a 16-byte chunk keeping bytes < k1 (1..15).
