@@ -69,6 +69,17 @@ public:
 		stepToKey.erase(it->second);
 		keyToStep.erase(it);
 	}
+	// Pages from the least recently used on (leastRecentlyUsedPage, :168-173,
+	// walked forward), stopping before the first page `stop` rejects.
+	template <class Stop>
+	uint64_t lru_order(uint32_t* out, uint64_t cap, Stop stop) const {
+		uint64_t n = 0;
+		for (auto it = stepToKey.begin(); it != stepToKey.end() && n < cap; ++it) {
+			if (stop(it->second)) break;
+			out[n++] = it->second;
+		}
+		return n;
+	}
 
 private:
 	uint64_t step = 0;
@@ -413,6 +424,17 @@ int fdb_wc_stats(fdb_write_checker* wc, uint64_t* checked_succeed, uint64_t* che
 	if (checked_fail) *checked_fail = wc->failed;
 	if (history_size) *history_size = (uint64_t)wc->lru.size();
 	if (writing) *writing = wc->writing.size();
+	return 0;
+}
+
+// The batched form of the reference's sweep actor (AsyncFileWriteChecker.h:218-232),
+// which re-reads the least recently used page and waits while it is being
+// written: the next pages it would visit, in that order, up to the first page
+// being written.
+int fdb_wc_sweep_pages(fdb_write_checker* wc, uint32_t* pages_out, uint64_t cap, uint64_t* n) {
+	if (!wc || !n || (cap && !pages_out)) return fdbcrc::set_error(FDB_CRC32C_EINVAL, "fdb_wc: null argument", hipSuccess);
+	if (int rc = wc->drain()) return rc;
+	*n = wc->lru.lru_order(pages_out, cap, [&](uint32_t p) { return wc->writing.count(p) != 0; });
 	return 0;
 }
 

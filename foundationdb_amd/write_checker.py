@@ -34,6 +34,7 @@ def _lib():
             "fdb_wc_wait": ([vp, u64], ctypes.c_int),
             "fdb_wc_stats": ([vp, P(u64), P(u64), P(u64), P(u64)], ctypes.c_int),
             "fdb_wc_history": ([vp, u32, P(u32), P(u64)], ctypes.c_int),
+            "fdb_wc_sweep_pages": ([vp, vp, u64, P(u64)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -123,6 +124,13 @@ class WriteChecker:
         v = [ctypes.c_uint64() for _ in range(4)]
         _check(_lib().fdb_wc_stats(self.h, *[ctypes.byref(x) for x in v]), "fdb_wc_stats")
         return {"succeed": v[0].value, "fail": v[1].value, "history": v[2].value, "writing": v[3].value}
+
+    def sweep_pages(self, cap=1024):
+        """Pages the reference's sweep actor should re-read next (fdb_wc_sweep_pages)."""
+        buf = np.zeros(max(cap, 1), np.uint32)
+        n = ctypes.c_uint64()
+        _check(_lib().fdb_wc_sweep_pages(self.h, buf.ctypes.data, cap, ctypes.byref(n)), "fdb_wc_sweep_pages")
+        return [int(x) for x in buf[:n.value]]
 
     def history_entry(self, page):
         c, t = ctypes.c_uint32(), ctypes.c_uint64()

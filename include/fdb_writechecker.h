@@ -75,6 +75,18 @@ int fdb_wc_poll(fdb_write_checker* wc, uint64_t* applied);
 /* Block until `ticket` (and everything before it) is applied. */
 int fdb_wc_wait(fdb_write_checker* wc, uint64_t ticket);
 
+/* Sweep: the reference's background actor (fdbrpc/AsyncFileWriteChecker.h:218-232)
+ * re-reads the least recently used history page, waiting while that page is
+ * being written.  As written it reads offset page*4096, one page past the
+ * 1-based page's bytes [(page-1)*4096, page*4096), and a 4096-byte read there
+ * covers no full page by updateChecksumHistory's rule (pageEnd excludes the
+ * last full page, :287-297), so it verifies nothing.  This call gives the
+ * pages such a sweep should visit, in its order: from the least recently used
+ * on, stopping before the first page being written; the caller reads each
+ * page's bytes [(page-1)*4096, page*4096) -- in one batch, e.g. with the
+ * pipeline or a device read -- and passes them to fdb_wc_read /
+ * fdb_wc_read_device, which verify synced pages and drop the verified ones. */
+int fdb_wc_sweep_pages(fdb_write_checker* wc, uint32_t* pages_out, uint64_t cap, uint64_t* n);
 /* Counters and history inspection. */
 int fdb_wc_stats(fdb_write_checker* wc, uint64_t* checked_succeed, uint64_t* checked_fail, uint64_t* history_size,
                  uint64_t* writing);

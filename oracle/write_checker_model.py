@@ -132,3 +132,15 @@ class WriteCheckerModel:
 
     def history(self):
         return {p: self.lru.find(p) for p in self.lru.key_to_step}
+
+    def sweep_pages(self, cap):
+        """Pages the sweep actor (AsyncFileWriteChecker.h:218-232) visits next:
+        from the least recently used on (leastRecentlyUsedPage, :168-173),
+        stopping where it would wait for a page being written."""
+        out = []
+        for step in sorted(self.lru.step_to_key):
+            p = self.lru.step_to_key[step]
+            if p in self.writing or len(out) == cap:
+                break
+            out.append(p)
+        return out

@@ -61,6 +61,7 @@ def replay(ops, budget, native_factory):
             nat.truncate(off)
         st = nat.stats()
         assert (st["succeed"], st["fail"], st["history"]) == (model.succeed, model.failed, model.lru.size())
+        assert nat.sweep_pages(37) == model.sweep_pages(37)
     hist = model.history()
     for p in range(1, FILE_PAGES + 2):
         assert nat.history_entry(p) == (hist.get(p))
@@ -89,6 +90,39 @@ def test_reference_quirks_kept():
     assert c.write(np.ones(3 * 4096, np.uint8), 4096, 5) == [2, 3]
     c.truncate(3 * 4096)
     assert c.stats()["history"] == 1 and c.history_entry(2) is not None
+    c.close()
+
+
+def test_sweep_order_and_batched_verification():
+    """fdb_wc_sweep_pages lists history pages from the least recently used on
+    and stops at a page being written (where the reference's sweep actor
+    waits); reading the listed pages' bytes verifies them in one batch: synced
+    pages that match leave the history, a lost write is reported.  The
+    reference's own sweep reads offset page*4096, whose 4096 bytes hold no
+    full page by updateChecksumHistory's rule: it verifies nothing."""
+    import foundationdb_amd.write_checker as W
+    W.reset_budget()
+    c = W.WriteChecker(1000, gpu_threshold=0)
+    rng = np.random.default_rng(4)
+    data = rng.integers(0, 256, 64 * 4096, dtype=np.uint8)
+    pages = c.write(data[:20 * 4096], 0, 10)  # pages 1..19 (the last full page is left out)
+    c.write_done(pages)
+    late = c.write(data[30 * 4096:34 * 4096], 30 * 4096, 11)  # pages 31..33, still being written
+    assert c.sweep_pages(100) == list(range(1, 20))
+    assert c.sweep_pages(5) == [1, 2, 3, 4, 5]
+    c.write_done(late)
+    assert c.sweep_pages(100) == list(range(1, 20)) + late
+    c.sync(12)
+    # the reference's sweep read for page 1: offset 4096, 4096 bytes -> no full page checked
+    assert c.read(data[4096:8192], 4096) == 0 and c.stats()["history"] == 22
+    # the batched sweep: bytes [(p-1)*4096, p*4096) of pages 1..19 in one read, page 7 lost
+    disk = data[:20 * 4096].copy()
+    disk[6 * 4096 + 100] ^= 1
+    failures = c.read(disk, 0)
+    assert failures == 1
+    st = c.stats()
+    assert st["fail"] == 1 and st["succeed"] == 18
+    assert c.sweep_pages(100)[0] == 7  # the lost write stays in the history
     c.close()
 
 
