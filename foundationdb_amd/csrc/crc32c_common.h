@@ -82,6 +82,42 @@ __device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t
 	__syncthreads();
 }
 
+// The same fill split in two for 1024-thread workgroups, so a kernel can put
+// the table loads in flight first and write them to LDS once its own start-up
+// loads have returned: fill_issue_1024 loads each thread's share (8 slicing
+// quads' values, 2 lane-table quads), fill_commit_1024 writes them and syncs.
+struct FillRegs {
+	uint32_t v[8];
+	u32x4 lv[2];
+};
+__device__ __forceinline__ void fill_issue_1024(FillRegs& R, const DevTables* __restrict__ t) {
+	typedef __attribute__((address_space(1))) const uint32_t g_u32;
+	auto gl = [](const uint32_t* p) -> uint32_t { return *((g_u32*)reinterpret_cast<uintptr_t>(p)); };
+	const uint32_t* s4 = &t->slice4[0][0];
+	const uint32_t* ln = &t->lane[0][0][0];
+#pragma unroll
+	for (uint32_t i = 0; i < 8; ++i) {
+		const uint32_t W = 4 * (threadIdx.x + i * 1024);
+		const uint32_t pair = (W & 16383u) >> 5;
+		R.v[i] = gl(s4 + (((W >> 14) * 2 + (pair & 1)) << 8) + (pair >> 1));
+	}
+#pragma unroll
+	for (uint32_t i = 0; i < 2; ++i) {
+		const uint32_t V = 4 * (threadIdx.x + i * 1024);
+		const uint32_t nv = (V >> 5) & 127u, l = (V >> 12) * 32 + (V & 31u);
+#pragma unroll
+		for (uint32_t e = 0; e < 4; ++e) R.lv[i][e] = gl(ln + (l + e) * 128 + nv);
+	}
+}
+__device__ __forceinline__ void fill_commit_1024(const FillRegs& R, uint32_t* lds) {
+	u32x4* q4 = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+	for (uint32_t i = 0; i < 8; ++i) q4[(kS4Off / 16) + threadIdx.x + i * 1024] = u32x4{R.v[i], R.v[i], R.v[i], R.v[i]};
+#pragma unroll
+	for (uint32_t i = 0; i < 2; ++i) q4[(kS4LaneOff / 16) + threadIdx.x + i * 1024] = R.lv[i];
+	__syncthreads();
+}
+
 struct LaneCtx {
 	uint32_t ld_off;   // byte offset of this lane's first 16 B load inside a block
 	int lane;

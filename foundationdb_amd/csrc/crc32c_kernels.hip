@@ -267,6 +267,10 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	typedef __attribute__((address_space(1))) const uint32_t g_u32;
 	auto gl32 = [](const uint32_t* p) -> uint32_t { return *((g_u32*)reinterpret_cast<uintptr_t>(p)); };
 	auto gl64 = [](const uint64_t* p) -> uint64_t { return *((g_u64*)reinterpret_cast<uintptr_t>(p)); };
+	// the LDS table loads go out first: they return while the header, the
+	// entry search and the window load (dependent round trips) proceed
+	FillRegs fill;
+	fill_issue_1024(fill, P.tabs);
 	const uint64_t count = rdfirst64(gl64(P.hdr + 2));  // blocks
 	if (count == 0) return;
 	const uint64_t nbig = rdfirst64(gl64(P.hdr + 3));   // entries
@@ -307,20 +311,33 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		wj = j0;
 	};
 	// the entry holding block b: the last q with es[q] <= b (64-ary narrowing)
+	// (256-ary narrowing: four samples per lane per round trip -- two rounds
+	// up to 16 Ki entries, three up to 4 Mi)
 	auto find = [&](uint32_t b) -> uint64_t {
 		uint64_t q0 = 0, n = nbig;  // es[q0] <= b
-		while (n > 64) {
-			const uint64_t stp = (n + 63) >> 6;
-			const uint64_t k = (uint64_t)lane * stp;
-			const uint32_t v = gl32(P.es + q0 + (k < n ? k : 0));
-			const bool le = k < n && v <= b;
-			const uint64_t cnt = __builtin_popcountll(__ballot(le));
+		for (;;) {
+			if (n <= 64) {
+				const uint32_t v = gl32(P.es + q0 + (lane < n ? lane : 0));
+				const bool le = lane < n && v <= b;
+				return q0 + __builtin_popcountll(__ballot(le)) - 1;
+			}
+			const uint64_t stp = (n + 255) >> 8;
+			uint32_t v[4];
+#pragma unroll
+			for (uint32_t u = 0; u < 4; ++u) {
+				const uint64_t k = (4 * (uint64_t)lane + u) * stp;
+				v[u] = gl32(P.es + q0 + (k < n ? k : 0));
+			}
+			uint64_t cnt = 0;
+#pragma unroll
+			for (uint32_t u = 0; u < 4; ++u) {
+				const uint64_t k = (4 * (uint64_t)lane + u) * stp;
+				cnt += __builtin_popcountll(__ballot(k < n && v[u] <= b));
+			}
+			if (stp == 1) return q0 + cnt - 1;
 			q0 += (cnt - 1) * stp;
 			n = n - (cnt - 1) * stp < stp ? n - (cnt - 1) * stp : stp;
 		}
-		const uint32_t v = gl32(P.es + q0 + (lane < n ? lane : 0));
-		const bool le = lane < n && v <= b;
-		return q0 + __builtin_popcountll(__ballot(le)) - 1;
 	};
 
 	// ---- per-grab metadata (wave-uniform) ----------------------------------
@@ -490,8 +507,8 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	meta_of(gA, MA);
 	meta_of(gB, MB);
 	Block u0[U], u1[U];
-	load_u(u0, MA, 0);  // in flight during the LDS fill
-	fill_lds_b(lds, T);
+	load_u(u0, MA, 0);  // in flight while the tables are written
+	fill_commit_1024(fill, lds);
 	uint32_t f = 0;
 	// one grab: X is its metadata, Y the next grab's (its first unit is
 	// loaded here), rebuilt for the grab after it

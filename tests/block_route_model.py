@@ -52,15 +52,17 @@ class Wave:
         self.load_window(self.find(first_block))
 
     def find(self, b):
-        """Last q with es[q] <= b (the kernel's 64-ary narrowing)."""
+        """Last q with es[q] <= b (the kernel's 256-ary narrowing, four samples per lane)."""
         q0, n = 0, self.nbig
-        while n > 64:
-            stp = (n + 63) // 64
-            cnt = sum(1 for lane in range(64) if lane * stp < n and self.es[q0 + lane * stp] <= b)
+        while True:
+            if n <= 64:
+                return q0 + sum(1 for lane in range(n) if self.es[q0 + lane] <= b) - 1
+            stp = (n + 255) // 256
+            cnt = sum(1 for s in range(256) if s * stp < n and self.es[q0 + s * stp] <= b)
+            if stp == 1:
+                return q0 + cnt - 1
             q0 += (cnt - 1) * stp
             n = min(stp, n - (cnt - 1) * stp)
-        cnt = sum(1 for lane in range(n) if self.es[q0 + lane] <= b)
-        return q0 + cnt - 1
 
     def load_window(self, j0):
         self.wj = j0
