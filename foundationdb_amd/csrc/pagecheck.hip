@@ -75,16 +75,39 @@ __device__ void hashlittle2_a16(const uint8_t* k, uint64_t length, uint32_t* pc,
 	a -= c; a ^= ROT(c, 16); c += b;                                                                                  \
 	b -= a; b ^= ROT(a, 19); a += c;                                                                                  \
 	c -= b; c ^= ROT(b, 4);  b += a;
-	while (length > 48) {  // four whole rounds, and more data after them
-		const u32x4 x = *((g_u32x4*)reinterpret_cast<uintptr_t>(k));
-		const u32x4 y = *((g_u32x4*)reinterpret_cast<uintptr_t>(k + 16));
-		const u32x4 z = *((g_u32x4*)reinterpret_cast<uintptr_t>(k + 32));
-		a += x[0]; b += x[1]; c += x[2]; MIX();
-		a += x[3]; b += y[0]; c += y[1]; MIX();
-		a += y[2]; b += y[3]; c += z[0]; MIX();
-		a += z[1]; b += z[2]; c += z[3]; MIX();
-		length -= 48;
-		k += 48;
+	// groups of 48 bytes (four whole rounds) while more data follows them: the
+	// reference's `while (length > 12)` taken four rounds at a time.  One lane
+	// walks one page and the lanes are few (only the pages no other check
+	// accepted), so each group's loads go out kPre groups ahead (clamped to the
+	// last group: duplicates are never used) -- the mix chain never waits for
+	// memory once the pipeline is full.
+	constexpr int kPre = 8;
+	const uint64_t m = length > 48 ? (length - 1) / 48 : 0;
+	if (m) {
+		u32x4 q[kPre][3];
+		auto ld = [&](int s, uint64_t g) {
+			const uint8_t* p = k + 48 * (g < m ? g : m - 1);
+			q[s][0] = *((g_u32x4*)reinterpret_cast<uintptr_t>(p));
+			q[s][1] = *((g_u32x4*)reinterpret_cast<uintptr_t>(p + 16));
+			q[s][2] = *((g_u32x4*)reinterpret_cast<uintptr_t>(p + 32));
+		};
+#pragma unroll
+		for (int s = 0; s < kPre; ++s) ld(s, s);
+		for (uint64_t g0 = 0; g0 < m; g0 += kPre) {
+#pragma unroll
+			for (int s = 0; s < kPre; ++s) {
+				if (g0 + s < m) {
+					const u32x4 x = q[s][0], y = q[s][1], z = q[s][2];
+					a += x[0]; b += x[1]; c += x[2]; MIX();
+					a += x[3]; b += y[0]; c += y[1]; MIX();
+					a += y[2]; b += y[3]; c += z[0]; MIX();
+					a += z[1]; b += z[2]; c += z[3]; MIX();
+				}
+				ld(s, g0 + s + kPre);
+			}
+		}
+		length -= 48 * m;
+		k += 48 * m;
 	}
 #undef MIX
 #undef ROT
