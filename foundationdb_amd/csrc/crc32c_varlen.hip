@@ -399,39 +399,126 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 	}
 }
 
+// BIG: the block route is on (bigmin != 0); without it the route's sums
+// and entries are compiled out (fewer registers: 8 blocks per CU).
+template <bool BIG>
 __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
-	__shared__ uint32_t s4[4][256];  // slice4 tables (no bank replication: this kernel is not LDS-bound)
+	const uint64_t bigmin = BIG ? P.bigmin : 0;
+	__shared__ uint32_t s4[4][256];    // slice4 tables (no bank replication: this kernel is not LDS-bound)
+	__shared__ uint32_t iz[16 * 128];  // inv_z nibble tables: x^(-8z), z < 16 (small buffers' trailing zeros)
 	__shared__ uint32_t wsum[3][4];
 	__shared__ uint32_t s_pre[3][4];
 	__shared__ uint64_t s_stat[4][3];
 	const DevTables* T = P.tabs;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	// Latency chain: the table loads, this thread's metadata and the first
+	// round of predecessor tile sums go out together; the small buffers' chunk
+	// loads follow as soon as the metadata is back, in the shadow of the tile
+	// sums, and the one barrier of the kernel waits for all of them.
+	uint32_t tv[12];
 #pragma unroll
-	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = T->slice4[k][threadIdx.x];
+	for (int k = 0; k < 4; ++k) tv[k] = gld32(&T->slice4[k][threadIdx.x]);
+#pragma unroll
+	for (int k = 0; k < 8; ++k) tv[4 + k] = gld32(&T->inv_z[0][0][0] + threadIdx.x + 256 * k);
 	const uint32_t tile = blockIdx.x;
-	// this thread's buffer: its metadata and seed loads go out first, so their
-	// latency overlaps the tile-prefix loads below
 	const uint64_t i = (uint64_t)tile * kTileW + threadIdx.x;
 	const bool ok = i < P.count;
 	uint64_t off = 0, len = 0;
 	v7_buffer(P, ok ? i : P.count - 1, off, len);
 	const uint32_t sdv = P.seeds ? P.seeds[ok ? i : P.count - 1] : P.seed;
 	if (!ok) len = 0;
+	// general path (neither scanned nor self-summed): eight tile sums per thread
+	// in flight at once (one load latency per 2048 predecessor tiles)
+	const bool tl = !P.scanned && !P.selfsum;
+	uint32_t v[8], vB[8], vN[8];
+	auto tile_loads = [&](uint32_t k0) {
+#pragma unroll
+		for (uint32_t u = 0; u < 8; ++u) {
+			const uint32_t k = k0 + u * blockDim.x;
+			const uint32_t kc = k < tile ? k : 0;
+			v[u] = (uint32_t)gld64(P.tsum + kc);
+			vB[u] = bigmin ? (uint32_t)gld64(P.bsum + kc) : 0u;
+			vN[u] = bigmin ? (uint32_t)gld64(P.nsum + kc) : 0u;
+		}
+	};
+	if (tl) tile_loads(threadIdx.x);
+#pragma unroll
+	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = tv[k];
+#pragma unroll
+	for (int k = 0; k < 8; ++k) iz[threadIdx.x + 256 * k] = tv[4 + k];
 #if FDBCRC_V7_RANGES > 1
 	if (tile == 0)
 		for (uint64_t k = threadIdx.x; k < P.nwave / kV7RangesPerBlock; k += 256) P.ctr[k] = 0;
 #endif
 	if (tile == 0)
 		for (uint32_t k = threadIdx.x; k < P.nbctr; k += 256) P.bctr[k] = 0;
+	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
+	const Geo7 g = geo7(P0, len, bigmin);
+	// small buffer (16-byte chunks spanning at most kSmallSpan bytes): its
+	// chunks, loaded now (exec-masked: chunks past the buffer's last are not
+	// read; 1 Mi x 64 B packets 0.057 -> 0.048 ms against clamped re-reads)
+	constexpr uint32_t NC = kSmallSpan / 16;
+	const bool small = ok && len >= 16 && !g.W && !g.nb;
+	const uint32_t nch = small ? (uint32_t)(((P0 + len + 15) & ~uint64_t(15)) - g.A) >> 4 : 0u;
+	u32x4 ch[NC];
+#pragma unroll
+	for (uint32_t j = 0; j < NC; ++j)
+		ch[j] = j < nch ? ld16(reinterpret_cast<const uint8_t*>(g.A + 16 * j)) : u32x4{0u, 0u, 0u, 0u};
+	// The tables are in LDS once every thread's writes are: the barrier (its
+	// fence waits for every load in flight) also collects the chunks and the
+	// first round of tile sums, which were all in flight together.
+	__syncthreads();
+	// small buffer: its chunks [A, E) as 4-byte words from a zero register,
+	// the bytes before P0 zeroed and ~seed injected at P0 (crc32c.cpp:197),
+	// the zt bytes after P1 zeroed and then divided out (x^(-8 zt), LDS
+	// nibble tables).  Finished here, so the chunks are dead before the scans.
+	uint32_t pre = 0, preB = 0, preN = 0;
+	if (tl) {  // the first round of tile sums (the rest, for batches past 2048 tiles, below)
+#pragma unroll
+		for (uint32_t u = 0; u < 8; ++u) {
+			const bool in = threadIdx.x + u * blockDim.x < tile;
+			pre += in ? v[u] : 0u;
+			preB += in ? vB[u] : 0u;
+			preN += in ? vN[u] : 0u;
+		}
+	}
+	uint32_t xs = 0;
+	if (nch) {
+		const Masks mk = edge_masks(g.k0, 16u - g.zt, ~sdv);
+#pragma unroll
+		for (uint32_t j = 0; j < NC; ++j) {
+			if (j < nch) {
+#pragma unroll
+				for (int d = 0; d < 4; ++d) {
+					uint32_t w = ch[j][d];
+					if (j == 0) w = (w & mk.lm[d]) ^ mk.inj[d];
+					if (j == 1 && d == 0) w ^= mk.spill;
+					if (j == nch - 1) w &= mk.tm[d];
+					xs ^= w;
+					xs = s4[0][xs & 255u] ^ s4[1][(xs >> 8) & 255u] ^ s4[2][(xs >> 16) & 255u] ^ s4[3][xs >> 24];
+				}
+			}
+		}
+		if (g.zt) {
+			const uint32_t* t = iz + 128 * g.zt;
+			uint32_t r = 0;
+#pragma unroll
+			for (int n = 0; n < 8; ++n) r ^= t[16 * n + ((xs >> (4 * n)) & 15u)];
+			xs = r;
+		}
+	}
 	// exclusive prefixes of this tile (window slots, route blocks, route
 	// entries): the sums of all earlier tiles, read in parallel by the whole
 	// block (no inter-block waiting).  Every total is below 2^32 (the engine's
 	// slot limit), so the sums are 32-bit.
-	uint32_t pre = 0, preB = 0, preN = 0;
+#ifdef FDBCRC_EXP_NOPRE
+	if (true) {
+	} else
+#endif
 	if (P.scanned) {
 		if (threadIdx.x == 0) {
 			pre = (uint32_t)P.tsum[tile];
-			if (P.bigmin) {
+			if (bigmin) {
 				preB = (uint32_t)P.bsum[tile];
 				preN = (uint32_t)P.nsum[tile];
 			}
@@ -449,7 +536,7 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 			}
 #pragma unroll
 			for (uint32_t u = 0; u < 8; ++u) {
-				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o[u], l[u], P.bigmin);
+				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o[u], l[u], bigmin);
 				const bool in = j0 + u * blockDim.x < n;
 				pre += in ? gj.W : 0u;
 				preB += in ? gj.nb : 0u;
@@ -457,18 +544,8 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 			}
 		}
 	} else {
-		// eight tile sums per thread in flight at once (one load latency per
-		// 2048 predecessor tiles, not one per 256)
-		for (uint32_t k0 = threadIdx.x; k0 < tile; k0 += 8 * blockDim.x) {
-			uint32_t v[8], vB[8], vN[8];
-#pragma unroll
-			for (uint32_t u = 0; u < 8; ++u) {
-				const uint32_t k = k0 + u * blockDim.x;
-				const uint32_t kc = k < tile ? k : 0;
-				v[u] = (uint32_t)gld64(P.tsum + kc);
-				vB[u] = P.bigmin ? (uint32_t)gld64(P.bsum + kc) : 0u;
-				vN[u] = P.bigmin ? (uint32_t)gld64(P.nsum + kc) : 0u;
-			}
+		for (uint32_t k0 = threadIdx.x + 8 * blockDim.x; k0 < tile; k0 += 8 * blockDim.x) {
+			tile_loads(k0);
 #pragma unroll
 			for (uint32_t u = 0; u < 8; ++u) {
 				const bool in = k0 + u * blockDim.x < tile;
@@ -486,8 +563,6 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		s_pre[1][wv] = preB;
 		s_pre[2][wv] = preN;
 	}
-	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
-	const Geo7 g = geo7(P0, len, P.bigmin);
 	const uint32_t W = ok ? g.W : 0u, B = ok ? g.nb : 0u, N = (ok && g.nb) ? 1u : 0u;
 	if (tile == 0 && P.hstat) {  // the first 256 buffers' bytes by span class, for the host's next route choice
 		const uint64_t span = ok && len >= 16 ? ((P0 + len + 15) & ~uint64_t(15)) - (P0 & ~uint64_t(15)) : 0;
@@ -558,44 +633,20 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 			P.out[i] = ~r;
 			return;
 		}
-		// small buffer: its chunks [A, E) as 4-byte words from a zero register,
-		// the bytes before P0 zeroed and ~seed injected at P0 (crc32c.cpp:197),
-		// the zt bytes after P1 zeroed and then divided out (x^(-8 zt)).  All
-		// chunk loads are issued first: one latency.
-		constexpr uint32_t NC = kSmallSpan / 16;
-		const uint32_t nch = (uint32_t)(((P0 + len + 15) & ~uint64_t(15)) - g.A) >> 4;
-		// chunks past the buffer's last are not loaded (exec-masked: 1 Mi x 64 B
-		// packets 0.057 -> 0.048 ms against clamped re-reads of the last chunk)
-		u32x4 ch[NC];
-#pragma unroll
-		for (uint32_t j = 0; j < NC; ++j)
-			ch[j] = j < nch ? ld16(reinterpret_cast<const uint8_t*>(g.A + 16 * j)) : u32x4{0u, 0u, 0u, 0u};
-		const Masks mk = edge_masks(g.k0, 16u - g.zt, s0);
-		uint32_t x = 0;
-#pragma unroll
-		for (uint32_t j = 0; j < NC; ++j) {
-			if (j < nch) {
-#pragma unroll
-				for (int d = 0; d < 4; ++d) {
-					uint32_t w = ch[j][d];
-					if (j == 0) w = (w & mk.lm[d]) ^ mk.inj[d];
-					if (j == 1 && d == 0) w ^= mk.spill;
-					if (j == nch - 1) w &= mk.tm[d];
-					x ^= w;
-					x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
-				}
-			}
-		}
-		P.out[i] = ~(g.zt ? vmul(&T->inv_z[g.zt][0][0], x) : x);
+		P.out[i] = ~xs;  // small buffer, finished before the prefixes
 		return;
 	}
 	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
+	// a buffer starting on a 16-byte boundary inside its first window (lo != 0:
+	// the streaming kernel masks that window anyway) has no garbage before it:
+	// the streaming kernel injects its ~seed itself and reads no lead term
+	if (!g.k0 && g.lo) return;
 	// lead term: the lead chunk's bytes below k0 (read only when the buffer
 	// starts inside its chunk) with the register ~seed injected at k0, carried
 	// to the end of the pass block (chunkpow).  The garbage after the buffer's
 	// end is masked by the streaming kernel (it always sits in lane 63).
-	u32x4 ch = u32x4{0u, 0u, 0u, 0u};
-	if (g.k0) ch = ld16(reinterpret_cast<const uint8_t*>(g.A));
+	u32x4 lc = u32x4{0u, 0u, 0u, 0u};
+	if (g.k0) lc = ld16(reinterpret_cast<const uint8_t*>(g.A));
 	// Four 4-byte steps: the garbage bytes below k0 kept (~lm), ~seed XORed in
 	// at byte k0 (inj); for k0 > 12 the part of ~seed past the chunk is still
 	// in the register after it (spill).
@@ -603,7 +654,7 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	uint32_t x = 0;
 #pragma unroll
 	for (int d = 0; d < 4; ++d) {
-		x ^= (ch[d] & ~mk.lm[d]) ^ mk.inj[d];
+		x ^= (lc[d] & ~mk.lm[d]) ^ mk.inj[d];
 		x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
 	}
 	x ^= mk.spill;
@@ -627,6 +678,7 @@ struct Tab7 {
 	uint32_t f;
 	uint32_t oi;   // output index relative to the wave's first tile
 	uint32_t S;    // team sum of the slot, XORed onto the slot's edge terms (team-sum form)
+	uint32_t sd;   // lead slot of a buffer starting on a 16-byte boundary: ~seed, injected at its first byte
 	uint64_t em;   // (uniform) slots that need masking: window 0 (lo != 0), tail bytes, empty slots
 };
 // A slot whose chunks all hold its buffer's own bytes needs no masking.
@@ -686,19 +738,20 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	uint64_t B_bi0 = 0;
 	uint64_t B_wb;          // window 0 address
 	uint32_t B_g, B_W, B_f; // first slot, windows, lo | zt << 11
-	uint32_t B_cl;
+	uint32_t B_cl, B_sd;
 	uint32_t Gb1 = 0;       // wave-relative end of the batch's slots
 	uint64_t p_shift = 0;   // bytes from the end of the wave's last window to its buffer's end
 	// The metadata of the next 64-buffer batch is loaded one batch ahead: when
 	// build() consumes it, the loads have long returned, so they never make the
 	// table build wait for the data loads in flight (vmcnt is in order).
 	uint64_t pf_off = 0, pf_len = 0;
-	uint32_t pf_g = 0, pf_cl = 0;
+	uint32_t pf_g = 0, pf_cl = 0, pf_sd = 0;
 	auto prefetch = [&](uint64_t bi0) {  // unconditional, clamped into the batch
 		const uint64_t j = bi0 + lane < P.count ? bi0 + lane : P.count - 1;
 		v7_buffer(P, j, pf_off, pf_len);
 		pf_g = gld32(P.gs + j);
 		pf_cl = gld32(P.cl + j);
+		pf_sd = P.seeds ? gld32(P.seeds + j) : P.seed;
 	};
 	auto build = [&]() {
 		const uint64_t bi0 = nb_bi0;
@@ -713,7 +766,12 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		B_g = g;
 		B_W = W;
 		B_f = ge.lo | (ge.zt << k7_ZT);
-		B_cl = cl;
+		// a buffer starting on a 16-byte boundary inside its first window has no
+		// lead term (prep leaves cl unwritten): its ~seed is injected into its
+		// first word where that window is masked anyway
+		const bool inj = !ge.k0 && ge.lo;
+		B_cl = inj ? 0u : cl;
+		B_sd = inj ? ~pf_sd : 0u;
 		nb_bi0 = bi0 + 64;
 		prefetch(nb_bi0 < P.count ? nb_bi0 : bi0);
 		// end of the slots of this batch: g + W is non-decreasing over the
@@ -738,7 +796,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			if (shfl32(st, jj + step) <= (uint32_t)lane) jj += step;
 		const uint64_t wb = shfl64(B_wb, jj);
 		const uint32_t g = shfl32(B_g, jj), W = shfl32(B_W, jj), bf = shfl32(B_f, jj);
-		const uint32_t cl = shfl32(B_cl, jj);
+		const uint32_t cl = shfl32(B_cl, jj), sd = shfl32(B_sd, jj);
 		const uint32_t slot = ts + (uint32_t)lane;
 		const uint32_t m = slot - g;
 		const uint32_t gend = g + W - 1;                          // the buffer's last slot
@@ -756,6 +814,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			X.wa = wb + 1024 * (uint64_t)m;
 			X.f = f;
 			X.S = lead ? cl : 0u;
+			X.sd = lead ? sd : 0u;
 			X.oi = (uint32_t)(B_bi0 - bi_w) + jj;
 		}
 		// bytes from the end of the wave's last window to the buffer's end
@@ -771,6 +830,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		X.f = 1024u;
 		X.oi = 0;
 		X.S = 0;
+		X.sd = 0;
 		uint32_t filled = 0;
 		for (;;) {
 			if (Gb1 > sb + filled) filled = expand(X, sb, filled);
@@ -781,7 +841,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			const uint64_t w0 = rdlane64(X.wa, 0);
 			if ((uint32_t)lane >= filled) X.wa = w0;
 		}
-		X.em = __ballot(slot_edge(X.f));
+		X.em = __ballot(slot_edge(X.f));  // (slots with sd have lo != 0)
 		return filled;
 	};
 	// load k of a pass fetches team {0,2,1,3}[k]'s window.  Every load is
@@ -814,6 +874,11 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 				const bool z = c.ld_off < lo;
 #pragma unroll
 				for (int d = 0; d < 4; ++d) b.r[k][d] = z ? 0u : b.r[k][d];
+				const uint32_t sd = rdlane(X.sd, (int)(4 * p + (((k & 1) << 1) | (k >> 1))));
+				if (sd) {  // aligned buffer: ~seed into the first word of its lead chunk (window offset lo)
+					const uint32_t ln = 32 * ((lo >> 4) & 1) + 16 * ((lo >> 5) & 1) + ((lo >> 6) & 15);
+					b.r[k][0] ^= (uint32_t)lane == ln ? sd : 0u;
+				}
 			}
 			const uint32_t zt = (f >> k7_ZT) & 15u;
 			if ((f & (k7_FIN | k7_PEND)) == k7_FIN && zt) {  // last window: bytes after P1 (lane 63's chunk)
@@ -942,6 +1007,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	t1.f = 1024u;  // empty: the first table's "previous table" finishes nothing
 	t1.oi = 0;
 	t1.S = 0;
+	t1.sd = 0;
 	t1.em = ~0ull;
 	phase1(t1, 0);
 	prefetch(nb_bi0);
@@ -1049,7 +1115,10 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	if (P.scanned)
 		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4, P.bigmin ? P.bsum : nullptr,
 		                               P.bigmin ? P.nsum : nullptr);
-	k_v7prep<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	if (P.bigmin)
+		k_v7prep<true><<<(unsigned)ntile, 256, 0, stream>>>(P);
+	else
+		k_v7prep<false><<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.bigmin) {
 		BigParams B{};
 		B.hdr = P.hdr; B.es = P.es; B.eE = P.eE; B.eidx = P.eidx; B.elot = P.elot; B.esd = P.esd;

@@ -15,7 +15,7 @@ F.fill_splitmix64(buf, 0x5EED)
 ONLY = sys.argv[1:]
 
 
-def run(name, lengths, align=256, reps=10):
+def run(name, lengths, align=256, reps=int(os.environ.get("REPS", 10))):
     if ONLY and not any(o in name for o in ONLY):
         return
     lengths = np.asarray(lengths, dtype=np.int64)
