@@ -6,6 +6,15 @@
 
 namespace fdbcrc {
 
+// Window engine (crc32c_varlen.hip): passes of data in flight per wave while
+// one is computed (depth D: D + 1 blocks in rotation), and slots per table
+// (4 slots per pass, a multiple of D + 1 passes, so the next table's first
+// passes land in the first blocks again).
+#ifndef FDBCRC_V7_DEPTH
+#define FDBCRC_V7_DEPTH 1
+#endif
+constexpr uint32_t kV7TabSlots = FDBCRC_V7_DEPTH == 2 ? 60u : 64u;  // 15 or 16 passes
+
 struct DevTables {
 	uint32_t slice[2][256];     // [0] byte + one zero byte (T1), [1] single byte (T0)
 	uint32_t block[8][16];      // nibble tables of x^(8*4096): block-to-block shift
@@ -15,7 +24,7 @@ struct DevTables {
 	uint32_t pow2[64][8][16];   // nibble tables of x^(8*2^m): shift by arbitrary byte counts
 	uint32_t corr[4][16][8][16];  // x^(-8(z + 1024(3-t))): quarter t's team value -> piece register, minus z zeros
 	// varlen v7 (1 KiB window slots, 64 slots per table)
-	uint32_t table_shift[8][16];     // x^(8*65536): a piece's register carried across a 64-slot table
+	uint32_t table_shift[8][16];     // x^(8*1024*kV7TabSlots): a piece's register carried across a table
 	uint32_t slotw[64][16][8][16];   // x^(8*(1024*(d-3) - z)): slot sum of pass p -> its buffer's end
 	                                 // (d = last slot - 4p, z trailing zeros)
 	uint32_t carryw[64][16][8][16];  // x^(8*(1024*(k+1) - z)): a register carried into a table -> its

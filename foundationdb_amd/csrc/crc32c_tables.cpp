@@ -26,7 +26,7 @@ void build_dev_tables(DevTables* t) {
 	for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(z), t->inv_z[z]);
 	for (int q = 0; q < 4; ++q)
 		for (int z = 0; z < 16; ++z) mul_tables_nibble(xpow8_inv(z + 1024u * (3 - q)), t->corr[q][z]);
-	mul_tables_nibble(xpow8(65536), t->table_shift);
+	mul_tables_nibble(xpow8(1024u * kV7TabSlots), t->table_shift);
 	for (int d = 0; d < 64; ++d)
 		for (int z = 0; z < 16; ++z) {
 			const int64_t e = 1024 * (int64_t)(d - 3) - z;

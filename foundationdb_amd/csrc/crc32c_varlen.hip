@@ -511,10 +511,6 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	// entries): the sums of all earlier tiles, read in parallel by the whole
 	// block (no inter-block waiting).  Every total is below 2^32 (the engine's
 	// slot limit), so the sums are 32-bit.
-#ifdef FDBCRC_EXP_NOPRE
-	if (true) {
-	} else
-#endif
 	if (P.scanned) {
 		if (threadIdx.x == 0) {
 			pre = (uint32_t)P.tsum[tile];
@@ -639,8 +635,11 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
 	// a buffer starting on a 16-byte boundary inside its first window (lo != 0:
 	// the streaming kernel masks that window anyway) has no garbage before it:
-	// the streaming kernel injects its ~seed itself and reads no lead term
-	if (!g.k0 && g.lo) return;
+	// the streaming kernel injects its ~seed, stored here, itself
+	if (!g.k0 && g.lo) {
+		P.cl[i] = s0;
+		return;
+	}
 	// lead term: the lead chunk's bytes below k0 (read only when the buffer
 	// starts inside its chunk) with the register ~seed injected at k0, carried
 	// to the end of the pass block (chunkpow).  The garbage after the buffer's
@@ -662,7 +661,8 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 }
 
 // Streaming kernel.  Tables of 64 slots (wave-relative), passes of 4 slots.
-constexpr uint32_t k7_LO = 0x7FFu;          // bytes of the window not loaded at its start (1024: empty slot)
+constexpr uint32_t k7_LO = 0x7F0u;          // bytes of the window not loaded at its start (1024: empty slot)
+constexpr uint32_t k7_INJ = 1u;             // lead slot of an aligned buffer: S holds ~seed, injected at its first byte
 constexpr uint32_t k7_ZT = 11;              // trailing zeros of the buffer, when it ends in this table (4 bits)
 constexpr uint32_t k7_FIN = 1u << 15;       // the buffer's last slot in this wave
 constexpr uint32_t k7_PEND = 1u << 16;      // ... because the wave ends there: the buffer continues
@@ -673,12 +673,13 @@ constexpr uint32_t k7_KF = 20;              // first slot of the buffer inside t
 constexpr uint32_t k7_KL = 26;              // last slot of the buffer's part in the table, 63 if open (6 bits)
 // s_waitcnt vmcnt(6) (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15, vmcnt[5:4] at [15:14])
 __device__ __forceinline__ void kWaitVm6() { __builtin_amdgcn_s_waitcnt(0x0F76); }
+// s_waitcnt vmcnt(8)
+__device__ __forceinline__ void kWaitVm8() { __builtin_amdgcn_s_waitcnt(0x0F78); }
 struct Tab7 {
 	uint64_t wa;   // window address
 	uint32_t f;
 	uint32_t oi;   // output index relative to the wave's first tile
 	uint32_t S;    // team sum of the slot, XORed onto the slot's edge terms (team-sum form)
-	uint32_t sd;   // lead slot of a buffer starting on a 16-byte boundary: ~seed, injected at its first byte
 	uint64_t em;   // (uniform) slots that need masking: window 0 (lo != 0), tail bytes, empty slots
 };
 // A slot whose chunks all hold its buffer's own bytes needs no masking.
@@ -687,6 +688,7 @@ __device__ __forceinline__ bool slot_edge(uint32_t f) {
 }
 
 __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
+	constexpr uint32_t kTS = kV7TabSlots;  // slots per table
 	__shared__ uint32_t lds[kLdsBytesB / 4];
 	const DevTables* __restrict__ T = P.tabs;
 	const LaneCtx c = make_ctx();
@@ -738,20 +740,19 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	uint64_t B_bi0 = 0;
 	uint64_t B_wb;          // window 0 address
 	uint32_t B_g, B_W, B_f; // first slot, windows, lo | zt << 11
-	uint32_t B_cl, B_sd;
+	uint32_t B_cl;
 	uint32_t Gb1 = 0;       // wave-relative end of the batch's slots
 	uint64_t p_shift = 0;   // bytes from the end of the wave's last window to its buffer's end
 	// The metadata of the next 64-buffer batch is loaded one batch ahead: when
 	// build() consumes it, the loads have long returned, so they never make the
 	// table build wait for the data loads in flight (vmcnt is in order).
 	uint64_t pf_off = 0, pf_len = 0;
-	uint32_t pf_g = 0, pf_cl = 0, pf_sd = 0;
+	uint32_t pf_g = 0, pf_cl = 0;
 	auto prefetch = [&](uint64_t bi0) {  // unconditional, clamped into the batch
 		const uint64_t j = bi0 + lane < P.count ? bi0 + lane : P.count - 1;
 		v7_buffer(P, j, pf_off, pf_len);
 		pf_g = gld32(P.gs + j);
 		pf_cl = gld32(P.cl + j);
-		pf_sd = P.seeds ? gld32(P.seeds + j) : P.seed;
 	};
 	auto build = [&]() {
 		const uint64_t bi0 = nb_bi0;
@@ -765,13 +766,11 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		B_wb = ge.A - ge.lo;
 		B_g = g;
 		B_W = W;
-		B_f = ge.lo | (ge.zt << k7_ZT);
+		B_f = ge.lo | (ge.zt << k7_ZT) | ((!ge.k0 && ge.lo) ? k7_INJ : 0u);
 		// a buffer starting on a 16-byte boundary inside its first window has no
-		// lead term (prep leaves cl unwritten): its ~seed is injected into its
-		// first word where that window is masked anyway
-		const bool inj = !ge.k0 && ge.lo;
-		B_cl = inj ? 0u : cl;
-		B_sd = inj ? ~pf_sd : 0u;
+		// lead term: prep stored its ~seed instead, injected into its first word
+		// where that window is masked anyway (k7_INJ)
+		B_cl = cl;
 		nb_bi0 = bi0 + 64;
 		prefetch(nb_bi0 < P.count ? nb_bi0 : bi0);
 		// end of the slots of this batch: g + W is non-decreasing over the
@@ -785,7 +784,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	};
 	// slots [sb + k_lo, min(Gb1, sb + 64)) of the current batch into table lanes
 	auto expand = [&](Tab7& X, uint32_t sb, uint32_t k_lo) -> uint32_t {
-		const uint32_t k_hi = Gb1 - sb < 64u ? Gb1 - sb : 64u;
+		const uint32_t k_hi = Gb1 - sb < kTS ? Gb1 - sb : kTS;
 		const uint32_t ts = lo_s + sb;  // global slot of table lane 0
 		// buffer start inside the table, clamped (non-decreasing in j); the
 		// owner of lane k is the largest j with st_j <= k
@@ -796,7 +795,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			if (shfl32(st, jj + step) <= (uint32_t)lane) jj += step;
 		const uint64_t wb = shfl64(B_wb, jj);
 		const uint32_t g = shfl32(B_g, jj), W = shfl32(B_W, jj), bf = shfl32(B_f, jj);
-		const uint32_t cl = shfl32(B_cl, jj), sd = shfl32(B_sd, jj);
+		const uint32_t cl = shfl32(B_cl, jj);
 		const uint32_t slot = ts + (uint32_t)lane;
 		const uint32_t m = slot - g;
 		const uint32_t gend = g + W - 1;                          // the buffer's last slot
@@ -805,16 +804,15 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		const bool fin = slot == wend, pend = fin && wend != gend;
 		const bool split = g < lo_s || g + W > hi_s;
 		const bool cont = g < ts;
-		const bool ends = wend - ts < 64u;  // the part ends inside this table
-		const uint32_t f = (lead ? (bf & 1023u) : 0u) | ((ends && wend == gend) ? (bf & (15u << k7_ZT)) : 0u) |
+		const bool ends = wend - ts < kTS;  // the part ends inside this table
+		const uint32_t f = (lead ? (bf & (1023u | k7_INJ)) : 0u) | ((ends && wend == gend) ? (bf & (15u << k7_ZT)) : 0u) |
 		                   (fin ? k7_FIN : 0u) | (pend ? k7_PEND : 0u) | (split ? k7_SPLIT : 0u) |
 		                   (g >= lo_s ? k7_INV : 0u) | (cont ? k7_CONT : 0u) | ((cont ? 0u : g - ts) << k7_KF) |
-		                   ((ends ? wend - ts : 63u) << k7_KL);
+		                   ((ends ? wend - ts : kTS - 1) << k7_KL);
 		if ((uint32_t)lane >= k_lo && (uint32_t)lane < k_hi) {
 			X.wa = wb + 1024 * (uint64_t)m;
 			X.f = f;
 			X.S = lead ? cl : 0u;
-			X.sd = lead ? sd : 0u;
 			X.oi = (uint32_t)(B_bi0 - bi_w) + jj;
 		}
 		// bytes from the end of the wave's last window to the buffer's end
@@ -830,14 +828,13 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		X.f = 1024u;
 		X.oi = 0;
 		X.S = 0;
-		X.sd = 0;
 		uint32_t filled = 0;
 		for (;;) {
 			if (Gb1 > sb + filled) filled = expand(X, sb, filled);
-			if (filled == 64 || !more) break;
+			if (filled == kTS || !more) break;
 			build();
 		}
-		if (filled && filled < 64) {  // empty slots re-read a chunk of slot 0 (never used)
+		if (filled && filled < kTS) {  // empty slots re-read a chunk of slot 0 (never used)
 			const uint64_t w0 = rdlane64(X.wa, 0);
 			if ((uint32_t)lane >= filled) X.wa = w0;
 		}
@@ -874,10 +871,12 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 				const bool z = c.ld_off < lo;
 #pragma unroll
 				for (int d = 0; d < 4; ++d) b.r[k][d] = z ? 0u : b.r[k][d];
-				const uint32_t sd = rdlane(X.sd, (int)(4 * p + (((k & 1) << 1) | (k >> 1))));
-				if (sd) {  // aligned buffer: ~seed into the first word of its lead chunk (window offset lo)
+				if (f & k7_INJ) {  // aligned buffer: ~seed (held in S) into the first word of its lead chunk (window offset lo)
+					const int s = (int)(4 * p + (((k & 1) << 1) | (k >> 1)));
+					const uint32_t sd = rdlane(X.S, s);
 					const uint32_t ln = 32 * ((lo >> 4) & 1) + 16 * ((lo >> 5) & 1) + ((lo >> 6) & 15);
 					b.r[k][0] ^= (uint32_t)lane == ln ? sd : 0u;
+					X.S = lane == s ? 0u : X.S;
 				}
 			}
 			const uint32_t zt = (f >> k7_ZT) & 15u;
@@ -932,8 +931,8 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		uint32_t cc = 0;
 		if (carry) cc = umul(fin0 ? T->carryw[kl0][(f0 >> k7_ZT) & 15u] : T->table_shift, carry);
 		const bool fin = (f & k7_FIN) && (uint32_t)lane < pend_filled;
-		v ^= (cont && (fin || lane == 63)) ? cc : 0u;
-		carry = (pend_filled == 64 && !(rdlane(f, 63) & k7_FIN)) ? rdlane(v, 63) : 0u;
+		v ^= (cont && (fin || lane == (int)kTS - 1)) ? cc : 0u;
+		carry = (pend_filled == kTS && !(rdlane(f, kTS - 1) & k7_FIN)) ? rdlane(v, kTS - 1) : 0u;
 		const uint64_t pm = __ballot(fin && (f & k7_PEND));
 		if (pm) {  // the wave's last buffer continues in the next wave: shift its part to the buffer's end
 			const int k = __builtin_ctzll(pm);
@@ -944,9 +943,56 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		// holding window 0 carries the final inversion
 		atomicXor(fin ? P.out + bi_w + X.oi : P.dummy + w * 64 + lane, fin ? ((f & k7_INV) ? ~v : v) : 0u);
 	};
+#if FDBCRC_V7_DEPTH >= 2
+	// D + 1 blocks in rotation (a register copy would wait for the loads in
+	// flight): while pass p computes from one, passes p + 1 .. p + D load into
+	// the others -- 4D KiB in flight per wave.  Pass p of a table uses block
+	// p % (D + 1); a full table's pass count is a multiple of D + 1, so the
+	// next table's first D passes land in blocks 0 .. D - 1 again.
+	constexpr uint32_t D = FDBCRC_V7_DEPTH;
+	static_assert((kTS / 4) % (D + 1) == 0, "passes per table: a multiple of D + 1");
+	Block bk[D + 1];
+	// pass q of X (q < npX), else pass q - npX of the next table V (npV passes
+	// built), else a discarded re-read of X's pass 0: every path issues the
+	// same four loads into b
+	auto issue = [&](Block& b, const Tab7& X, const Tab7& V, uint32_t q, uint32_t npX, uint32_t npV) {
+		if (q < npX) load(b, X, q);
+		else if (q - npX < npV) load(b, V, q - npX);
+		else load(b, X, 0);
+	};
+	// all passes of table X (passes 0 .. D - 1 already issued into blocks
+	// 0 .. D - 1); V holds the previous table (phase 1 done) and is rebuilt
+	// as the next table
+	auto run_table = [&](Tab7& X, Tab7& V, uint32_t sbX, uint32_t fX) -> uint32_t {
+		const uint32_t npX = (fX + 3) >> 2;
+		issue(bk[D], X, V, D, npX, 0);
+		__builtin_amdgcn_sched_barrier(0);
+		phase2(V);
+		const uint32_t fY = fX == kTS ? build_table(V, sbX + kTS) : 0u;
+		const uint32_t npV = (fY + 3) >> 2;
+		__builtin_amdgcn_sched_barrier(0);
+		compute(bk[0], X, 0);
+		__builtin_amdgcn_sched_barrier(0);
+		for (uint32_t p = 1; p < npX;) {
+#pragma unroll
+			for (uint32_t r = 0; r <= D; ++r) {  // p = 1 + r (mod D + 1)
+				if (p >= npX) goto done;
+				issue(bk[(1 + r + D) % (D + 1)], X, V, p + D, npX, npV);
+				__builtin_amdgcn_sched_barrier(0);
+				compute(bk[(1 + r) % (D + 1)], X, p);
+				__builtin_amdgcn_sched_barrier(0);
+				++p;
+			}
+		}
+	done:
+		phase1(X, fX);
+		return fY;
+	};
+#else
 	// Two blocks in ping-pong (a register copy would wait for the loads in
 	// flight): pass p computes from one while pass p + 1 loads into the other.
 	// Full tables have 16 passes, so the next table's pass 0 lands in ba.
+	static_assert(kTS == 64, "16 passes per table");
 	Block ba, bb;
 	// all passes of table X (its pass 0 already issued into ba); V holds the
 	// previous table (phase 1 done) and is rebuilt as the next table
@@ -989,7 +1035,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 			__builtin_amdgcn_sched_barrier(0);
 			compute(ba, X, p);
 			__builtin_amdgcn_sched_barrier(0);
-			fY = fX == 64 ? build_table(V, sbX + 64) : 0u;
+			fY = fX == kTS ? build_table(V, sbX + kTS) : 0u;
 			if (fY) load(ba, V, 0);
 			__builtin_amdgcn_sched_barrier(0);
 			compute(bb, X, p + 1);
@@ -1001,29 +1047,36 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		phase1(X, fX);
 		return fY;
 	};
+#endif
 
 	Tab7 t0, t1;
 	t1.wa = 0;
 	t1.f = 1024u;  // empty: the first table's "previous table" finishes nothing
 	t1.oi = 0;
 	t1.S = 0;
-	t1.sd = 0;
 	t1.em = ~0ull;
 	phase1(t1, 0);
 	prefetch(nb_bi0);
 	build();
 	uint32_t sb = 0;
 	uint32_t f0 = build_table(t0, 0);
+#if FDBCRC_V7_DEPTH >= 2
+	if (f0) {
+#pragma unroll
+		for (uint32_t j = 0; j < D; ++j) load(bk[j], t0, j < ((f0 + 3) >> 2) ? j : 0u);
+	}
+#else
 	if (f0) load(ba, t0, 0);
+#endif
 	while (f0) {
 		const uint32_t f1 = run_table(t0, t1, sb, f0);
-		sb += 64;
+		sb += kTS;
 		if (!f1) {
 			phase2(t0);
 			break;
 		}
 		f0 = run_table(t1, t0, sb, f1);
-		sb += 64;
+		sb += kTS;
 		if (!f0) phase2(t1);
 	}
 #if FDBCRC_V7_RANGES > 1
