@@ -269,7 +269,7 @@ constexpr uint32_t kTileW = 256;
 #endif
 constexpr uint64_t kV7RangesPerBlock = (FDBCRC_V7_THREADS / 64) * FDBCRC_V7_RANGES;
 #ifndef FDBCRC_SELFSUM_TILES
-#define FDBCRC_SELFSUM_TILES 8
+#define FDBCRC_SELFSUM_TILES 32
 #endif
 constexpr uint64_t kSelfSumTiles = FDBCRC_SELFSUM_TILES;
 #ifndef FDBCRC_SCAN_TILES
@@ -1157,9 +1157,10 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.bctr = reinterpret_cast<uint32_t*>(rp);
 	P.nbctr = (uint32_t)(kPageCtrWords * grid);
 	// tile prefixes: each prep block sums its predecessors (up to kScanTiles tiles);
-	// larger batches scan the tile sums first; batches of at most 8 tiles
-	// skip the count kernel (a prep block counts its predecessors' windows
-	// itself: one launch less, which is most of a small batch's latency)
+	// larger batches scan the tile sums first; batches of at most
+	// kSelfSumTiles tiles skip the count kernel (a prep block counts its
+	// predecessors' windows itself: one launch less, which is most of a small
+	// batch's latency; 32 tiles: chunks 0.202 -> 0.198 ms, 8 Ki x 16 KiB +-0)
 	// (summing the predecessors costs each prep block O(tile) loads: past
 	// kScanTiles tiles one scan block is cheaper)
 	P.scanned = ntile > kScanTiles;
