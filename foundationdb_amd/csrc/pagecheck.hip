@@ -24,7 +24,7 @@
 // xxh3_kernels.hip) checksum only those pages, compare kernels write the
 // status and append the pages a check rejected to the next algorithm's list
 // (CRC -> XXH3 -> lookup3, the reference's order), and the lookup3 pages run
-// densely, one lane each.  Every page is read by the algorithm its
+// densely, one lane each, their bytes staged through LDS with coalesced loads.  Every page is read by the algorithm its
 // trailer/header selects and by no other, plus the later algorithms only
 // after a rejection.
 #include <hip/hip_runtime.h>
@@ -63,11 +63,83 @@ __device__ __forceinline__ void push(bool want, uint32_t i, uint32_t* list, unsi
 // reference's tail mix (same values as its masked reads).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
-__device__ void hashlittle2_a16(const uint8_t* k, uint64_t length, uint32_t* pc, uint32_t* pb) {
+// Wave-cooperative main loop (STAGED): the wave's 64 pages (one per lane, all
+// of one length) are read in stages of kSt = 192 bytes (16 rounds) per page,
+// coalesced -- load t of a stage covers chunks u = 64t + lane, i.e. chunk u % 12
+// of lane u / 12's page: 12 lanes read one page's 192 contiguous bytes -- and
+// the chunks reach the lane that owns the page through LDS (page stride 49
+// words, so the 64 lanes' word reads hit distinct banks).  Lane-per-page
+// loads touch a cache line per lane per instruction; these touch ~13 per 1 KiB.
+constexpr uint32_t kSt = 192, kStW = 49;
+// pages per wave in the lookup3 kernels (lanes past it duplicate pages and
+// discard the result): fewer pages per wave, more waves per SIMD for the mix
+// chains to interleave -- measured on the bench's mix (64 Ki fall-through
+// pages): 64 -> 65.5 us, 32 -> 67.1 us, 16 -> 105 us (the duplicates' loads)
+#ifndef FDBPC_L3_PER_WAVE
+#define FDBPC_L3_PER_WAVE 64
+#endif
+constexpr uint32_t kL3PerWave = FDBPC_L3_PER_WAVE;
+template <bool STAGED>
+__device__ void hashlittle2_core(const uint8_t* k, uint64_t length, uint32_t* pc, uint32_t* pb, uint32_t* lw) {
 	uint32_t a, b, c;
 	a = b = c = 0xdeadbeefu + (uint32_t)length + *pc;
 	c += *pb;
 #define ROT(x, r) (((x) << (r)) | ((x) >> (32 - (r))))
+#define MIX()                                                                                                          \
+	a -= c; a ^= ROT(c, 4);  c += b;                                                                                  \
+	b -= a; b ^= ROT(a, 6);  a += c;                                                                                  \
+	c -= b; c ^= ROT(b, 8);  b += a;                                                                                  \
+	a -= c; a ^= ROT(c, 16); c += b;                                                                                  \
+	b -= a; b ^= ROT(a, 19); a += c;                                                                                  \
+	c -= b; c ^= ROT(b, 4);  b += a;
+	if (STAGED) {
+		// whole stages while more data follows them (the reference's
+		// `while (length > 12)`, 16 rounds at a time); `length` is wave-uniform
+		const uint64_t nst = length > kSt ? (length - 1) / kSt : 0;
+		if (nst) {
+			const int lane = threadIdx.x & 63;
+			uint64_t ad[12];
+			uint32_t wo[12];
+			const uint64_t kp = reinterpret_cast<uint64_t>(k);
+#pragma unroll
+			for (int t = 0; t < 12; ++t) {
+				const uint32_t u = 64u * t + (uint32_t)lane, pg = u / 12u, ck = u % 12u;
+				const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(kp >> 32), (int)pg) << 32) |
+				                      (uint64_t)(uint32_t)__shfl((int)(uint32_t)kp, (int)pg);
+				ad[t] = base + 16u * ck;
+				wo[t] = pg * kStW + 4u * ck;
+			}
+			u32x4 st[12];
+#pragma unroll
+			for (int t = 0; t < 12; ++t) st[t] = *((g_u32x4*)ad[t]);
+			const uint32_t* mine = lw + lane * kStW;
+			// one stage in flight while one is mixed (two in flight measured the
+			// same: the mix chain, one wave per SIMD, bounds the bench's mix)
+			for (uint64_t sg = 0; sg < nst; ++sg) {
+#pragma unroll
+				for (int t = 0; t < 12; ++t)
+#pragma unroll
+					for (int e = 0; e < 4; ++e) lw[wo[t] + e] = st[t][e];
+				// the next stage's loads (the last stage re-reads itself: discarded)
+				const uint64_t nx = (sg + 1 < nst ? sg + 1 : sg) * kSt;
+#pragma unroll
+				for (int t = 0; t < 12; ++t) st[t] = *((g_u32x4*)(ad[t] + nx));
+				__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are done
+				__builtin_amdgcn_wave_barrier();
+#pragma unroll
+				for (int r = 0; r < 16; ++r) {
+					a += mine[3 * r];
+					b += mine[3 * r + 1];
+					c += mine[3 * r + 2];
+					MIX();
+				}
+				__builtin_amdgcn_wave_barrier();
+			}
+			length -= kSt * nst;
+			k += kSt * nst;
+		}
+	}
+#undef MIX
 #define MIX()                                                                                                          \
 	a -= c; a ^= ROT(c, 4);  c += b;                                                                                  \
 	b -= a; b ^= ROT(a, 6);  a += c;                                                                                  \
@@ -297,20 +369,25 @@ __global__ __launch_bounds__(256) void k_sq_final(const uint8_t* __restrict__ pa
                                                   const uint32_t* __restrict__ l3_l, uint8_t* __restrict__ status,
                                                   unsigned long long* __restrict__ ctr) {
 	const uint64_t n = ctr[L_L3];
-	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if ((uint64_t)blockIdx.x * blockDim.x >= n) return;
+	if ((uint64_t)blockIdx.x * 4 * kL3PerWave >= n) return;
 	__shared__ uint32_t s_bad;
+	__shared__ uint32_t lw[4][64 * kStW];  // per wave: one stage of its 64 lanes' pages
 	if (threadIdx.x == 0) s_bad = 0;
 	__syncthreads();
 	bool bad = false;
-	if (j < n) {
-		const uint32_t i = l3_l[j];
+	const uint32_t lane = threadIdx.x & 63;
+	const uint64_t j0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kL3PerWave;  // the wave's first entry
+	const uint64_t j = j0 + lane % kL3PerWave;
+	if (j0 < n) {  // wave-uniform: the whole wave reads cooperatively, lanes past the list re-read the last page
+		const uint32_t i = l3_l[j < n ? j : n - 1];
 		const uint8_t* p = pages + (uint64_t)i * ps;
 		uint32_t c = first_pgno + i, b = 0x5ca1ab1eu;
-		hashlittle2_a16(p, ps - 8, &c, &b);  // pages are 16-byte aligned (fdb_sqlite_verify_pages contract)
+		hashlittle2_core<true>(p, ps - 8, &c, &b, lw[threadIdx.x >> 6]);  // pages 16-byte aligned (the contract)
 		const bool ok = c == ld32(p + ps - 8) && b == ld32(p + ps - 4);
-		status[i] = ok ? 3 : 0;
-		bad = !ok;
+		if (j < n && lane < kL3PerWave) {
+			status[i] = ok ? 3 : 0;
+			bad = !ok;
+		}
 	}
 	count_bad(bad, &s_bad, &ctr[3]);
 }
@@ -381,20 +458,25 @@ __global__ __launch_bounds__(256) void k_dq_compare(const uint8_t* __restrict__ 
 __global__ __launch_bounds__(256) void k_dq_final(const uint8_t* __restrict__ pages, const uint32_t* __restrict__ v0_l,
                                                   uint8_t* __restrict__ ok, unsigned long long* __restrict__ ctr) {
 	const uint64_t n = ctr[2];
-	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if ((uint64_t)blockIdx.x * blockDim.x >= n) return;
+	if ((uint64_t)blockIdx.x * 4 * kL3PerWave >= n) return;
 	__shared__ uint32_t s_bad;
+	__shared__ uint32_t lw[4][64 * kStW];  // per wave: one stage of its 64 lanes' pages
 	if (threadIdx.x == 0) s_bad = 0;
 	__syncthreads();
 	bool bad = false;
-	if (j < n) {
-		const uint64_t i = v0_l[j];
+	const uint32_t lane = threadIdx.x & 63;
+	const uint64_t j0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kL3PerWave;
+	const uint64_t j = j0 + lane % kL3PerWave;
+	if (j0 < n) {  // wave-uniform (see k_sq_final)
+		const uint64_t i = v0_l[j < n ? j : n - 1];
 		const uint8_t* p = pages + i * 4096;
 		uint32_t c = 0x12345678u, b = 0xbeefabcdu;
-		hashlittle2_a16(p + 16, 4080, &c, &b);
+		hashlittle2_core<true>(p + 16, 4080, &c, &b, lw[threadIdx.x >> 6]);
 		const bool good = ld64(p) == (((uint64_t)c << 32) | b) && ld64(p + 8) == 0xFDBull;
-		ok[i] = good ? 1 : 0;
-		bad = !good;
+		if (j < n && lane < kL3PerWave) {
+			ok[i] = good ? 1 : 0;
+			bad = !good;
+		}
 	}
 	count_bad(bad, &s_bad, &ctr[3]);
 }
@@ -462,7 +544,7 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 	P.d_count = n_xxh;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
 	k_sq_after_xxh<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_b, w.xxh_out, status, w.list_c, w.ctr);
-	k_sq_final<<<blocks(count), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, w.ctr);
+	k_sq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, w.ctr);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
 	return 0;
 }
@@ -488,7 +570,7 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	P.d_count = n2;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
 	k_dq_compare<<<blocks(count), 256, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok, &w.ctr[3]);
-	k_dq_final<<<blocks(count), 256, 0, s>>>(pages, w.list_c, ok, w.ctr);
+	k_dq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ok, w.ctr);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
 	return 0;
 }
