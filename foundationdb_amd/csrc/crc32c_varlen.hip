@@ -402,13 +402,14 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 // BIG: the block route is on (bigmin != 0); without it the route's sums
 // and entries are compiled out (fewer registers: 8 blocks per CU).
 template <bool BIG>
-__global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
+__device__ __forceinline__ void v7prep(const V7Params& P) {
 	const uint64_t bigmin = BIG ? P.bigmin : 0;
 	__shared__ uint32_t s4[4][256];    // slice4 tables (no bank replication: this kernel is not LDS-bound)
 	__shared__ uint32_t iz[16 * 128];  // inv_z nibble tables: x^(-8z), z < 16 (small buffers' trailing zeros)
 	__shared__ uint32_t wsum[3][4];
 	__shared__ uint32_t s_pre[3][4];
 	__shared__ uint64_t s_stat[4][3];
+	__shared__ u32x4 s_tc[256];         // windowed buffers' last chunks (tail terms)
 	const DevTables* T = P.tabs;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	// Latency chain: the table loads, this thread's metadata and the first
@@ -464,6 +465,12 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 #pragma unroll
 	for (uint32_t j = 0; j < NC; ++j)
 		ch[j] = j < nch ? ld16(reinterpret_cast<const uint8_t*>(g.A + 16 * j)) : u32x4{0u, 0u, 0u, 0u};
+	// windowed buffer ending inside its last chunk: that chunk, for the tail term
+	// (parked in LDS across the barrier: registers are what limits this
+	// kernel's blocks per CU)
+	const bool tailw = ok && g.W && g.zt;
+	s_tc[threadIdx.x] = tailw ? ld16(reinterpret_cast<const uint8_t*>(((P0 + len + 15) & ~uint64_t(15)) - 16))
+	                          : u32x4{0u, 0u, 0u, 0u};
 	// The tables are in LDS once every thread's writes are: the barrier (its
 	// fence waits for every load in flight) also collects the chunks and the
 	// first round of tile sums, which were all in flight together.
@@ -632,7 +639,29 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 		P.out[i] = ~xs;  // small buffer, finished before the prefixes
 		return;
 	}
-	P.out[i] = 0u;  // windowed buffers may be finished in parts (atomicXor)
+	// Windowed buffers are finished in parts (atomicXor into out[]).  The
+	// window kernel does not mask the zt bytes after the buffer's end (they sit
+	// in its last chunk): their contribution is cancelled here instead.  Fed
+	// alone into the register at E = P1 + zt they give G (four slicing steps
+	// over the chunk's last zt bytes), which the kernel's x^(-8 zt) carries to
+	// G * x^(-8 zt) at P1 -- independent of where the window sits -- so out[]
+	// starts at that term (~(R ^ T) = ~R ^ T: the final inversion is unaffected).
+	uint32_t tterm = 0;
+	if (g.zt) {
+		const u32x4 tc = s_tc[threadIdx.x];
+		uint32_t keep[4];
+		keep_below7(16u - g.zt, keep);
+		uint32_t x = 0;
+#pragma unroll
+		for (int d = 0; d < 4; ++d) {
+			x ^= tc[d] & ~keep[d];
+			x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
+		}
+		const uint32_t* t = iz + 128 * g.zt;
+#pragma unroll
+		for (int n = 0; n < 8; ++n) tterm ^= t[16 * n + ((x >> (4 * n)) & 15u)];
+	}
+	P.out[i] = tterm;
 	// a buffer starting on a 16-byte boundary inside its first window (lo != 0:
 	// the streaming kernel masks that window anyway) has no garbage before it:
 	// the streaming kernel injects its ~seed, stored here, itself
@@ -660,6 +689,14 @@ __global__ __launch_bounds__(256) void k_v7prep(V7Params P) {
 	P.cl[i] = vmul(&T->chunkpow[64u * (gi & 3u) + (g.lo >> 4)][0][0], x);
 }
 
+// Windows only: at most 72 VGPRs, so 7 blocks per CU hold a whole zipf
+// batch (1587 tiles) in one round; with the block route the register demand
+// is higher and the tile counts are small.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_v7prep_w(V7Params P) {
+	v7prep<false>(P);
+}
+__global__ __launch_bounds__(256) void k_v7prep_b(V7Params P) { v7prep<true>(P); }
+
 // Streaming kernel.  Tables of 64 slots (wave-relative), passes of 4 slots.
 constexpr uint32_t k7_LO = 0x7F0u;          // bytes of the window not loaded at its start (1024: empty slot)
 constexpr uint32_t k7_INJ = 1u;             // lead slot of an aligned buffer: S holds ~seed, injected at its first byte
@@ -683,9 +720,7 @@ struct Tab7 {
 	uint64_t em;   // (uniform) slots that need masking: window 0 (lo != 0), tail bytes, empty slots
 };
 // A slot whose chunks all hold its buffer's own bytes needs no masking.
-__device__ __forceinline__ bool slot_edge(uint32_t f) {
-	return (f & k7_LO) || ((f & (k7_FIN | k7_PEND)) == k7_FIN && ((f >> k7_ZT) & 15u));
-}
+__device__ __forceinline__ bool slot_edge(uint32_t f) { return f & k7_LO; }
 
 __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	constexpr uint32_t kTS = kV7TabSlots;  // slots per table
@@ -879,13 +914,8 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 					X.S = lane == s ? 0u : X.S;
 				}
 			}
-			const uint32_t zt = (f >> k7_ZT) & 15u;
-			if ((f & (k7_FIN | k7_PEND)) == k7_FIN && zt) {  // last window: bytes after P1 (lane 63's chunk)
-				uint32_t km[4];
-				keep_below7(16u - zt, km);
-#pragma unroll
-				for (int d = 0; d < 4; ++d) b.r[k][d] &= lane == 63 ? km[d] : ~0u;
-			}
+			// (the bytes after a buffer's end, in lane 63's chunk of its last
+			// window, are not masked: prep's tail term in out[] cancels them)
 		}
 		}
 		unswizzle(b);
@@ -1170,9 +1200,9 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4, P.bigmin ? P.bsum : nullptr,
 		                               P.bigmin ? P.nsum : nullptr);
 	if (P.bigmin)
-		k_v7prep<true><<<(unsigned)ntile, 256, 0, stream>>>(P);
+		k_v7prep_b<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	else
-		k_v7prep<false><<<(unsigned)ntile, 256, 0, stream>>>(P);
+		k_v7prep_w<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.bigmin) {
 		BigParams B{};
 		B.hdr = P.hdr; B.es = P.es; B.eE = P.eE; B.eidx = P.eidx; B.elot = P.elot; B.esd = P.esd;
