@@ -409,7 +409,6 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	__shared__ uint32_t wsum[3][4];
 	__shared__ uint32_t s_pre[3][4];
 	__shared__ uint64_t s_stat[4][3];
-	__shared__ u32x4 s_tc[256];         // windowed buffers' last chunks (tail terms)
 	const DevTables* T = P.tabs;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	// Latency chain: the table loads, this thread's metadata and the first
@@ -458,19 +457,19 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	// small buffer (16-byte chunks spanning at most kSmallSpan bytes): its
 	// chunks, loaded now (exec-masked: chunks past the buffer's last are not
 	// read; 1 Mi x 64 B packets 0.057 -> 0.048 ms against clamped re-reads)
+	// A windowed buffer ending inside its last chunk (zt != 0) takes the same
+	// path with that one chunk, its own bytes masked: the result is its tail
+	// term (below, where out[] is initialised).
 	constexpr uint32_t NC = kSmallSpan / 16;
 	const bool small = ok && len >= 16 && !g.W && !g.nb;
-	const uint32_t nch = small ? (uint32_t)(((P0 + len + 15) & ~uint64_t(15)) - g.A) >> 4 : 0u;
+	const bool tailw = ok && g.W && g.zt;
+	const uint64_t E16 = (P0 + len + 15) & ~uint64_t(15);
+	const uint32_t nch = small ? (uint32_t)(E16 - g.A) >> 4 : (tailw ? 1u : 0u);
+	const uint64_t cb = small ? g.A : E16 - 16;
 	u32x4 ch[NC];
 #pragma unroll
 	for (uint32_t j = 0; j < NC; ++j)
-		ch[j] = j < nch ? ld16(reinterpret_cast<const uint8_t*>(g.A + 16 * j)) : u32x4{0u, 0u, 0u, 0u};
-	// windowed buffer ending inside its last chunk: that chunk, for the tail term
-	// (parked in LDS across the barrier: registers are what limits this
-	// kernel's blocks per CU)
-	const bool tailw = ok && g.W && g.zt;
-	s_tc[threadIdx.x] = tailw ? ld16(reinterpret_cast<const uint8_t*>(((P0 + len + 15) & ~uint64_t(15)) - 16))
-	                          : u32x4{0u, 0u, 0u, 0u};
+		ch[j] = j < nch ? ld16(reinterpret_cast<const uint8_t*>(cb + 16 * j)) : u32x4{0u, 0u, 0u, 0u};
 	// The tables are in LDS once every thread's writes are: the barrier (its
 	// fence waits for every load in flight) also collects the chunks and the
 	// first round of tile sums, which were all in flight together.
@@ -491,7 +490,9 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	}
 	uint32_t xs = 0;
 	if (nch) {
-		const Masks mk = edge_masks(g.k0, 16u - g.zt, ~sdv);
+		// small: bytes from k0 on, ~seed at k0, bytes up to 16 - zt in the last
+		// chunk; tail term: only the zt bytes after the end, no seed
+		const Masks mk = small ? edge_masks(g.k0, 16u - g.zt, ~sdv) : edge_masks(16u - g.zt, 16u, 0u);
 #pragma unroll
 		for (uint32_t j = 0; j < NC; ++j) {
 			if (j < nch) {
@@ -646,22 +647,7 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	// over the chunk's last zt bytes), which the kernel's x^(-8 zt) carries to
 	// G * x^(-8 zt) at P1 -- independent of where the window sits -- so out[]
 	// starts at that term (~(R ^ T) = ~R ^ T: the final inversion is unaffected).
-	uint32_t tterm = 0;
-	if (g.zt) {
-		const u32x4 tc = s_tc[threadIdx.x];
-		uint32_t keep[4];
-		keep_below7(16u - g.zt, keep);
-		uint32_t x = 0;
-#pragma unroll
-		for (int d = 0; d < 4; ++d) {
-			x ^= tc[d] & ~keep[d];
-			x = s4[0][x & 255u] ^ s4[1][(x >> 8) & 255u] ^ s4[2][(x >> 16) & 255u] ^ s4[3][x >> 24];
-		}
-		const uint32_t* t = iz + 128 * g.zt;
-#pragma unroll
-		for (int n = 0; n < 8; ++n) tterm ^= t[16 * n + ((x >> (4 * n)) & 15u)];
-	}
-	P.out[i] = tterm;
+	P.out[i] = xs;  // the tail term (computed with the small buffers above; 0 if zt = 0)
 	// a buffer starting on a 16-byte boundary inside its first window (lo != 0:
 	// the streaming kernel masks that window anyway) has no garbage before it:
 	// the streaming kernel injects its ~seed, stored here, itself
