@@ -60,3 +60,30 @@ def test_every_alignment_and_threshold_length():
     for i, (o, n) in enumerate(zip(offs, lengths)):
         A, E, W, _, _, _ = M.geo7(o, n)
         assert (W > 0) == (E - A > M.SMALL_SPAN), (o, n)
+
+
+def test_tail_term_identity():
+    """The window kernel does not mask the zt < 16 bytes after a buffer's end;
+    prep cancels them with T = chain(0, garbage) * x^(-8 zt), written as out[]'s
+    initial value (crc32c_varlen.hip, v7prep).  Checked here in the forward
+    form on the C oracle: chain(r, B || G) = chain(r, B) * x^(8 zt) ^ chain(0, G),
+    so (chain(r, B || G) ^ T * x^(8 zt)) * x^(-8 zt) = chain(r, B), and
+    ~chain(r, B) is crc32c_append's result (crc32c.cpp:197, 310)."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(7)
+
+    def chain(reg, data):  # raw register after feeding data into reg
+        return (~O.crc32c(~reg & 0xFFFFFFFF, bytes(data))) & 0xFFFFFFFF
+
+    for _ in range(200):
+        n = int(rng.integers(16, 300))
+        zt = int(rng.integers(1, 16))
+        buf = rng.integers(0, 256, n + zt, dtype=np.uint8).tobytes()
+        seed = int(rng.integers(0, 2**32))
+        body, garbage = buf[:n], buf[n:]
+        r0 = ~seed & 0xFFFFFFFF
+        unmasked = chain(r0, body + garbage)        # what the window kernel's chains hold at E
+        t_fwd = chain(0, garbage)                  # T * x^(8 zt): leading zeros of the chunk are free
+        assert t_fwd == chain(0, bytes(16 - zt) + garbage)
+        assert unmasked ^ t_fwd == O.shift(chain(r0, body), zt)
+        assert (~chain(r0, body)) & 0xFFFFFFFF == O.crc32c(seed, body)
