@@ -10,6 +10,9 @@ JOBS ?= 8
 CSRC := foundationdb_amd/csrc
 OBJ := build/obj
 LIB := foundationdb_amd/lib/libfdb_crc32c.so
+# bounds-checked build for kernel debugging (defined before `all`: prerequisites
+# are expanded when a rule is read)
+DBG_LIB := foundationdb_amd/lib/libfdb_crc32c_debug.so
 
 HIP_SRCS := $(wildcard $(CSRC)/*.hip)
 CPP_SRCS := $(wildcard $(CSRC)/*.cpp)
@@ -53,7 +56,6 @@ oracle:
 
 # bounds-checked build for kernel debugging (foundationdb_amd/lib/libfdb_crc32c_debug.so)
 # (built by default: the GPU suite replays route batches against it)
-DBG_LIB := foundationdb_amd/lib/libfdb_crc32c_debug.so
 DBG_OBJS := $(patsubst $(CSRC)/%.hip,build/dbg/%.hip.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,build/dbg/%.cpp.o,$(CPP_SRCS))
 build/dbg/crc32c_kernels.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 build/dbg/%.hip.o: $(CSRC)/%.hip $(HDRS)
