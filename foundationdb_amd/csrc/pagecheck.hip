@@ -285,9 +285,12 @@ enum { L_CRC = 0, L_XXH = 1, L_L3 = 2 };
 
 // One pass over the trailers: part1 == 0 -> CRC list; else top byte zero ->
 // XXH3 list; else lookup3 list.
+// The trailers are saved in trl[] (8 B per page, coalesced): the compare
+// passes read them there instead of each page's last line again from HBM.
 __global__ __launch_bounds__(kCB) void k_sq_classify(const uint8_t* __restrict__ pages, uint64_t ps, uint64_t count,
                                                      uint8_t* __restrict__ status, uint32_t* crc_l, uint32_t* xxh_l,
-                                                     uint32_t* l3_l, unsigned long long* __restrict__ ctr) {
+                                                     uint32_t* l3_l, unsigned long long* __restrict__ ctr,
+                                                     uint64_t* __restrict__ trl) {
 	__shared__ Stage<3> S;
 	stage_init(S);
 	const uint64_t i0 = (uint64_t)blockIdx.x * kSpan;
@@ -295,8 +298,12 @@ __global__ __launch_bounds__(kCB) void k_sq_classify(const uint8_t* __restrict__
 	for (uint32_t k = 0; k < kPer; ++k) {
 		const uint64_t i = i0 + k * kCB + threadIdx.x;
 		const bool in = i < count;
-		const uint32_t part1 = in ? ld32(pages + i * ps + ps - 8) : 1u;
-		if (in) status[i] = kPending;
+		const uint64_t t = in ? ld64(pages + i * ps + ps - 8) : 1u;
+		const uint32_t part1 = (uint32_t)t;
+		if (in) {
+			status[i] = kPending;
+			trl[i] = t;
+		}
 		stage_push(S, L_CRC, in && part1 == 0, (uint32_t)i);
 		stage_push(S, L_XXH, in && part1 != 0 && (part1 >> 24) == 0, (uint32_t)i);
 		stage_push(S, L_L3, in && (part1 >> 24) != 0, (uint32_t)i);
@@ -312,7 +319,8 @@ __global__ __launch_bounds__(kCB) void k_sq_classify(const uint8_t* __restrict__
 __global__ __launch_bounds__(kCB) void k_sq_after_crc(const uint8_t* __restrict__ pages, uint64_t ps,
                                                       const uint32_t* __restrict__ crc_l, const uint32_t* __restrict__ crc_out,
                                                       bool by_page, uint8_t* __restrict__ status, uint32_t* xxh_l,
-                                                      unsigned long long* __restrict__ ctr) {
+                                                      unsigned long long* __restrict__ ctr,
+                                                      const uint64_t* __restrict__ trl) {
 	const uint64_t n = ctr[L_CRC];
 	const uint64_t j0 = (uint64_t)blockIdx.x * kSpan;
 	if (j0 >= n) return;  // uniform: the whole workgroup leaves
@@ -325,7 +333,7 @@ __global__ __launch_bounds__(kCB) void k_sq_after_crc(const uint8_t* __restrict_
 		uint32_t i = 0;
 		if (j < n) {
 			i = crc_l[j];
-			const bool ok = (by_page ? crc_out[i] : crc_out[j]) == ld32(pages + i * ps + ps - 4);
+			const bool ok = (by_page ? crc_out[i] : crc_out[j]) == (uint32_t)(trl[i] >> 32);
 			if (ok) status[i] = 1;
 			fail = !ok;
 		}
@@ -338,7 +346,8 @@ __global__ __launch_bounds__(kCB) void k_sq_after_crc(const uint8_t* __restrict_
 __global__ __launch_bounds__(kCB) void k_sq_after_xxh(const uint8_t* __restrict__ pages, uint64_t ps,
                                                       const uint32_t* __restrict__ xxh_l, const uint64_t* __restrict__ xxh_out,
                                                       uint8_t* __restrict__ status, uint32_t* l3_l,
-                                                      unsigned long long* __restrict__ ctr) {
+                                                      unsigned long long* __restrict__ ctr,
+                                                      const uint64_t* __restrict__ trl) {
 	const uint64_t n = ctr[L_XXH];
 	const uint64_t j0 = (uint64_t)blockIdx.x * kSpan;
 	if (j0 >= n) return;
@@ -352,8 +361,8 @@ __global__ __launch_bounds__(kCB) void k_sq_after_xxh(const uint8_t* __restrict_
 		if (j < n) {
 			i = xxh_l[j];
 			const uint64_t h = xxh_out[j];
-			const uint8_t* t = pages + i * ps + ps - 8;
-			const bool ok = ld32(t) == (uint32_t)((h >> 32) & 0x00ffffffu) && ld32(t + 4) == (uint32_t)h;
+			const uint64_t t = trl[i];
+			const bool ok = (uint32_t)t == (uint32_t)((h >> 32) & 0x00ffffffu) && (uint32_t)(t >> 32) == (uint32_t)h;
 			if (ok) status[i] = 2;
 			fail = !ok;
 		}
@@ -367,7 +376,8 @@ __global__ __launch_bounds__(kCB) void k_sq_after_xxh(const uint8_t* __restrict_
 // with the page number (:147-155), then the final status and the corrupt count.
 __global__ __launch_bounds__(256) void k_sq_final(const uint8_t* __restrict__ pages, uint64_t ps, uint32_t first_pgno,
                                                   const uint32_t* __restrict__ l3_l, uint8_t* __restrict__ status,
-                                                  unsigned long long* __restrict__ ctr) {
+                                                  unsigned long long* __restrict__ ctr,
+                                                  const uint64_t* __restrict__ trl) {
 	const uint64_t n = ctr[L_L3];
 	if ((uint64_t)blockIdx.x * 4 * kL3PerWave >= n) return;
 	__shared__ uint32_t s_bad;
@@ -383,7 +393,8 @@ __global__ __launch_bounds__(256) void k_sq_final(const uint8_t* __restrict__ pa
 		const uint8_t* p = pages + (uint64_t)i * ps;
 		uint32_t c = first_pgno + i, b = 0x5ca1ab1eu;
 		hashlittle2_core<true>(p, ps - 8, &c, &b, lw[threadIdx.x >> 6]);  // pages 16-byte aligned (the contract)
-		const bool ok = c == ld32(p + ps - 8) && b == ld32(p + ps - 4);
+		const uint64_t t = trl[i];
+		const bool ok = c == (uint32_t)t && b == (uint32_t)(t >> 32);
 		if (j < n && lane < kL3PerWave) {
 			status[i] = ok ? 3 : 0;
 			bad = !ok;
@@ -487,13 +498,14 @@ __global__ __launch_bounds__(256) void k_dq_final(const uint8_t* __restrict__ pa
 uint64_t workspace_bytes(uint64_t count) {
 	// counters, three u32 lists, u32 CRC results, u64 XXH3 results, and the
 	// general engine's workspace (page sizes other than 4 KiB)
-	return 64 + 8 * count + 4 * count * 4 + 64 + fdbcrc::varlen7_workspace_bytes(count, 0) + 16;
+	return 64 + 8 * count + 4 * count * 4 + 64 + fdbcrc::varlen7_workspace_bytes(count, 0) + 16 + 8 * count + 16;
 }
 
 struct Ws {
 	unsigned long long* ctr;
 	uint32_t *list_a, *list_b, *list_c, *crc_out;
 	uint64_t* xxh_out;
+	uint64_t* trl;  // SQLite: every page's trailer {part1, part2}, saved by the classify pass
 	void* eng;
 };
 static Ws carve(void* ws, uint64_t count) {
@@ -511,6 +523,9 @@ static Ws carve(void* ws, uint64_t count) {
 	p += 4 * count;
 	w.crc_out = reinterpret_cast<uint32_t*>(p);
 	p += 4 * count;
+	p = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
+	w.trl = reinterpret_cast<uint64_t*>(p);
+	p += 8 * count;
 	w.eng = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
 	return w;
 }
@@ -521,18 +536,21 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
                   uint64_t* d_bad, const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s) {
 	const Ws w = carve(ws, count);
 	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
-	k_sq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, count, status, w.list_a, w.list_b, w.list_c, w.ctr);
+	k_sq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, count, status, w.list_a, w.list_b, w.list_c, w.ctr,
+	                                                  w.trl);
 	const uint64_t* n_crc = reinterpret_cast<const uint64_t*>(&w.ctr[L_CRC]);
 	const uint64_t* n_xxh = reinterpret_cast<const uint64_t*>(&w.ctr[L_XXH]);
 	if (ps == 4096) {
 		if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n_crc, count, 0, 8, 0xFDBEEFDBu, w.crc_out, tabs,
 		                                     num_cus, s))
 			return -1;
-		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, false, status, w.list_b, w.ctr);
+		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, false, status, w.list_b, w.ctr,
+		                                                   w.trl);
 	} else {
 		// other page sizes: every page through the general fixed-stride engine
 		fdbcrc::launch_fixed_general(pages, ps, ps - 8, count, 0xFDBEEFDBu, nullptr, w.crc_out, tabs, num_cus, w.eng, s);
-		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, true, status, w.list_b, w.ctr);
+		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, true, status, w.list_b, w.ctr,
+		                                                   w.trl);
 	}
 	fdbxxh::XxhParams P{};
 	P.base = pages;
@@ -543,8 +561,8 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 	P.idx = w.list_b;
 	P.d_count = n_xxh;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_sq_after_xxh<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_b, w.xxh_out, status, w.list_c, w.ctr);
-	k_sq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, w.ctr);
+	k_sq_after_xxh<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_b, w.xxh_out, status, w.list_c, w.ctr, w.trl);
+	k_sq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, w.ctr, w.trl);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
 	return 0;
 }
