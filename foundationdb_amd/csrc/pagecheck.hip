@@ -411,9 +411,12 @@ __global__ void k_store_bad(const unsigned long long* __restrict__ ctr, uint64_t
 // DiskQueue (4096-byte pages)
 // ---------------------------------------------------------------------------
 // ctr[0] V1 list, ctr[1] V2 list, ctr[2] V0 (lookup3) list, ctr[3] failures.
+// The first 8 bytes of each page (V1's hash32, V2's hash64) are saved in
+// hs[] for the compare pass, from the line the version is read from.
 __global__ __launch_bounds__(kCB) void k_dq_classify(const uint8_t* __restrict__ pages, uint64_t count,
                                                      uint8_t* __restrict__ ok, uint32_t* v1_l, uint32_t* v2_l,
-                                                     uint32_t* v0_l, unsigned long long* __restrict__ ctr) {
+                                                     uint32_t* v0_l, unsigned long long* __restrict__ ctr,
+                                                     uint64_t* __restrict__ hs) {
 	__shared__ Stage<3> S;
 	__shared__ uint32_t s_bad;
 	if (threadIdx.x == 0) s_bad = 0;
@@ -424,7 +427,10 @@ __global__ __launch_bounds__(kCB) void k_dq_classify(const uint8_t* __restrict__
 		const uint64_t i = i0 + k * kCB + threadIdx.x;
 		const bool in = i < count;
 		const uint32_t ver = in ? (ld32(pages + i * 4096 + 8) >> 16) : 0xFFFFu;  // implementationVersion, bytes 10..11
-		if (in) ok[i] = ver <= 2 ? kPending : 0;
+		if (in) {
+			ok[i] = ver <= 2 ? kPending : 0;
+			hs[i] = ld64(pages + i * 4096);
+		}
 		stage_push(S, 0, in && ver == 1, (uint32_t)i);
 		stage_push(S, 1, in && ver == 2, (uint32_t)i);
 		stage_push(S, 2, in && ver == 0, (uint32_t)i);
@@ -439,7 +445,8 @@ __global__ __launch_bounds__(kCB) void k_dq_classify(const uint8_t* __restrict__
 __global__ __launch_bounds__(256) void k_dq_compare(const uint8_t* __restrict__ pages, const uint32_t* __restrict__ v1_l,
                                                     const uint32_t* __restrict__ v2_l, const unsigned long long* __restrict__ ctr,
                                                     const uint32_t* __restrict__ crc_out, const uint64_t* __restrict__ xxh_out,
-                                                    uint8_t* __restrict__ ok, unsigned long long* __restrict__ ctr_bad) {
+                                                    uint8_t* __restrict__ ok, unsigned long long* __restrict__ ctr_bad,
+                                                    const uint64_t* __restrict__ hs) {
 	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const uint64_t n1 = ctr[0], n2 = ctr[1];
 	if ((uint64_t)blockIdx.x * blockDim.x >= (n1 > n2 ? n1 : n2)) return;
@@ -449,7 +456,7 @@ __global__ __launch_bounds__(256) void k_dq_compare(const uint8_t* __restrict__ 
 	bool bad = false;
 	if (j < n1) {
 		const uint64_t i = v1_l[j];
-		const bool g = crc_out[j] == ld32(pages + i * 4096);
+		const bool g = crc_out[j] == (uint32_t)hs[i];
 		ok[i] = g ? 1 : 0;
 		bad = !g;
 	}
@@ -458,7 +465,7 @@ __global__ __launch_bounds__(256) void k_dq_compare(const uint8_t* __restrict__ 
 	bad = false;
 	if (j < n2) {
 		const uint64_t i = v2_l[j];
-		const bool g = xxh_out[j] == ld64(pages + i * 4096);
+		const bool g = xxh_out[j] == hs[i];
 		ok[i] = g ? 1 : 0;
 		bad = !g;
 	}
@@ -505,7 +512,7 @@ struct Ws {
 	unsigned long long* ctr;
 	uint32_t *list_a, *list_b, *list_c, *crc_out;
 	uint64_t* xxh_out;
-	uint64_t* trl;  // SQLite: every page's trailer {part1, part2}, saved by the classify pass
+	uint64_t* trl;  // every page's trailer (SQLite) or first 8 bytes (DiskQueue), saved by the classify pass
 	void* eng;
 };
 static Ws carve(void* ws, uint64_t count) {
@@ -571,7 +578,7 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
                     const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s) {
 	const Ws w = carve(ws, count);
 	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
-	k_dq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, ok, w.list_a, w.list_b, w.list_c, w.ctr);
+	k_dq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, ok, w.list_a, w.list_b, w.list_c, w.ctr, w.trl);
 	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
 	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
 	// V1: crc32c(0xfdbeefdb, bytes [4, 4096))
@@ -587,7 +594,8 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	P.idx = w.list_b;
 	P.d_count = n2;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_dq_compare<<<blocks(count), 256, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok, &w.ctr[3]);
+	k_dq_compare<<<blocks(count), 256, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok, &w.ctr[3],
+	                                           w.trl);
 	k_dq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ok, w.ctr);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
 	return 0;
