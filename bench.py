@@ -14,9 +14,15 @@ GPU, and exits with the child's status; under an outer launcher it uses the
 launcher's ranks.  Every rank checks that the world size equals --gpus.
 Pages shard trivially (the whole-file scan of
 fdbserver/kvstore/KeyValueStoreSQLite.cpp:1378-1470 split by page range):
-every rank checksums its own batch of the same shape (weak scaling, no
-data-path collective); RCCL is used only to take the max elapsed time over
-ranks and to gather the per-rank byte counts and kernel times.
+rank r checksums shard r of one global splitmix64 file -- bytes
+[r*4 GiB, (r+1)*4 GiB), generated in its own HBM by jumping the generator --
+and checks it against the reference's digest of that shard
+(tests/golden, make_golden.py --shards): weak scaling, no data-path
+collective.  RCCL (all_gather over xGMI) is used only to take the max elapsed
+time over ranks and to gather the per-rank byte counts, parity flags and
+kernel times.  --force-pg initialises the process group at world size 1 too,
+so one GPU exercises the whole multi-GPU path; --shard-base K makes rank r
+checksum shard K + r.
 
 Rank 0 prints ONE JSON line.  `value` is GiB/s of buffer bytes read, whole
 job, from the host clock around the K timed steps.  `roofline.achieved` is the
@@ -50,13 +56,17 @@ GIB = float(1 << 30)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=30, help="untimed steps (the clock settles within ~30 launches)")
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5, help="untimed steps (the driver's setting)")
     p.add_argument("--workload", default="pages4k", choices=sorted(W.WORKLOADS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--dry-cpu", action="store_true",
                    help="test the multi-rank harness on CPU (gloo, host checksums); not a measurement")
+    p.add_argument("--force-pg", action="store_true",
+                   help="initialise the RCCL process group even at world size 1 (exercises the multi-GPU path)")
+    p.add_argument("--shard-base", type=int, default=0,
+                   help="rank r checksums shard shard_base + r of the global batch (page workloads)")
     return p.parse_args()
 
 
@@ -156,16 +166,18 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: world size {world} != --gpus {args.gpus}")
     dry = args.dry_cpu
+    use_pg = world > 1 or args.force_pg  # the collective path (RCCL, or gloo for --dry-cpu)
+    shard = args.shard_base + rank        # this rank's shard of the global batch
     if dry:
         dev = torch.device("cpu")
-        if world > 1:
+        if use_pg:
             dist.init_process_group("gloo")
             assert dist.get_world_size() == args.gpus
-        wl = W.DryCpuPages(rank)
+        wl = W.DryCpuPages(shard)
         sync = lambda: None  # noqa: E731
         stream = None
     else:
-        if world > 1:
+        if use_pg:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             if dist.get_world_size() != args.gpus:
@@ -173,14 +185,14 @@ def main():
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
         F.gpu_init()
-        wl = W.WORKLOADS[args.workload](dev, rank)
+        wl = W.WORKLOADS[args.workload](dev, shard)
         stream = torch.cuda.current_stream(dev)
         sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
     for _ in range(args.warmup):
         wl.step(stream)
     sync()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     sync()
 
@@ -200,7 +212,7 @@ def main():
     if timed:
         ev1.record(stream)
     sync()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps if timed else elapsed / args.steps * 1e3
@@ -209,10 +221,10 @@ def main():
     if not args.no_verify:
         ok = wl.verify()
 
-    stats = torch.tensor([elapsed, float(wl.bytes_per_step), 0.0 if ok else 1.0, kernel_ms], dtype=torch.float64,
-                         device=dev)
+    stats = torch.tensor([elapsed, float(wl.bytes_per_step), 0.0 if ok else 1.0, kernel_ms, float(shard)],
+                         dtype=torch.float64, device=dev)
     per_rank = [stats]
-    if world > 1:
+    if use_pg:  # RCCL all_gather over xGMI (gloo on the dry run): max time, byte count, parity, shards
         per_rank = [torch.empty_like(stats) for _ in range(world)]
         dist.all_gather(per_rank, stats)
     per_rank = [[float(x) for x in t.cpu()] for t in per_rank]
@@ -242,8 +254,9 @@ def main():
                                                   "for max-time / byte-count reduction"),
             "pct_of_hbm_read_peak": round(100.0 * value * GIB / 1e9 / HBM_PEAK_GBS, 2),
             "parity_ok": bool(ok),
-            "world_size": dist.get_world_size() if world > 1 else 1,
-            "per_rank": [{"rank": i, "bytes_per_step": int(r[1]), "elapsed_s": round(r[0], 6),
+            "world_size": dist.get_world_size() if use_pg else 1,
+            "collective": (dist.get_backend() if use_pg else None),
+            "per_rank": [{"rank": i, "shard": int(r[4]), "bytes_per_step": int(r[1]), "elapsed_s": round(r[0], 6),
                           "avg_launch_ms": round(r[3], 4), "parity_ok": r[2] == 0.0} for i, r in enumerate(per_rank)],
             "roofline": {
                 "bound": "pcie" if host_timed else "hbm",
@@ -265,7 +278,7 @@ def main():
             if mt:
                 rec["cpu_baseline_threads"] = mt  # context: the same reference path on 16 host cores
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)

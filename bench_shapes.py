@@ -16,6 +16,16 @@ import numpy as np
 STATE = 0x5EED
 ZIPF_ALIGN = 256
 CHUNK_ALIGN = 4096
+GOLDEN_GAMMA = 0x9E3779B97F4A7C15
+SHARD_BYTES = 4 << 30  # one rank's page batch: 1 Mi x 4 KiB or 512 Ki x 8 KiB pages
+
+
+def shard_state(shard, state=STATE):
+    """splitmix64 state whose stream starts at byte shard * SHARD_BYTES of the
+    global stream (word k = mix(state + (k+1)*gamma), so a jump of n words adds
+    n*gamma): BASELINE configs[3]'s whole-file scan, rank r checksumming bytes
+    [r*4 GiB, (r+1)*4 GiB) of one file, each rank generating its own shard."""
+    return (state + shard * (SHARD_BYTES // 8) * GOLDEN_GAMMA) & 0xFFFFFFFFFFFFFFFF
 
 
 def zipf_lengths(total_bytes=1 << 30, seed=1):

@@ -76,19 +76,24 @@ class CpuSample:
 
 
 class Pages:
-    """configs[1] (4 KiB) and configs[3]'s per-GPU shard (8 KiB SQLite pages)."""
+    """configs[1] (4 KiB) and configs[3]'s per-GPU shard (8 KiB SQLite pages).
+    `shard` r is bytes [r*4 GiB, (r+1)*4 GiB) of one global splitmix64 file
+    (bench_shapes.shard_state): rank r of an N-GPU run checksums shard r."""
 
-    def __init__(self, dev, rank, page_bytes=4096, count=1 << 20, seed=0):
-        self.dev, self.page_bytes, self.count, self.seed = dev, page_bytes, count, seed
+    def __init__(self, dev, shard, page_bytes=4096, count=1 << 20, seed=0):
+        self.dev, self.page_bytes, self.count, self.seed, self.shard = dev, page_bytes, count, seed, shard
         self.kernel_name = "fdbcrc::k_pages4k<2>" if page_bytes == 4096 else "fdbcrc::k_pages4k<2, PAIR> (8 KiB pages as block pairs)"
         if page_bytes != 4096:
             self.metric = f"device-resident CRC32C GiB/s on {page_bytes // 1024} KiB page batches; % of HBM-read peak"
+        sharded = count * page_bytes == S.SHARD_BYTES
+        self.state = S.shard_state(shard) if sharded else STATE
         self.buf = torch.empty(count * page_bytes, dtype=torch.uint8, device=dev)
-        F.fill_splitmix64(self.buf, STATE)
+        F.fill_splitmix64(self.buf, self.state)
         self.out = torch.empty(count, dtype=torch.uint32, device=dev)
         self.bytes_per_step = count * page_bytes
         self.algorithmic_bytes_per_step = count * (page_bytes + 4)
-        self.data_desc = (f"synthetic: splitmix64 stream (state 0x{STATE:X}) generated in HBM, "
+        where = f"shard {shard} (bytes [{shard}*4 GiB, +4 GiB) of one file) of " if sharded else ""
+        self.data_desc = (f"synthetic: {where}the splitmix64 stream (state 0x{STATE:X}) generated in HBM, "
                           f"{count} pages x {page_bytes} B, seed 0x{seed:08x}")
         self.config = {"workload": f"{count} x {page_bytes} B pages, device-resident, fixed stride",
                        "pages": count, "page_bytes": page_bytes, "seed": seed, "stride": page_bytes}
@@ -98,13 +103,9 @@ class Pages:
                       stream=stream)
 
     def verify(self):
-        g = _golden()
         got = self.out.cpu().numpy()
-        if self.page_bytes == 4096 and self.count == 1 << 20:
-            d = [d for d in g["pages_full"]["digests"] if d["seed"] == self.seed][0]
-            return int(np.bitwise_xor.reduce(got)) == d["xor"] and int(got.astype(np.uint64).sum()) == d["sum"]
-        if self.page_bytes == 8192 and self.count == 1 << 19 and self.seed == 0xFDBEEFDB:
-            d = g["pages_full"]["digest_8k_fdbeefdb"]
+        d = shard_digest(self.page_bytes, self.count, self.seed, self.state)
+        if d is not None:  # the reference's own digest of this exact shard
             return int(np.bitwise_xor.reduce(got)) == d["xor"] and int(got.astype(np.uint64).sum()) == d["sum"]
         return _spot_check(self.buf, np.arange(self.count, dtype=np.uint64) * self.page_bytes,
                            np.full(self.count, self.page_bytes, np.uint64), self.seed, got)
@@ -112,10 +113,28 @@ class Pages:
     def cpu_sample(self):
         from oracle import oracle as O
         n = 65536 if self.page_bytes == 4096 else 32768
-        buf = O.splitmix64(n * self.page_bytes // 8, STATE).view(np.uint8)
+        buf = O.splitmix64(n * self.page_bytes // 8, self.state).view(np.uint8)
         return CpuSample(f"{n} x {self.page_bytes} B pages (configs[0] sample of the same stream)",
                          n * self.page_bytes, buf, stride=self.page_bytes, length=self.page_bytes, count=n,
                          seed=self.seed)
+
+
+def shard_digest(page_bytes, count, seed, state):
+    """{xor, sum} the reference produced for this page batch (tests/golden:
+    pages_full for the state 0x5EED batch, pages_shards for rank shards), or None."""
+    g = _golden()
+    full = g["pages_full"]
+    if state == STATE and page_bytes == 4096 and count == full["count"]:
+        for d in full["digests"]:
+            if d["seed"] == seed:
+                return d
+    if state == STATE and page_bytes == 8192 and seed == 0xFDBEEFDB and count == full["digest_8k_fdbeefdb"]["count"]:
+        return full["digest_8k_fdbeefdb"]
+    for ents in g.get("pages_shards", {}).values():
+        for d in ents:
+            if (d["state"], d["page_bytes"], d["count"], d["seed"]) == (state, page_bytes, count, seed):
+                return d
+    return None
 
 
 def _varlen_digest(shape, lengths, seed):
@@ -394,10 +413,13 @@ class SqliteVerify:
         self.data_desc = (f"synthetic: splitmix64 pages (state 0x{STATE:X}) in HBM with XXH3 / CRC-32C / corrupt "
                           "trailers 12:3:1")
         self.config = {"workload": f"{count} x 4 KiB SQLite pages, mixed trailers, device-resident", "pages": count}
-        self.status = None
+        # caller-owned outputs: no allocation or fill inside the timed steps
+        self.status = torch.empty(count, dtype=torch.uint8, device=dev)
+        self.bad = torch.empty(1, dtype=torch.uint64, device=dev)
 
     def step(self, stream):
-        self.status, self.bad = self.PC.sqlite_verify_pages(self.buf, 4096, self.count, first_pgno=1, stream=stream)
+        self.PC.sqlite_verify_pages(self.buf, 4096, self.count, first_pgno=1, stream=stream, status=self.status,
+                                    bad=self.bad)
 
     def verify(self):
         from oracle import oracle as O

@@ -21,6 +21,8 @@ from .crc32c import (  # noqa: F401
     poison_lds,
     release_stream,
     stream_bytes,
+    stream_status,
+    workspace_status,
     testutil_lib,
     gpu_init,
     host_impl,

@@ -93,6 +93,10 @@ def lib():
         L.crc32c_gpu_release_stream.argtypes = [vp]
         L.crc32c_gpu_stream_bytes.restype = u64
         L.crc32c_gpu_stream_bytes.argtypes = [vp]
+        L.crc32c_gpu_stream_status.restype = ctypes.c_int
+        L.crc32c_gpu_stream_status.argtypes = [vp]
+        L.crc32c_gpu_workspace_status.restype = ctypes.c_int
+        L.crc32c_gpu_workspace_status.argtypes = [vp, vp]
         L.crc32c_host_register.restype = ctypes.c_int
         L.crc32c_host_register.argtypes = [vp, u64]
         L.crc32c_host_unregister.restype = ctypes.c_int
@@ -291,6 +295,20 @@ def release_stream(stream):
     _check(lib().crc32c_gpu_release_stream(_stream_handle(stream)), "crc32c_gpu_release_stream")
 
 
+def stream_status(stream=None):
+    """Wait for `stream`; raise CRC32CError (EINVAL) if a varlen/chained batch
+    on it was refused on the device since the last check (crc32c_gpu_stream_status)."""
+    _check(lib().crc32c_gpu_stream_status(_stream_handle(stream)), "crc32c_gpu_stream_status")
+
+
+def workspace_status(workspace, stream=None):
+    """Wait for `stream`; raise CRC32CError (EINVAL) if the last batch planned in
+    the caller-owned `workspace` was refused (crc32c_gpu_workspace_status)."""
+    _require_device(workspace, "workspace")
+    _check(lib().crc32c_gpu_workspace_status(ctypes.c_void_p(workspace.data_ptr()), _stream_handle(stream)),
+           "crc32c_gpu_workspace_status")
+
+
 def stream_bytes(stream=None):
     """Device bytes the library holds for `stream` (crc32c_gpu_stream_bytes)."""
     return int(lib().crc32c_gpu_stream_bytes(_stream_handle(stream)))
@@ -328,6 +346,11 @@ class Pipeline:
     def __init__(self, segment_bytes=64 << 20, nstreams=4, device=None):
         import numpy as np  # noqa: F401
         self._p = ctypes.c_void_p()
+        # ticket -> (host arrays the C job points into, results): held until
+        # poll/wait reports the job done (or close()), whether or not the
+        # caller keeps its PipelineJob -- the C side keeps raw pointers to all
+        # of them and touches them from any later submit/poll/wait
+        self._live = {}
         ctx = torch.cuda.device(device) if device is not None else _NullCtx()
         with ctx:
             _check(lib().crc32c_pipeline_create(ctypes.byref(self._p), segment_bytes, nstreams),
@@ -335,8 +358,20 @@ class Pipeline:
 
     def close(self):
         if self._p:
-            lib().crc32c_pipeline_destroy(self._p)
+            lib().crc32c_pipeline_destroy(self._p)  # synchronises every lane first
             self._p = ctypes.c_void_p()
+        self._live.clear()
+
+    def _job(self, ticket, result, keep):
+        self._live[ticket] = (keep, result)
+        if len(self._live) > 64:  # drop what finished behind the caller's back (jobs never polled)
+            for t in [t for t in self._live if t != ticket]:
+                if lib().crc32c_pipeline_poll(self._p, t) != 0:
+                    self._live.pop(t, None)
+        return PipelineJob(self, ticket, result)
+
+    def _retired(self, ticket):
+        self._live.pop(ticket, None)
 
     def __del__(self):
         try:
@@ -353,7 +388,7 @@ class Pipeline:
         return a.ctypes.data
 
     # The host arrays of a submitted job must stay alive until it completes:
-    # the pipeline keeps references to them per ticket.
+    # the pipeline keeps references to them per ticket (self._live).
     def _varlen_args(self, buf, offsets, lengths, seeds, out):
         import numpy as np
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -381,7 +416,7 @@ class Pipeline:
                                                    lengths.ctypes.data, n, seed & 0xFFFFFFFF, _np_ptr(sd),
                                                    ctypes.c_void_p(self._addr(out)), ctypes.byref(t)),
                "crc32c_pipeline_submit_varlen")
-        return PipelineJob(self, t.value, out, keep=(buf, offsets, lengths, sd))
+        return self._job(t.value, out, keep=(buf, offsets, lengths, sd))
 
     def submit_fixed(self, buf, stride, length, count, seed=0, seeds=None, out=None):
         out, sd = self._fixed_args(buf, stride, length, count, seeds, out)
@@ -389,7 +424,7 @@ class Pipeline:
         _check(lib().crc32c_pipeline_submit_fixed(self._p, ctypes.c_void_p(self._addr(buf)), stride, length, count,
                                                   seed & 0xFFFFFFFF, _np_ptr(sd), ctypes.c_void_p(self._addr(out)),
                                                   ctypes.byref(t)), "crc32c_pipeline_submit_fixed")
-        return PipelineJob(self, t.value, out, keep=(buf, sd))
+        return self._job(t.value, out, keep=(buf, sd))
 
     def varlen(self, buf, offsets, lengths, seed=0, seeds=None, out=None):
         offsets, lengths, n, sd, out = self._varlen_args(buf, offsets, lengths, seeds, out)
@@ -421,7 +456,7 @@ class Pipeline:
             _check(lib().fdb_sqlite_verify_pages_host_submit(self._p, ctypes.c_void_p(self._addr(pages)), page_size,
                                                              count, first_pgno, status.ctypes.data, bad.ctypes.data,
                                                              ctypes.byref(t)), "fdb_sqlite_verify_pages_host_submit")
-            return PipelineJob(self, t.value, (status, bad), keep=(pages,))
+            return self._job(t.value, (status, bad), keep=(pages,))
         _check(lib().fdb_sqlite_verify_pages_host(self._p, ctypes.c_void_p(self._addr(pages)), page_size, count,
                                                   first_pgno, status.ctypes.data, bad.ctypes.data),
                "fdb_sqlite_verify_pages_host")
@@ -439,7 +474,7 @@ class Pipeline:
             _check(lib().fdb_diskqueue_check_pages_host_submit(self._p, ctypes.c_void_p(self._addr(pages)), count,
                                                                ok.ctypes.data, bad.ctypes.data, ctypes.byref(t)),
                    "fdb_diskqueue_check_pages_host_submit")
-            return PipelineJob(self, t.value, (ok, bad), keep=(pages,))
+            return self._job(t.value, (ok, bad), keep=(pages,))
         _check(lib().fdb_diskqueue_check_pages_host(self._p, ctypes.c_void_p(self._addr(pages)), count,
                                                     ok.ctypes.data, bad.ctypes.data), "fdb_diskqueue_check_pages_host")
         return ok, bad
@@ -448,8 +483,8 @@ class Pipeline:
 class PipelineJob:
     """A submitted host-resident batch (crc32c_pipeline_poll / _wait)."""
 
-    def __init__(self, pipe, ticket, result, keep=()):
-        self.pipe, self.ticket, self.result, self._keep = pipe, ticket, result, keep
+    def __init__(self, pipe, ticket, result):
+        self.pipe, self.ticket, self.result = pipe, ticket, result
         self.done = False
 
     def poll(self):
@@ -457,13 +492,18 @@ class PipelineJob:
         if not self.done:
             rc = lib().crc32c_pipeline_poll(self.pipe._p, self.ticket)
             if rc < 0:
+                self.pipe._retired(self.ticket)  # finished (failed): the C side no longer touches its arrays
                 _check(rc, "crc32c_pipeline_poll")
             self.done = rc == 1
+            if self.done:
+                self.pipe._retired(self.ticket)
         return self.done
 
     def wait(self):
         if not self.done:
-            _check(lib().crc32c_pipeline_wait(self.pipe._p, self.ticket), "crc32c_pipeline_wait")
+            rc = lib().crc32c_pipeline_wait(self.pipe._p, self.ticket)
+            self.pipe._retired(self.ticket)  # finished either way
+            _check(rc, "crc32c_pipeline_wait")
             self.done = True
         return self.result
 

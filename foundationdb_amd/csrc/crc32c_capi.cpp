@@ -21,6 +21,7 @@ namespace fdbcrc {
 namespace {
 
 constexpr int kMaxDevices = 64;
+constexpr int kHstatErr = 6;  // u64 word of the stream's host-mapped block holding its refusal flag
 
 // Library-owned state of one (device, stream).  `mu` is held from the
 // workspace lookup through the enqueue of the kernels that use it, so a
@@ -127,27 +128,43 @@ int stream_workspace(DeviceState* st, hipStream_t s, uint64_t need, void** ws, u
 	return 0;
 }
 
+// The stream's host-mapped words: [0..2] route statistics of its last varlen
+// batch, [kHstatErr] its sticky refusal flag (crc32c_gpu_stream_status).
+bool stream_mapped(StreamState* ss) {
+	if (ss->hst_h) return true;
+	void* h = nullptr;
+	void* d = nullptr;
+	if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess) return false;
+	memset(h, 0, 64);
+	if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+		(void)hipHostFree(h);
+		return false;
+	}
+	ss->hst_h = static_cast<uint64_t*>(h);
+	ss->hst_d = static_cast<uint64_t*>(d);
+	return true;
+}
+
+uint32_t* stream_err(DeviceState* st, hipStream_t s) {
+	StreamState* ss = stream_state(st, s);
+	std::lock_guard<std::mutex> lock(g_mu);
+	return stream_mapped(ss) ? reinterpret_cast<uint32_t*>(ss->hst_d + kHstatErr) : nullptr;
+}
+
 // Route of the stream's next varlen batch from the span statistics its last
 // batch left (prep writes them into host-mapped memory; read without any
 // synchronisation: a stale or torn value only costs speed, never
 // correctness).  Caller holds the stream's lock.  Falls back to kRouteBoth.
 int stream_route(DeviceState* st, hipStream_t s, uint64_t** hstat) {
 	StreamState* ss = stream_state(st, s);
-	if (!ss->hst_h) {
-		void* h = nullptr;
-		void* d = nullptr;
-		if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess) {
-			*hstat = nullptr;
-			return kRouteBoth;
-		}
-		memset(h, 0, 64);
-		if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-			(void)hipHostFree(h);
-			*hstat = nullptr;
-			return kRouteBoth;
-		}
-		ss->hst_h = static_cast<uint64_t*>(h);
-		ss->hst_d = static_cast<uint64_t*>(d);
+	bool mapped;
+	{
+		std::lock_guard<std::mutex> lock(g_mu);
+		mapped = stream_mapped(ss);
+	}
+	if (!mapped) {
+		*hstat = nullptr;
+		return kRouteBoth;
 	}
 	*hstat = ss->hst_d;
 	static const int forced = [] {  // development: FDBCRC_ROUTE=0|1|2 pins the route
@@ -338,11 +355,13 @@ uint64_t crc32c_gpu_varlen_workspace_bytes(uint64_t count) {
 	return varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16);
 }
 
+// d_base may be null (the reference accepts any pointer for length 0, and
+// d_base = 0 makes the offsets absolute device addresses).
 static int batch_varlen_impl(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                              uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
                              uint64_t workspace_bytes, void* stream, int route, uint64_t* hstat) {
 	if (count == 0) return 0;
-	if (!d_out || !d_offsets || !d_lengths || !d_base)
+	if (!d_out || !d_offsets || !d_lengths)
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
@@ -353,7 +372,8 @@ static int batch_varlen_impl(const void* d_base, const uint64_t* d_offsets, cons
 	debug_window_varlen(d_base, d_offsets, d_lengths, count);
 #endif
 	launch_varlen(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, seed, d_seeds, d_out, st->tables,
-	              st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream), route, hstat);
+	              st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream), route, hstat,
+	              hstat ? reinterpret_cast<uint32_t*>(hstat + kHstatErr) : nullptr);
 #ifdef FDBCRC_DEBUG
 	(void)hipDeviceSynchronize();
 	debug_report("batch_varlen");
@@ -372,7 +392,7 @@ int crc32c_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, co
 int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                             uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
 	if (count == 0) return 0;
-	if (!d_out || !d_offsets || !d_lengths || !d_base)
+	if (!d_out || !d_offsets || !d_lengths)
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
@@ -397,12 +417,12 @@ uint64_t crc32c_gpu_chained_workspace_bytes(uint64_t nsegs) {
 	return align16(varlen_workspace_bytes(nsegs ? nsegs : 1, (uint64_t)st->num_cus * 16)) + align16(4 * nsegs + 4);
 }
 
-int crc32c_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
-                                uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
-                                const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace, uint64_t workspace_bytes,
-                                void* stream) {
+static int batch_chained_impl(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                              uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
+                              const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace, uint64_t workspace_bytes,
+                              void* stream, uint32_t* err) {
 	if (nchains == 0) return 0;
-	if (!d_out || !d_chain_starts || (nsegs && (!d_base || !d_seg_offsets || !d_seg_lengths)))
+	if (!d_out || !d_chain_starts || (nsegs && (!d_seg_offsets || !d_seg_lengths)))
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_chained: null pointer");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
@@ -413,16 +433,24 @@ int crc32c_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offset
 	uint32_t* segcrc = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_workspace) + vws);
 	if (nsegs)  // raw(0, M_j) of every segment: seed 0xffffffff
 		launch_varlen(static_cast<const uint8_t*>(d_base), d_seg_offsets, d_seg_lengths, nsegs, 0xffffffffu, nullptr,
-		              segcrc, st->tables, st->num_cus, d_workspace, s);
+		              segcrc, st->tables, st->num_cus, d_workspace, s, kRouteBoth, nullptr, err);
 	launch_chain_fold(d_chain_starts, nchains, d_seg_lengths, segcrc, seed, d_seeds, d_out, st->tables, st->num_cus, s);
 	return check_launch("crc32c_gpu_batch_chained launch");
+}
+
+int crc32c_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
+                                uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
+                                const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace, uint64_t workspace_bytes,
+                                void* stream) {
+	return batch_chained_impl(d_base, d_seg_offsets, d_seg_lengths, nsegs, d_chain_starts, nchains, seed, d_seeds, d_out,
+	                          d_workspace, workspace_bytes, stream, nullptr);
 }
 
 int crc32c_gpu_batch_chained(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
                              uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
                              const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
 	if (nchains == 0) return 0;
-	if (!d_out || !d_chain_starts || (nsegs && (!d_base || !d_seg_offsets || !d_seg_lengths)))
+	if (!d_out || !d_chain_starts || (nsegs && (!d_seg_offsets || !d_seg_lengths)))
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_chained: null pointer");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
@@ -432,8 +460,8 @@ int crc32c_gpu_batch_chained(const void* d_base, const uint64_t* d_seg_offsets, 
 	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), crc32c_gpu_chained_workspace_bytes(nsegs),
 	                              &ws, &have, &hold))
 		return rc;
-	return crc32c_gpu_batch_chained_ws(d_base, d_seg_offsets, d_seg_lengths, nsegs, d_chain_starts, nchains, seed,
-	                                   d_seeds, d_out, ws, have, stream);
+	return batch_chained_impl(d_base, d_seg_offsets, d_seg_lengths, nsegs, d_chain_starts, nchains, seed, d_seeds, d_out,
+	                          ws, have, stream, stream_err(st, reinterpret_cast<hipStream_t>(stream)));
 }
 
 // ---- XXH3-64 (include/fdb_xxh3.h) -------------------------------------------
@@ -556,8 +584,10 @@ uint64_t fdb_pagecheck_workspace_bytes(uint64_t count) { return fdbpc::workspace
 static int pages_ok(const void* d_pages, uint64_t page_size, uint64_t count, const void* d_out, const char* who) {
 	if (!d_pages || !d_out) return fail(FDB_CRC32C_EINVAL, who);
 	if (reinterpret_cast<uintptr_t>(d_pages) % 16) return fail(FDB_CRC32C_EINVAL, "pages must be 16-byte aligned");
-	if (page_size % 8 || page_size <= 248 || page_size >= (1ull << 31))
-		return fail(FDB_CRC32C_EINVAL, "page_size must be a multiple of 8 in (248, 2^31)");
+	// multiples of 16: every page then starts 16-byte aligned, as the kernels'
+	// 16-byte vector loads require (SQLite page sizes are powers of two >= 512)
+	if (page_size % 16 || page_size <= 248 || page_size >= (1ull << 31))
+		return fail(FDB_CRC32C_EINVAL, "page_size must be a multiple of 16 in (248, 2^31)");
 	if (count >= (1ull << 32)) return fail(FDB_CRC32C_EINVAL, "count must be < 2^32");
 	return 0;
 }
@@ -628,6 +658,34 @@ int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok
 }
 
 int crc32c_gpu_release_stream(void* stream) { return release_stream(reinterpret_cast<hipStream_t>(stream)); }
+
+int crc32c_gpu_stream_status(void* stream) {
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+	hipError_t e = hipStreamSynchronize(s);
+	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "crc32c_gpu_stream_status: hipStreamSynchronize", e);
+	StreamState* ss = stream_state(st, s);
+	std::lock_guard<std::mutex> lock(g_mu);
+	if (!ss->hst_h) return 0;
+	volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(ss->hst_h + kHstatErr);
+	if (!*w) return 0;
+	*w = 0;
+	return fail(FDB_CRC32C_EINVAL, "a variable-length batch on this stream was refused: it covered 2^32 - 1 or more "
+	                               "1 KiB windows (or 4 KiB blocks); its checksums are undefined");
+}
+
+int crc32c_gpu_workspace_status(const void* d_workspace, void* stream) {
+	if (!d_workspace) return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_workspace_status: null workspace");
+	uint64_t flag = 0;
+	hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+	hipError_t e = hipMemcpyAsync(&flag, varlen_refused_word(d_workspace), 8, hipMemcpyDeviceToHost, s);
+	if (e == hipSuccess) e = hipStreamSynchronize(s);
+	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "crc32c_gpu_workspace_status", e);
+	if (flag != 1) return 0;
+	return fail(FDB_CRC32C_EINVAL, "the last variable-length batch in this workspace was refused: it covered 2^32 - 1 "
+	                               "or more 1 KiB windows (or 4 KiB blocks); its checksums are undefined");
+}
 
 uint64_t crc32c_gpu_stream_bytes(void* stream) { return stream_bytes(reinterpret_cast<hipStream_t>(stream)); }
 

@@ -6,14 +6,10 @@
 
 namespace fdbcrc {
 
-// Window engine (crc32c_varlen.hip): passes of data in flight per wave while
-// one is computed (depth D: D + 1 blocks in rotation), and slots per table
-// (4 slots per pass, a multiple of D + 1 passes, so the next table's first
-// passes land in the first blocks again).
-#ifndef FDBCRC_V7_DEPTH
-#define FDBCRC_V7_DEPTH 1
-#endif
-constexpr uint32_t kV7TabSlots = FDBCRC_V7_DEPTH == 2 ? 60u : 64u;  // 15 or 16 passes
+// Window engine (crc32c_varlen.hip): slots per table (4 slots per pass, 16
+// passes: two blocks in ping-pong, so the next table's first pass lands in the
+// first block again).
+constexpr uint32_t kV7TabSlots = 64u;
 
 struct DevTables {
 	uint32_t slice[2][256];     // [0] byte + one zero byte (T1), [1] single byte (T0)
@@ -68,9 +64,15 @@ inline int route_for_stats(const volatile uint64_t* s) {
 	return win == 0 ? kRouteBlocks : kRouteBoth;
 }
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
+// err (device-visible, may be null): set to 1 (never cleared here) when the
+// planner refuses the batch -- 2^32 - 1 or more 1 KiB windows or 4 KiB route
+// blocks, which its 32-bit indices cannot number.  A refused batch writes no
+// checksums (the streaming kernels do nothing); the refusal is also left in
+// the workspace: varlen_refused_word(ws) is 1 after such a batch, else 0.
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
-                  hipStream_t stream, int route = kRouteBoth, uint64_t* hstat = nullptr);
+                  hipStream_t stream, int route = kRouteBoth, uint64_t* hstat = nullptr, uint32_t* err = nullptr);
+inline const uint64_t* varlen_refused_word(const void* ws) { return static_cast<const uint64_t*>(ws) + 6; }
 // Fixed stride, any length/alignment (same engine, same workspace size as varlen).
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
                          const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
@@ -79,7 +81,8 @@ int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, 
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
-                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat);
+                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat,
+                   uint32_t* err = nullptr);
 // Grouped chains (crc32c_chain.hip): out[c] = fold of segments [starts[c], starts[c+1])
 // whose independent registers segcrc[j] = crc32c_append(0xffffffff, segment j).
 int launch_chain_fold(const uint64_t* starts, uint64_t nchains, const uint64_t* lengths, const uint32_t* segcrc,

@@ -64,9 +64,19 @@ struct Job {
 	uint32_t first_pgno = 0;
 	bool pinned = false;
 	uint64_t next = 0;      // first buffer not yet issued
+	uint64_t piece = 0;     // next piece of buffer `next` when it is longer than a segment
 	uint32_t inflight = 0;  // segments issued, not retired
 	uint64_t bad = 0;
 	int rc = 0;
+	// buffers longer than a segment: checksummed in segment-sized pieces (piece 0
+	// with the buffer's seed, the others with seed 0) and folded with
+	// crc32c_combine once every piece has retired, in any order
+	struct Long {
+		std::vector<uint32_t> crc;
+		std::vector<uint64_t> len;
+		uint64_t left = 0;
+	};
+	std::map<uint64_t, Long> longs;
 	bool finished() const { return inflight == 0 && (rc != 0 || next >= count); }
 	size_t esize() const { return (kind == VARLEN || kind == FIXED) ? 4 : 1; }
 };
@@ -94,6 +104,7 @@ struct fdb_crc32c_pipeline {
 		hipEvent_t done = nullptr;
 		bool busy = false;
 		uint64_t ticket = 0, start = 0, n = 0, seq = 0;
+		uint64_t piece = ~0ull;  // piece index of a long buffer's segment (~0: a segment of whole buffers)
 	};
 	std::vector<Lane> lanes;
 	std::deque<Job> jobs;          // unfinished or unreported, in ticket order
@@ -142,25 +153,81 @@ void retire(Pipe* p, Pipe::Lane& L, hipError_t status) {
 	--j->inflight;
 	if (status != hipSuccess) {
 		if (!j->rc) j->rc = hip_fail("pipeline segment", status);
+	} else if (!j->rc && L.piece != ~0ull) {
+		auto it = j->longs.find(L.start);
+		if (it != j->longs.end()) {
+			Job::Long& g = it->second;
+			g.crc[L.piece] = L.h_res[0];
+			if (--g.left == 0) {  // crc32c_append(seed, P0 || P1 || ...) from the pieces' checksums
+				uint32_t c = g.crc[0];
+				for (size_t k = 1; k < g.crc.size(); ++k) c = crc32c_combine(c, g.crc[k], g.len[k]);
+				memcpy(j->out + L.start * 4, &c, 4);
+				j->longs.erase(it);
+			}
+		}
 	} else if (!j->rc) {
 		memcpy(j->out + L.start * j->esize(), L.h_res, L.n * j->esize());
 		if (j->kind == SQLITE || j->kind == DISKQUEUE) j->bad += *L.h_bad;
 	}
+	if (j->rc) j->longs.clear();
 	if (j->finished() && !j->rc && j->bad_out) *j->bad_out = j->bad;
+}
+
+// Enqueues the next piece of buffer j.next (longer than a segment) on lane L:
+// one segment-sized range through the device engine, its checksum D2H.
+int issue_piece(Pipe* p, Pipe::Lane& L, Job& j, uint64_t off, uint64_t len) {
+	const uint64_t i = j.next, k = j.piece;
+	const uint64_t npieces = (len + p->seg_bytes - 1) / p->seg_bytes;
+	if (k == 0) {
+		Job::Long& g = j.longs[i];
+		g.crc.assign(npieces, 0);
+		g.len.assign(npieces, 0);
+		g.left = npieces;
+	}
+	const uint64_t po = k * p->seg_bytes, pl = std::min(p->seg_bytes, len - po);
+	j.longs[i].len[k] = pl;
+	const uint8_t* src = j.base + off + po;
+	hipError_t e = hipSuccess;
+	if (!j.pinned) {
+		if (!L.h_stage && (e = hipHostMalloc(&L.h_stage, p->seg_bytes, hipHostMallocDefault)) != hipSuccess)
+			return set_error(FDB_CRC32C_ENOMEM, "pipeline: staging", e);
+		memcpy(L.h_stage, src, pl);
+		src = L.h_stage;
+	}
+	// the piece keeps its host alignment mod 16 (page-shaped pieces run the page kernel)
+	const uint64_t h = reinterpret_cast<uintptr_t>(j.base + off + po) % 16;
+	uint8_t* dst = L.d_data + h;
+	if ((e = hipMemcpyAsync(dst, src, pl, hipMemcpyHostToDevice, L.stream)) != hipSuccess) return hip_fail("H2D data", e);
+	const uint32_t seed = k ? 0u : (j.seeds ? j.seeds[i] : j.seed);
+	if (int rc = crc32c_gpu_batch_fixed(dst, 0, pl, 1, seed, nullptr, L.d_res, L.stream)) return rc;
+	if ((e = hipMemcpyAsync(L.h_res, L.d_res, 4, hipMemcpyDeviceToHost, L.stream)) != hipSuccess)
+		return hip_fail("D2H results", e);
+	if ((e = hipEventRecord(L.done, L.stream)) != hipSuccess) return hip_fail("hipEventRecord", e);
+	L.busy = true;
+	L.ticket = j.ticket;
+	L.start = i;
+	L.n = 1;
+	L.piece = k;
+	L.seq = ++p->seq;
+	++j.inflight;
+	if (++j.piece == npieces) {
+		j.piece = 0;
+		j.next = i + 1;
+	}
+	return 0;
 }
 
 // Builds and enqueues the next segment of `j` on free lane L.
 int issue(Pipe* p, Pipe::Lane& L, Job& j) {
 	const uint64_t i = j.next;
 	uint64_t n = 0, lo = 0, span = 0, h = 0;
+	L.piece = ~0ull;
 	if (j.kind == VARLEN) {
+		if (j.lens[i] > p->seg_bytes) return issue_piece(p, L, j, j.offs[i], j.lens[i]);
 		uint64_t a = ~0ull, b = 0;
 		while (i + n < j.count && n < p->max_bufs) {
 			const uint64_t o = j.offs[i + n], l = j.lens[i + n];
-			if (l > p->seg_bytes) {
-				if (n == 0) return inval("pipeline_varlen: buffer larger than the pipeline's segment");
-				break;
-			}
+			if (l > p->seg_bytes) break;  // a long buffer starts the next segment
 			const uint64_t na = l ? std::min(a, o) : a, nb = l ? std::max(b, o + l) : b;
 			if (n && nb > na && nb - na > p->seg_bytes) break;
 			a = na;
@@ -175,7 +242,10 @@ int issue(Pipe* p, Pipe::Lane& L, Job& j) {
 			L.h_meta[p->max_bufs + k] = j.lens[i + k];
 		}
 	} else {
-		if (j.length > p->seg_bytes) return inval("pipeline: buffer larger than the pipeline's segment");
+		if (j.length > p->seg_bytes) {
+			if (j.kind == FIXED) return issue_piece(p, L, j, i * j.stride, j.length);
+			return inval("pipeline: page larger than the pipeline's segment");
+		}
 		n = std::min(j.count - i, p->max_bufs);
 		if (j.stride) n = std::min(n, (p->seg_bytes - j.length) / j.stride + 1);
 		lo = i * j.stride;
@@ -262,7 +332,9 @@ void pump(Pipe* p) {
 	}
 }
 
-// 1 done, 0 pending, < 0 the job's error.
+// 1 done, 0 pending, < 0 the job's error.  A failed job's error is kept for
+// the pipeline's lifetime: every later poll/wait of its ticket reports it
+// again (never a success for results that were not written).
 int job_state(Pipe* p, uint64_t ticket) {
 	if (ticket == 0 || ticket >= p->next_ticket) return inval("pipeline: unknown ticket");
 	Job* j = find_job(p, ticket);
@@ -289,10 +361,7 @@ int wait(Pipe* p, uint64_t ticket) {
 	for (;;) {
 		pump(p);
 		int st = job_state(p, ticket);
-		if (st != 0) {
-			if (st == 1) p->failed.erase(ticket);
-			return st == 1 ? 0 : st;
-		}
+		if (st != 0) return st == 1 ? 0 : st;
 		Pipe::Lane* oldest = nullptr;  // block on the oldest segment in flight
 		for (auto& L : p->lanes)
 			if (L.busy && (!oldest || L.seq < oldest->seq)) oldest = &L;
@@ -411,9 +480,7 @@ int crc32c_pipeline_poll(fdb_crc32c_pipeline* p, uint64_t ticket) {
 	if (!p) return inval("pipeline: null pipeline");
 	DeviceScope ds(p->device);
 	pump(p);
-	int st = job_state(p, ticket);
-	if (st < 0) p->failed.erase(ticket);
-	return st;
+	return job_state(p, ticket);
 }
 
 int crc32c_pipeline_wait(fdb_crc32c_pipeline* p, uint64_t ticket) { return wait(p, ticket); }
@@ -440,8 +507,8 @@ int fdb_sqlite_verify_pages_host_submit(fdb_crc32c_pipeline* p, const void* h_pa
                                         uint64_t count, uint32_t first_pgno, uint8_t* h_status, uint64_t* h_bad,
                                         uint64_t* ticket) {
 	if (count && (!h_pages || !h_status)) return inval("fdb_sqlite_verify_pages_host: null pointer");
-	if (page_size % 8 || page_size <= 248 || page_size >= (1ull << 31))
-		return inval("page_size must be a multiple of 8 in (248, 2^31)");
+	if (page_size % 16 || page_size <= 248 || page_size >= (1ull << 31))
+		return inval("page_size must be a multiple of 16 in (248, 2^31)");
 	if (count >= (1ull << 32)) return inval("count must be < 2^32");
 	Job j;
 	j.kind = SQLITE;

@@ -191,6 +191,25 @@ __device__ __forceinline__ uint32_t scan_add(uint32_t v) {
 	return v;
 }
 
+// Saturating 32-bit add (UINT32_MAX absorbs): the planner's slot and block
+// counts are 32-bit; a batch whose totals reach 2^32 - 1 is refused (the
+// last prep tile sees the saturated total, so overflow anywhere is caught).
+__device__ __forceinline__ uint32_t sadd(uint32_t a, uint32_t b) {
+	const uint32_t s = a + b;
+	return s < a ? 0xFFFFFFFFu : s;
+}
+__device__ __forceinline__ uint32_t sat32(uint64_t v) { return v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)v; }
+// scan_add with saturation at every step.
+__device__ __forceinline__ uint32_t scan_sadd(uint32_t v) {
+	v = sadd(v, __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false));
+	v = sadd(v, __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false));
+	v = sadd(v, __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false));
+	v = sadd(v, __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false));
+	v = sadd(v, __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false));
+	v = sadd(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false));
+	return v;
+}
+
 // Inclusive prefix sum of a 64-bit value over the wave.
 __device__ __forceinline__ uint64_t scan64(uint64_t v, int lane) {
 #pragma unroll
@@ -260,14 +279,10 @@ constexpr uint32_t kTileW = 256;
 #ifndef FDBCRC_V7_THREADS
 #define FDBCRC_V7_THREADS 768  // 12 waves per CU: 155 VGPRs per lane, no VGPR spills
 #endif
-// Slot ranges per wave.  R > 1: a workgroup owns R ranges per wave; each wave
-// starts on one and grabs the next from its workgroup's counter as it
-// finishes (the SIMD's issue arbitration favours older waves, so equal
-// ranges finish at different times).
-#ifndef FDBCRC_V7_RANGES
-#define FDBCRC_V7_RANGES 1
-#endif
-constexpr uint64_t kV7RangesPerBlock = (FDBCRC_V7_THREADS / 64) * FDBCRC_V7_RANGES;
+// One static slot range per wave (dynamic ranges grabbed from per-workgroup
+// counters were measured slower: each range restart -- tile search, first
+// table build, pipeline refill -- costs more than the balance gains).
+constexpr uint64_t kV7RangesPerBlock = FDBCRC_V7_THREADS / 64;
 #ifndef FDBCRC_SELFSUM_TILES
 #define FDBCRC_SELFSUM_TILES 32
 #endif
@@ -326,7 +341,8 @@ __device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len, uint64_t bigmin 
 	const uint64_t span = E - g.A;
 	const bool big = bigmin && len >= 16 && span >= bigmin && span < kBigMax;
 	g.nb = big ? (uint32_t)((span + 4095) >> 12) : 0u;
-	g.W = (!big && len >= 16 && span > kSmallSpan) ? (uint32_t)((span + 1023) >> 10) : 0u;
+	// (saturated: a span of 4 TiB or more alone overflows the slot count)
+	g.W = (!big && len >= 16 && span > kSmallSpan) ? sat32((span >> 10) + ((span & 1023) != 0)) : 0u;
 	g.lo = (uint32_t)(1024 * (uint64_t)g.W - span) & 1023u;
 	g.k0 = (uint32_t)(P0 & 15);
 	g.zt = (uint32_t)(E - P1);
@@ -349,7 +365,6 @@ struct V7Params {
 	uint32_t* gs;              // first slot of each buffer
 	uint32_t* cl;              // lead edge term (team-sum form)
 	uint32_t* dummy;           // 64 words per wave: target of the no-op XORs
-	uint32_t* ctr;             // per workgroup: slot ranges grabbed (FDBCRC_V7_RANGES > 1)
 	const DevTables* tabs;
 	uint32_t qalign;           // slots per wave rounded to a multiple of this (power of two)
 	// big-buffer block route (bigmin = 0: off; hdr[2] blocks and hdr[3] entries in total)
@@ -364,7 +379,11 @@ struct V7Params {
 	uint32_t* bctr;            // block kernel grab counters (zeroed here)
 	uint32_t nbctr;            // ... words
 	uint64_t* hstat;           // route statistics of tile 0 (host-mapped, may be null): RouteStat
+	uint32_t* err;             // sticky refusal flag of the stream (host-mapped, may be null)
 };
+// hdr[6]: 1 if the planner refused the batch (2^32 - 1 or more windows or
+// blocks: 32-bit slot indices); the streaming kernels then do nothing.
+constexpr int kHdrRefused = 6;
 __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_t& off, uint64_t& len) {
 	off = P.offsets ? P.offsets[i] : i * P.stride;
 	len = P.lengths ? P.lengths[i] : P.length;
@@ -381,8 +400,8 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 		B = g.nb;
 		N = g.nb ? 1u : 0u;
 	}
-	W = scan_add(W);
-	B = scan_add(B);
+	W = scan_sadd(W);
+	B = scan_sadd(B);
 	N = scan_add(N);
 	if ((threadIdx.x & 63) == 63) {
 		part[0][threadIdx.x >> 6] = W;
@@ -436,8 +455,8 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		for (uint32_t u = 0; u < 8; ++u) {
 			const uint32_t k = k0 + u * blockDim.x;
 			const uint32_t kc = k < tile ? k : 0;
-			v[u] = (uint32_t)gld64(P.tsum + kc);
-			vB[u] = bigmin ? (uint32_t)gld64(P.bsum + kc) : 0u;
+			v[u] = sat32(gld64(P.tsum + kc));
+			vB[u] = bigmin ? sat32(gld64(P.bsum + kc)) : 0u;
 			vN[u] = bigmin ? (uint32_t)gld64(P.nsum + kc) : 0u;
 		}
 	};
@@ -446,10 +465,6 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = tv[k];
 #pragma unroll
 	for (int k = 0; k < 8; ++k) iz[threadIdx.x + 256 * k] = tv[4 + k];
-#if FDBCRC_V7_RANGES > 1
-	if (tile == 0)
-		for (uint64_t k = threadIdx.x; k < P.nwave / kV7RangesPerBlock; k += 256) P.ctr[k] = 0;
-#endif
 	if (tile == 0)
 		for (uint32_t k = threadIdx.x; k < P.nbctr; k += 256) P.bctr[k] = 0;
 	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
@@ -462,7 +477,9 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	// term (below, where out[] is initialised).
 	constexpr uint32_t NC = kSmallSpan / 16;
 	const bool small = ok && len >= 16 && !g.W && !g.nb;
-	const bool tailw = ok && g.W && g.zt;
+	// (not for a span of 4 TiB or more: W saturates, the batch is refused, and
+	// its end is not memory anyone holds)
+	const bool tailw = ok && g.W && g.W != 0xFFFFFFFFu && g.zt;
 	const uint64_t E16 = (P0 + len + 15) & ~uint64_t(15);
 	const uint32_t nch = small ? (uint32_t)(E16 - g.A) >> 4 : (tailw ? 1u : 0u);
 	const uint64_t cb = small ? g.A : E16 - 16;
@@ -483,8 +500,8 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 #pragma unroll
 		for (uint32_t u = 0; u < 8; ++u) {
 			const bool in = threadIdx.x + u * blockDim.x < tile;
-			pre += in ? v[u] : 0u;
-			preB += in ? vB[u] : 0u;
+			pre = sadd(pre, in ? v[u] : 0u);
+			preB = sadd(preB, in ? vB[u] : 0u);
 			preN += in ? vN[u] : 0u;
 		}
 	}
@@ -517,13 +534,14 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	}
 	// exclusive prefixes of this tile (window slots, route blocks, route
 	// entries): the sums of all earlier tiles, read in parallel by the whole
-	// block (no inter-block waiting).  Every total is below 2^32 (the engine's
-	// slot limit), so the sums are 32-bit.
+	// block (no inter-block waiting).  The engine's slot and block indices are
+	// 32-bit, so the sums are 32-bit and saturating: a batch whose total
+	// reaches 2^32 - 1 is refused by the last tile.
 	if (P.scanned) {
 		if (threadIdx.x == 0) {
-			pre = (uint32_t)P.tsum[tile];
+			pre = sat32(P.tsum[tile]);
 			if (bigmin) {
-				preB = (uint32_t)P.bsum[tile];
+				preB = sat32(P.bsum[tile]);
 				preN = (uint32_t)P.nsum[tile];
 			}
 		}
@@ -542,8 +560,8 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 			for (uint32_t u = 0; u < 8; ++u) {
 				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o[u], l[u], bigmin);
 				const bool in = j0 + u * blockDim.x < n;
-				pre += in ? gj.W : 0u;
-				preB += in ? gj.nb : 0u;
+				pre = sadd(pre, in ? gj.W : 0u);
+				preB = sadd(preB, in ? gj.nb : 0u);
 				preN += in && gj.nb ? 1u : 0u;
 			}
 		}
@@ -553,14 +571,14 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 #pragma unroll
 			for (uint32_t u = 0; u < 8; ++u) {
 				const bool in = k0 + u * blockDim.x < tile;
-				pre += in ? v[u] : 0u;
-				preB += in ? vB[u] : 0u;
+				pre = sadd(pre, in ? v[u] : 0u);
+				preB = sadd(preB, in ? vB[u] : 0u);
 				preN += in ? vN[u] : 0u;
 			}
 		}
 	}
-	pre = rdlane(scan_add(pre), 63);
-	preB = rdlane(scan_add(preB), 63);
+	pre = rdlane(scan_sadd(pre), 63);
+	preB = rdlane(scan_sadd(preB), 63);
 	preN = rdlane(scan_add(preN), 63);
 	if (lane == 0) {
 		s_pre[0][wv] = pre;
@@ -579,7 +597,7 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 #pragma unroll
 			for (int k = 0; k < 3; ++k) s_stat[wv][k] = c[k];
 	}
-	const uint32_t incl = scan_add(W), inclB = scan_add(B), inclN = scan_add(N);
+	const uint32_t incl = scan_sadd(W), inclB = scan_sadd(B), inclN = scan_add(N);
 	if (lane == 63) {
 		wsum[0][wv] = incl;
 		wsum[1][wv] = inclB;
@@ -588,28 +606,33 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	__syncthreads();
 	uint32_t inwave = 0, agg = 0, inB = 0, aggB = 0, inN = 0, aggN = 0;
 	for (int k = 0; k < 4; ++k) {
-		inwave += k < wv ? wsum[0][k] : 0u;
-		agg += wsum[0][k];
-		inB += k < wv ? wsum[1][k] : 0u;
-		aggB += wsum[1][k];
+		inwave = sadd(inwave, k < wv ? wsum[0][k] : 0u);
+		agg = sadd(agg, wsum[0][k]);
+		inB = sadd(inB, k < wv ? wsum[1][k] : 0u);
+		aggB = sadd(aggB, wsum[1][k]);
 		inN += k < wv ? wsum[2][k] : 0u;
 		aggN += wsum[2][k];
 	}
-	const uint32_t excl = s_pre[0][0] + s_pre[0][1] + s_pre[0][2] + s_pre[0][3];
-	const uint32_t exclB = s_pre[1][0] + s_pre[1][1] + s_pre[1][2] + s_pre[1][3];
+	const uint32_t excl = sadd(sadd(s_pre[0][0], s_pre[0][1]), sadd(s_pre[0][2], s_pre[0][3]));
+	const uint32_t exclB = sadd(sadd(s_pre[1][0], s_pre[1][1]), sadd(s_pre[1][2], s_pre[1][3]));
 	const uint32_t exclN = s_pre[2][0] + s_pre[2][1] + s_pre[2][2] + s_pre[2][3];
 	if (threadIdx.x == 0) {
 		if (tile == 0 && P.hstat)
 			for (int k = 0; k < 3; ++k) P.hstat[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
 		P.incl[tile] = (uint64_t)excl + agg;
 		if (tile + 1 == P.ntile) {
-			const uint64_t total = (uint64_t)excl + agg;
-			uint64_t q = (total + P.nwave - 1) / P.nwave;
+			const uint32_t total = sadd(excl, agg), blocks = sadd(exclB, aggB);
+			// 32-bit slot / block indices: 2^32 - 1 or more of either refuses the
+			// batch (the saturated totals stick at the limit)
+			const bool refused = total == 0xFFFFFFFFu || blocks == 0xFFFFFFFFu;
+			uint64_t q = ((uint64_t)total + P.nwave - 1) / P.nwave;
 			q = q < P.qalign ? P.qalign : (q + P.qalign - 1) & ~uint64_t(P.qalign - 1);
-			P.hdr[0] = total;
+			P.hdr[0] = refused ? 0 : total;
 			P.hdr[1] = q;
-			P.hdr[2] = (uint64_t)exclB + aggB;
+			P.hdr[2] = refused ? 0 : blocks;
 			P.hdr[3] = (uint64_t)exclN + aggN;
+			P.hdr[kHdrRefused] = refused ? 1 : 0;
+			if (refused && P.err) *P.err = 1u;
 		}
 	}
 	if (!ok) return;
@@ -726,15 +749,9 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	// leave before the table fill
 	if (r_base * Qs >= total) return;
 	fill_lds_b(lds, T);
-	uint64_t w = r_base + rdfirst(threadIdx.x >> 6);
-	for (;;) {
+	const uint64_t w = r_base + rdfirst(threadIdx.x >> 6);
 	const uint64_t lo_s64 = w * Qs;
-	if (lo_s64 >= total || w >= r_base + kV7RangesPerBlock) return;
-#if FDBCRC_V7_RANGES > 1
-	// the next range, requested now: the atomic returns in the shadow of this range
-	uint32_t nxt = 0;
-	if (lane == 0) nxt = atomicAdd(P.ctr + blockIdx.x, 1u);
-#endif
+	if (lo_s64 >= total) return;
 	const uint32_t lo_s = (uint32_t)lo_s64;
 	const uint32_t hi_s = (uint32_t)(lo_s64 + Qs < total ? lo_s64 + Qs : total);
 	// the tile holding slot lo_s: the number of tiles whose inclusive prefix is
@@ -959,52 +976,6 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		// holding window 0 carries the final inversion
 		atomicXor(fin ? P.out + bi_w + X.oi : P.dummy + w * 64 + lane, fin ? ((f & k7_INV) ? ~v : v) : 0u);
 	};
-#if FDBCRC_V7_DEPTH >= 2
-	// D + 1 blocks in rotation (a register copy would wait for the loads in
-	// flight): while pass p computes from one, passes p + 1 .. p + D load into
-	// the others -- 4D KiB in flight per wave.  Pass p of a table uses block
-	// p % (D + 1); a full table's pass count is a multiple of D + 1, so the
-	// next table's first D passes land in blocks 0 .. D - 1 again.
-	constexpr uint32_t D = FDBCRC_V7_DEPTH;
-	static_assert((kTS / 4) % (D + 1) == 0, "passes per table: a multiple of D + 1");
-	Block bk[D + 1];
-	// pass q of X (q < npX), else pass q - npX of the next table V (npV passes
-	// built), else a discarded re-read of X's pass 0: every path issues the
-	// same four loads into b
-	auto issue = [&](Block& b, const Tab7& X, const Tab7& V, uint32_t q, uint32_t npX, uint32_t npV) {
-		if (q < npX) load(b, X, q);
-		else if (q - npX < npV) load(b, V, q - npX);
-		else load(b, X, 0);
-	};
-	// all passes of table X (passes 0 .. D - 1 already issued into blocks
-	// 0 .. D - 1); V holds the previous table (phase 1 done) and is rebuilt
-	// as the next table
-	auto run_table = [&](Tab7& X, Tab7& V, uint32_t sbX, uint32_t fX) -> uint32_t {
-		const uint32_t npX = (fX + 3) >> 2;
-		issue(bk[D], X, V, D, npX, 0);
-		__builtin_amdgcn_sched_barrier(0);
-		phase2(V);
-		const uint32_t fY = fX == kTS ? build_table(V, sbX + kTS) : 0u;
-		const uint32_t npV = (fY + 3) >> 2;
-		__builtin_amdgcn_sched_barrier(0);
-		compute(bk[0], X, 0);
-		__builtin_amdgcn_sched_barrier(0);
-		for (uint32_t p = 1; p < npX;) {
-#pragma unroll
-			for (uint32_t r = 0; r <= D; ++r) {  // p = 1 + r (mod D + 1)
-				if (p >= npX) goto done;
-				issue(bk[(1 + r + D) % (D + 1)], X, V, p + D, npX, npV);
-				__builtin_amdgcn_sched_barrier(0);
-				compute(bk[(1 + r) % (D + 1)], X, p);
-				__builtin_amdgcn_sched_barrier(0);
-				++p;
-			}
-		}
-	done:
-		phase1(X, fX);
-		return fY;
-	};
-#else
 	// Two blocks in ping-pong (a register copy would wait for the loads in
 	// flight): pass p computes from one while pass p + 1 loads into the other.
 	// Full tables have 16 passes, so the next table's pass 0 lands in ba.
@@ -1063,7 +1034,6 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		phase1(X, fX);
 		return fY;
 	};
-#endif
 
 	Tab7 t0, t1;
 	t1.wa = 0;
@@ -1076,14 +1046,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	build();
 	uint32_t sb = 0;
 	uint32_t f0 = build_table(t0, 0);
-#if FDBCRC_V7_DEPTH >= 2
-	if (f0) {
-#pragma unroll
-		for (uint32_t j = 0; j < D; ++j) load(bk[j], t0, j < ((f0 + 3) >> 2) ? j : 0u);
-	}
-#else
 	if (f0) load(ba, t0, 0);
-#endif
 	while (f0) {
 		const uint32_t f1 = run_table(t0, t1, sb, f0);
 		sb += kTS;
@@ -1095,13 +1058,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		sb += kTS;
 		if (!f0) phase2(t1);
 	}
-#if FDBCRC_V7_RANGES > 1
-	w = r_base + wpb + rdfirst(__shfl((int)nxt, 0));
-#else
 	(void)wpb;
-	return;
-#endif
-	}
 }
 
 #ifndef FDBCRC_BIGMIN
@@ -1113,7 +1070,6 @@ static uint64_t al16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
 uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 	nwave = nwave > 16 * 1024 ? nwave : 16 * 1024;  // covers any launch geometry up to 1024 CUs
-	nwave *= FDBCRC_V7_RANGES;                      // virtual waves: one per slot range
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
 	return 64 + 32 * (ntile + 1) + al16(4 * nwave + 8 * count) + 256 * nwave + 4 * nwave + 64  // window route
 	       + 16 * (ntile + 1) + 8 * count + 4 * al16(4 * count)                                    // block route
@@ -1122,9 +1078,10 @@ uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
-                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat) {
+                   const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat,
+                   uint32_t* err) {
 	const uint64_t grid = (uint64_t)num_cus;
-	const uint64_t nwave = grid * kV7RangesPerBlock;  // one virtual wave per slot range
+	const uint64_t nwave = grid * kV7RangesPerBlock;  // one slot range per wave
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
 	uint8_t* wp = static_cast<uint8_t*>(ws);
 	V7Params P{};
@@ -1148,7 +1105,8 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	                                                            : bigmin_env;
 	if (route == kRouteBlocks && P.bigmin == 0) route = kRouteWindows;
 	P.hstat = hstat;
-	P.hdr = reinterpret_cast<uint64_t*>(wp);      // [0..3]; [4..7]: k_scan scratch of the route's tile sums
+	P.err = err;
+	P.hdr = reinterpret_cast<uint64_t*>(wp);      // [0..3] totals and quantum, [kHdrRefused] refusal flag
 	P.tsum = reinterpret_cast<uint64_t*>(wp + 64);
 	P.incl = P.tsum + ntile + 1;
 	P.bsum = P.incl + ntile + 1;
@@ -1157,8 +1115,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.gs = wave_tile + nwave;
 	P.cl = P.gs + count;
 	P.dummy = P.cl + count;
-	P.ctr = P.dummy + 64 * nwave;
-	uint8_t* rp = reinterpret_cast<uint8_t*>(P.ctr + nwave) + 64;
+	uint8_t* rp = reinterpret_cast<uint8_t*>(P.dummy + 64 * nwave + nwave) + 64;
 	rp = reinterpret_cast<uint8_t*>(al16(reinterpret_cast<uint64_t>(rp)));
 	P.eE = reinterpret_cast<uint64_t*>(rp);
 	rp += 8 * count;
@@ -1206,9 +1163,9 @@ uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) { return varlen7
 
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
-                  hipStream_t stream, int route, uint64_t* hstat) {
+                  hipStream_t stream, int route, uint64_t* hstat, uint32_t* err) {
 	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream, route,
-	                      hstat);
+	                      hstat, err);
 }
 
 // Fixed stride, any length and alignment: the same engine with metadata

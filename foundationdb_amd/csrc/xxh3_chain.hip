@@ -128,14 +128,20 @@ __global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ 
 	}
 }
 
+// Ranges are clamped into the staging area [0, cap) and the chain starts to
+// [0, nsegs]: a wrong total_bytes (or chain start) gives undefined digests,
+// never a read past the staging area or past pre[].
 __global__ __launch_bounds__(256) void k_chain_ranges(const uint64_t* __restrict__ starts, uint64_t nchains,
-                                                      const uint64_t* __restrict__ pre, uint64_t* __restrict__ ch_off,
-                                                      uint64_t* __restrict__ ch_len) {
+                                                      uint64_t nsegs, const uint64_t* __restrict__ pre, uint64_t cap,
+                                                      uint64_t* __restrict__ ch_off, uint64_t* __restrict__ ch_len) {
 	const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (c >= nchains) return;
-	const uint64_t a = pre[starts[c]], b = pre[starts[c + 1]];
+	const uint64_t s0 = starts[c], s1 = starts[c + 1];
+	uint64_t a = pre[s0 < nsegs ? s0 : nsegs], b = pre[s1 < nsegs ? s1 : nsegs];
+	a = a < cap ? a : cap;
+	b = b < cap ? b : cap;
 	ch_off[c] = a;
-	ch_len[c] = b - a;
+	ch_len[c] = b > a ? b - a : 0;
 }
 
 static uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
@@ -171,7 +177,8 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	} else if (hipMemsetAsync(pre, 0, 8, s) != hipSuccess) {
 		return -1;
 	}
-	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, pre, ch_off, ch_len);
+	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, nsegs, pre, total_bytes, ch_off,
+	                                                                   ch_len);
 	XxhParams P{};
 	P.base = staging;
 	P.offsets = ch_off;

@@ -949,16 +949,11 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		k_xscan<<<1, 1024, 0, stream>>>(tiles, ntile, nwave);
 		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(P.lengths, P.count, tiles, ntile, wave_first, nwave);
 		P.wave_first = wave_first;
-#ifndef FDBXXH_VROWS
-#define FDBXXH_VROWS 1
-#endif
-#if FDBXXH_VROWS
 		if (P.seeds)
 			k_xxh3_vrows<true><<<(unsigned)grid, 256, 0, stream>>>(P);
 		else
 			k_xxh3_vrows<false><<<(unsigned)grid, 256, 0, stream>>>(P);
 		return 0;
-#endif
 	}
 	if (!P.offsets && P.length > 240 && (mis & 7) == 0) {
 		// fixed-length pages: four per wave in lockstep

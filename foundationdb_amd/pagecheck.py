@@ -35,15 +35,29 @@ def _vp(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
-def sqlite_verify_pages(pages, page_size, count=None, first_pgno=1, stream=None):
-    """Returns (status uint8 tensor, bad-page count tensor) for a batch of SQLite pages."""
+def _outputs(pages, count, status, bad, who):
+    """Caller-owned output tensors (no allocation or fill per call), or new
+    ones.  The library stores the bad count (it does not accumulate into it),
+    so neither needs initialising."""
+    if status is None:
+        status = torch.empty(count, dtype=torch.uint8, device=pages.device)
+    _require_device(status, f"{who}: status", pages.device, (torch.uint8,), count)
+    if bad is None:
+        bad = torch.empty(1, dtype=torch.uint64, device=pages.device)
+    _require_device(bad, f"{who}: bad", pages.device, (torch.uint64, torch.int64), 1)
+    return status, bad
+
+
+def sqlite_verify_pages(pages, page_size, count=None, first_pgno=1, stream=None, status=None, bad=None):
+    """Returns (status uint8 tensor, bad-page count tensor) for a batch of SQLite
+    pages.  `status` (uint8, >= count) and `bad` (one 64-bit word) may be
+    caller-owned device tensors, reused across calls."""
     _require_device(pages, "pages")
     nbytes = pages.numel() * pages.element_size()
     count = nbytes // page_size if count is None else int(count)
     if count * page_size > nbytes:
         raise CRC32CError("sqlite_verify_pages: pages extend past the tensor")
-    status = torch.empty(count, dtype=torch.uint8, device=pages.device)
-    bad = torch.zeros(1, dtype=torch.uint64, device=pages.device)
+    status, bad = _outputs(pages, count, status, bad, "sqlite_verify_pages")
     with torch.cuda.device(pages.device):
         rc = _lib().fdb_sqlite_verify_pages(_vp(pages), page_size, count, first_pgno, _vp(status), _vp(bad),
                                             _stream_handle(stream))
@@ -51,15 +65,15 @@ def sqlite_verify_pages(pages, page_size, count=None, first_pgno=1, stream=None)
     return status, bad
 
 
-def diskqueue_check_pages(pages, count=None, stream=None):
-    """Returns (ok uint8 tensor, bad-page count tensor) for a batch of 4 KiB DiskQueue pages."""
+def diskqueue_check_pages(pages, count=None, stream=None, ok=None, bad=None):
+    """Returns (ok uint8 tensor, bad-page count tensor) for a batch of 4 KiB
+    DiskQueue pages (`ok` and `bad` may be caller-owned, as above)."""
     _require_device(pages, "pages")
     nbytes = pages.numel() * pages.element_size()
     count = nbytes // 4096 if count is None else int(count)
     if count * 4096 > nbytes:
         raise CRC32CError("diskqueue_check_pages: pages extend past the tensor")
-    ok = torch.empty(count, dtype=torch.uint8, device=pages.device)
-    bad = torch.zeros(1, dtype=torch.uint64, device=pages.device)
+    ok, bad = _outputs(pages, count, ok, bad, "diskqueue_check_pages")
     with torch.cuda.device(pages.device):
         rc = _lib().fdb_diskqueue_check_pages(_vp(pages), count, _vp(ok), _vp(bad), _stream_handle(stream))
     _check(rc, "fdb_diskqueue_check_pages")

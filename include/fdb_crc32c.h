@@ -88,7 +88,10 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
                            const uint32_t* d_seeds, uint32_t* d_out, void* stream);
 
 /* Buffer i is the d_lengths[i] bytes at d_base + d_offsets[i] (any alignment,
- * any order, overlaps allowed).  Seed as above.  Writes d_out[i].
+ * any order, overlaps allowed).  Seed as above.  Writes d_out[i].  d_base may
+ * be NULL (then the offsets are absolute device addresses; a zero-length
+ * buffer is never read, whatever its address -- as the reference accepts any
+ * pointer for length 0).
  * Work is balanced by bytes across the GPU, so one 1 MiB buffer among many
  * 64 B packets is split over several wavefronts and merged on the device.
  * Uses a library-owned workspace per (device, stream); it is allocated on
@@ -96,11 +99,20 @@ int crc32c_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length,
  * arrives.
  * Thread-safe: concurrent calls on the same stream serialise on the
  * stream's workspace from lookup to enqueue.
- * Limit: the engine numbers 1 KiB windows with 32-bit slot indices, so a
- * batch must cover fewer than 2^32 windows in total (about 4 TiB of
+ * Concurrency contract: the kernels read whole 16-byte-aligned chunks, so the
+ * bytes that share a buffer's first or last 16-byte chunk (outside the
+ * buffer) are read too, and more than once: they must not be modified while
+ * the call is in flight, or that buffer's checksum is undefined.  They are
+ * never written, and they always lie in the same page as buffer bytes.
+ * Limit: the engine numbers 1 KiB windows (and 4 KiB blocks) with 32-bit
+ * indices, so a batch must cover fewer than 2^32 - 1 of them (about 4 TiB of
  * checksummed bytes, overlapping buffers counted once each) -- far above what
  * one GPU holds unless buffers overlap heavily.  The lengths live in device
- * memory, so the host cannot refuse such a batch: its output is undefined. */
+ * memory, so such a batch is refused ON THE DEVICE: the planner reads only
+ * the metadata and each buffer's first chunk, the streaming kernels read
+ * nothing, the batch's checksums are undefined, and
+ * crc32c_gpu_stream_status(stream) reports FDB_CRC32C_EINVAL
+ * (crc32c_gpu_workspace_status for the _ws form). */
 int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                             uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
 
@@ -136,6 +148,17 @@ int crc32c_gpu_batch_chained_ws(const void* d_base, const uint64_t* d_seg_offset
                                 uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint32_t seed,
                                 const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace, uint64_t workspace_bytes,
                                 void* stream);
+
+/* Refusals made on the device (see crc32c_gpu_batch_varlen's limit).
+ * crc32c_gpu_stream_status waits for `stream` and returns FDB_CRC32C_EINVAL if
+ * a variable-length or chained batch enqueued on it through the
+ * library-workspace entry points has been refused since the last call (and
+ * clears the flag), else 0.  crc32c_gpu_workspace_status waits for `stream`
+ * and returns FDB_CRC32C_EINVAL if the LAST batch planned in the caller-owned
+ * workspace d_workspace (crc32c_gpu_batch_varlen_ws / _chained_ws) was
+ * refused, else 0.  Both synchronise: call them off the hot path. */
+int crc32c_gpu_stream_status(void* stream);
+int crc32c_gpu_workspace_status(const void* d_workspace, void* stream);
 
 /* Per-stream library state.  The library keeps, per (device, stream) it has
  * seen, the planning workspace of the convenience entry points and the page
@@ -174,7 +197,12 @@ uint64_t crc32c_gpu_stream_bytes(void* stream);
  *                             loop until it returns non-zero.
  *   crc32c_pipeline_wait      block until job `ticket` completes: 0 or < 0.
  * Synchronous form: crc32c_pipeline_varlen / _fixed = submit + wait.
- * A buffer longer than segment_bytes is refused (EINVAL). */
+ * Any buffer length is accepted (the reference's crc32c_append is total,
+ * contrib/crc32/crc32c.cpp:346-356): a buffer longer than segment_bytes is
+ * checksummed in segment-sized pieces on the free streams and the pieces are
+ * folded on the host with crc32c_combine -- exact by CRC linearity.  (Only
+ * the page verifiers need a whole page per segment: page_size <=
+ * segment_bytes.) */
 typedef struct fdb_crc32c_pipeline fdb_crc32c_pipeline;
 int crc32c_pipeline_create(fdb_crc32c_pipeline** out, uint64_t segment_bytes, int nstreams);
 void crc32c_pipeline_destroy(fdb_crc32c_pipeline* p);

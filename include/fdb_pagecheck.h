@@ -21,7 +21,8 @@
  *
  * Both: device pointers, asynchronous on `stream`, d_bad (optional, device
  * u64) receives the number of pages that failed.  Pages must be 16-byte
- * aligned, page_size a multiple of 8 in (248, 2^31), count < 2^32.  Return
+ * aligned, page_size a multiple of 16 in (248, 2^31) (every page 16-byte aligned;
+ * SQLite page sizes are powers of two from 512), count < 2^32.  Return
  * 0 or a negative FDB_CRC32C_E* status (crc32c_gpu_last_error() explains).
  */
 #ifndef FDB_PAGECHECK_H

@@ -55,8 +55,9 @@ int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, cons
  * bytes at d_base + d_seg_offsets[j]; d_chain_starts holds nchains + 1
  * non-decreasing values <= nsegs.  The segments are gathered on the device
  * into a staging area of `total_bytes` (the caller's bound on the sum of the
- * segment lengths: a smaller bound leaves the digests undefined, never writes
- * outside the workspace), then hashed per chain. */
+ * segment lengths: a smaller bound leaves the digests undefined, but no read or
+ * write leaves the workspace -- the per-chain ranges are clamped to the
+ * staging area and the chain starts to [0, nsegs]), then hashed per chain. */
 int xxh3_gpu_batch_chained(const void* d_base, const uint64_t* d_seg_offsets, const uint64_t* d_seg_lengths,
                            uint64_t nsegs, const uint64_t* d_chain_starts, uint64_t nchains, uint64_t total_bytes,
                            uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* stream);

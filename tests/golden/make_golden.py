@@ -10,6 +10,7 @@ JSON holds parameters and the reference's outputs only.
 Usage (in the container that has /root/reference):
     make -C oracle && python tests/golden/make_golden.py            # everything
     python tests/golden/make_golden.py --varlen                       # only "varlen_full"
+    python tests/golden/make_golden.py --shards                       # only "pages_shards"
 """
 import ctypes
 import json
@@ -58,7 +59,41 @@ def varlen_full(g):
     g["varlen_full"] = out
 
 
+def pages_shards(g, nshard=8, threads=8):
+    """BASELINE configs[3]: a whole-file scan (SQLiteDB::checkAllPageChecksums,
+    fdbserver/kvstore/KeyValueStoreSQLite.cpp:1378-1470) sharded over up to 8
+    GPUs -- rank r checksums bytes [r*4 GiB, (r+1)*4 GiB) of one splitmix64
+    file.  The reference's crc32c_append over every page of every shard, as 8 KiB
+    pages with the SQLite seed (pages8k) and as 4 KiB pages with seed 0
+    (pages4k), xor/sum digests per shard."""
+    from concurrent.futures import ThreadPoolExecutor
+    from bench_shapes import GOLDEN_GAMMA, SHARD_BYTES, shard_state
+    out = {"state": 0x5EED, "shard_bytes": SHARD_BYTES, "gamma": GOLDEN_GAMMA, "pages8k": [], "pages4k": []}
+    for r in range(nshard):
+        data = O.splitmix64(SHARD_BYTES // 8, shard_state(r)).view(np.uint8)
+        for name, pb, seed in (("pages8k", 8192, 0xFDBEEFDB), ("pages4k", 4096, 0)):
+            n = SHARD_BYTES // pb
+            cuts = [n * k // threads for k in range(threads + 1)]
+            with ThreadPoolExecutor(threads) as pool:
+                parts = list(pool.map(lambda k: O.reference_batch_fixed(data[cuts[k] * pb:], pb, pb, cuts[k + 1] - cuts[k],
+                                                                         seed=seed), range(threads)))
+            c = np.concatenate(parts)
+            out[name].append({"rank": r, "state": shard_state(r), "count": n, "page_bytes": pb, "seed": seed,
+                              "xor": int(np.bitwise_xor.reduce(c)), "sum": int(c.astype(np.uint64).sum())})
+            print(name, r, hex(out[name][-1]["xor"]), flush=True)
+        del data
+    g["pages_shards"] = out
+
+
 def main():
+    if "--shards" in sys.argv:
+        with open(OUT) as fh:
+            g = json.load(fh)
+        pages_shards(g)
+        with open(OUT, "w") as fh:
+            json.dump(g, fh, separators=(",", ":"))
+        print("updated pages_shards in", OUT)
+        return
     if "--varlen" in sys.argv:
         with open(OUT) as fh:
             g = json.load(fh)
@@ -166,6 +201,7 @@ def main():
                     "oneshot": crc(0, th_data[:1 << 20])}
 
     varlen_full(g)
+    pages_shards(g)
 
     with open(OUT, "w") as fh:
         json.dump(g, fh, separators=(",", ":"))

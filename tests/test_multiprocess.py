@@ -96,6 +96,7 @@ def test_bench_gpus2_launches_two_ranks():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["scaling"] == "weak" and rec["parity_ok"]
     assert [p["rank"] for p in rec["per_rank"]] == [0, 1]
+    assert [p["shard"] for p in rec["per_rank"]] == [0, 1] and rec["collective"] == "gloo"
     assert sum(p["bytes_per_step"] for p in rec["per_rank"]) * 3 / rec["value"] / (1 << 30) == \
         pytest.approx(max(p["elapsed_s"] for p in rec["per_rank"]), rel=0.02)
     assert rec["value"] > 0 and rec["steps"] == 3
@@ -122,3 +123,38 @@ def test_bench_refuses_world_size_mismatch():
                env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
     assert r.returncode != 0 and "world size 1 != --gpus 2" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_force_pg_world1_and_shard_base():
+    """--force-pg initialises the process group at world size 1 (the collective
+    path runs with one rank) and --shard-base K moves rank 0 to shard K."""
+    r = _bench(["--gpus", "1", "--steps", "2", "--warmup", "1", "--dry-cpu", "--force-pg", "--shard-base", "5"],
+               env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(_free_port())}, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["world_size"] == 1 and rec["collective"] == "gloo" and rec["per_rank"][0]["shard"] == 5
+
+
+@pytest.mark.gpu
+def test_bench_rccl_path_on_one_gpu():
+    """bench.py's multi-GPU path on the one-GPU box: torch.distributed.run
+    --nproc-per-node 1 with --force-pg initialises RCCL (init_process_group
+    "nccl", device_id) and gathers the per-rank stats with an RCCL all_gather,
+    as every rank of the driver's 8-GPU run does; --shard-base 5 makes the rank
+    checksum shard 5 of the global 8 KiB-page file (configs[3]) and check it
+    against the reference's digest of that shard (tests/golden pages_shards)."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--workload", "pages8k", "--steps", "3", "--warmup", "1", "--force-pg",
+           "--shard-base", "5", "--cpu-seconds", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["world_size"] == 1 and rec["collective"] == "nccl", rec
+    assert rec["parity_ok"] and rec["per_rank"][0]["shard"] == 5 and rec["per_rank"][0]["parity_ok"]
+    assert "shard 5" in rec["data"] and rec["value"] > 0

@@ -1,8 +1,13 @@
 """The CPU oracle (our restatement of contrib/crc32) against the reference's own outputs."""
+import json
+import os
+
 import numpy as np
 import pytest
 
 from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def sm_bytes(nbytes, state):
@@ -143,3 +148,27 @@ def test_oracle_chained_matches_reference_file_transfer(golden, oracle_mod):
     lens = [min(c["read"], c["nbytes"] - o) for o in offs]
     assert int(O.chained(data, offs, lens, [0, len(offs)], seed=c["seed"])[0]) == c["crc"]
     assert int(O.chained(data, [0], [c["nbytes"]], [0, 1])[0]) == c["oneshot"] == c["crc"]
+
+
+def test_shard_generator_jump_and_shard_digests():
+    """configs[3]: rank r checksums bytes [r*4 GiB, (r+1)*4 GiB) of one splitmix64
+    file, generated by jumping the generator (bench_shapes.shard_state); the jump
+    is exact (checked at small word offsets against the continuous stream), and
+    shard 0 of the reference-generated shard digests is the full-size page batch
+    (tests/golden pages_shards vs pages_full)."""
+    import bench_shapes as S
+    whole = O.splitmix64(4096, S.STATE)
+    for w in (1, 7, 512, 3000):
+        st = (S.STATE + w * S.GOLDEN_GAMMA) & 0xFFFFFFFFFFFFFFFF
+        assert np.array_equal(O.splitmix64(64, st), whole[w:w + 64])
+    assert S.shard_state(0) == S.STATE
+    assert S.shard_state(3) == (S.STATE + 3 * (S.SHARD_BYTES // 8) * S.GOLDEN_GAMMA) % (1 << 64)
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "crc32c_golden.json")))
+    sh, full = g["pages_shards"], g["pages_full"]
+    assert len(sh["pages8k"]) == 8 and len(sh["pages4k"]) == 8
+    assert [d["state"] for d in sh["pages8k"]] == [S.shard_state(r) for r in range(8)]
+    d0 = [d for d in full["digests"] if d["seed"] == 0][0]
+    assert (sh["pages4k"][0]["xor"], sh["pages4k"][0]["sum"]) == (d0["xor"], d0["sum"])
+    assert (sh["pages8k"][0]["xor"], sh["pages8k"][0]["sum"]) == (full["digest_8k_fdbeefdb"]["xor"],
+                                                                  full["digest_8k_fdbeefdb"]["sum"])
+    assert len({d["xor"] for d in sh["pages8k"]}) == 8  # the shards differ

@@ -223,3 +223,39 @@ def test_gpu_xxh3_chained_packet_buffers(cuda):
     e = torch.zeros(0, dtype=torch.int64, device=cuda)
     got = X.batch_chained(d, e, e, t([0, 0, 0]), seed=9).cpu().numpy().view(np.uint64)
     assert list(got) == [O.ref_xxh3_64(b"", 9)] * 2
+
+
+@pytest.mark.gpu
+def test_gpu_xxh3_chained_underestimated_total(cuda):
+    """A total_bytes below the real sum of the segment lengths (caller error):
+    the digests are undefined but every read stays inside the workspace
+    (k_chain_ranges clamps to the staging area), so the call completes and the
+    chains that fit in the bound are still exact; chain starts past nsegs are
+    clamped too."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    h = O.splitmix64((4 << 20) // 8, 0x51).view(np.uint8)
+    d = torch.from_numpy(h).to(cuda)
+    n = 4000
+    rng = np.random.default_rng(136)
+    offs = rng.integers(0, h.size - 70000, n)
+    lens = rng.integers(1000, 65536, n)
+    starts = np.arange(0, n + 1, 4)
+    t = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device=cuda)
+    total = int(lens.sum())
+    for bound in (total // 3, 4096, 0):
+        got = X.batch_chained(d, t(offs), t(lens), t(starts), total_bytes=bound)
+        torch.cuda.synchronize()
+        got = got.cpu().numpy().view(np.uint64)
+        # chains wholly inside the bound are exact
+        pre = np.concatenate([[0], np.cumsum(lens)])
+        c = 0
+        while c + 1 < starts.size and pre[starts[c + 1]] <= bound:
+            cat = b"".join(h[o:o + l].tobytes() for o, l in zip(offs[starts[c]:starts[c + 1]], lens[starts[c]:starts[c + 1]]))
+            assert int(got[c]) == O.ref_xxh3_64(cat)
+            c += 1
+    # chain starts past nsegs: clamped, no out-of-range read of the prefix array
+    got = X.batch_chained(d, t(offs[:8]), t(lens[:8]), t([0, 4, 1 << 40]), total_bytes=int(lens[:8].sum()))
+    torch.cuda.synchronize()
+    cat = b"".join(h[o:o + l].tobytes() for o, l in zip(offs[:4], lens[:4]))
+    assert int(got.cpu().numpy().view(np.uint64)[0]) == O.ref_xxh3_64(cat)
