@@ -130,8 +130,9 @@ def shard_digest(page_bytes, count, seed, state):
                 return d
     if state == STATE and page_bytes == 8192 and seed == 0xFDBEEFDB and count == full["digest_8k_fdbeefdb"]["count"]:
         return full["digest_8k_fdbeefdb"]
-    for ents in g.get("pages_shards", {}).values():
-        for d in ents:
+    sh = g.get("pages_shards", {})
+    for name in ("pages4k", "pages8k"):
+        for d in sh.get(name, []):
             if (d["state"], d["page_bytes"], d["count"], d["seed"]) == (state, page_bytes, count, seed):
                 return d
     return None

@@ -35,6 +35,10 @@ struct StreamState {
 	uint64_t ctr_bytes = 0;
 	uint64_t* hst_h = nullptr;  // varlen route statistics of the stream's last batch (host-mapped)
 	uint64_t* hst_d = nullptr;  // ... its device address
+	// extent route state (crc32c_extent.hip): grown to the batches seen
+	void* xmem = nullptr;
+	uint64_t xcount = 0, xblk = 0;  // buffers and extent blocks it holds
+	uint32_t xepoch = 0;            // launches on the extent route (epoch tags, never 0)
 };
 
 struct DeviceState {
@@ -167,12 +171,56 @@ int stream_route(DeviceState* st, hipStream_t s, uint64_t** hstat) {
 		return kRouteBoth;
 	}
 	*hstat = ss->hst_d;
-	static const int forced = [] {  // development: FDBCRC_ROUTE=0|1|2 pins the route
+	static const int forced = [] {  // development: FDBCRC_ROUTE=0|1|2|3 pins the route
 		const char* e = getenv("FDBCRC_ROUTE");
 		return e ? atoi(e) : -1;
 	}();
-	if (forced >= kRouteBoth && forced <= kRouteBlocks) return forced;
+	if (forced >= kRouteBoth && forced <= kRouteExtent) return forced;
 	return route_for_stats(ss->hst_h);
+}
+
+// The stream's extent-route state for a batch of `count` buffers (caller
+// holds the stream's lock).  Sized for the extent the stream's last checked
+// batch needed (hstat, written by the device) with headroom; a batch whose
+// extent is larger than what is held is routed to the window engine on the
+// device (the capacity flag) and the next call grows the state.  false: no
+// state (allocation failed): the caller routes to the window engine.
+bool stream_extent(DeviceState* st, hipStream_t s, uint64_t count, XState* xs) {
+	StreamState* ss = stream_state(st, s);
+	constexpr uint64_t kMaxBlk = 1ull << 26;  // 256 GiB extents
+	uint64_t need = ss->hst_h ? ss->hst_h[kHstatNblk] : 0;
+	need = need > kMaxBlk ? kMaxBlk : need;
+	if (!ss->xmem || count > ss->xcount || need > ss->xblk) {
+		if (ss->xmem) {
+			if (hipStreamSynchronize(s) != hipSuccess) return false;
+			(void)hipFree(ss->xmem);
+			ss->xmem = nullptr;
+		}
+		uint64_t nc = count > ss->xcount ? count + count / 4 : ss->xcount;
+		uint64_t nb = need + need / 4;
+		const uint64_t guess = count * 16 > 65536 ? count * 16 : 65536;  // first batch: 64 KiB per buffer
+		nb = nb > guess ? nb : guess;
+		nb = nb > ss->xblk ? nb : ss->xblk;
+		nb = nb > kMaxBlk ? kMaxBlk : nb;
+		void* m = nullptr;
+		const uint64_t bytes = extent_state_bytes(nc, nb, st->num_cus);
+		if (hipMalloc(&m, bytes) != hipSuccess) {
+			(void)hipGetLastError();
+			ss->xcount = ss->xblk = 0;
+			return false;
+		}
+		if (hipMemsetAsync(m, 0, 256, s) != hipSuccess) {  // the epoch-tagged flags
+			(void)hipFree(m);
+			return false;
+		}
+		ss->xmem = m;
+		ss->xcount = nc;
+		ss->xblk = nb;
+	}
+	extent_state_carve(ss->xmem, ss->xcount, ss->xblk, st->num_cus, xs);
+	if (++ss->xepoch == 0) ++ss->xepoch;
+	xs->epoch = ss->xepoch;
+	return true;
 }
 
 int check_launch(const char* what) {
@@ -227,6 +275,7 @@ int release_stream(hipStream_t stream) {
 	if (ss->ws) (void)hipFree(ss->ws);
 	if (ss->ctr) (void)hipFree(ss->ctr);
 	if (ss->hst_h) (void)hipHostFree(ss->hst_h);
+	if (ss->xmem) (void)hipFree(ss->xmem);
 	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "hipStreamSynchronize(release)", e);
 	return 0;
 }
@@ -237,7 +286,8 @@ uint64_t stream_bytes(hipStream_t stream) {
 	std::lock_guard<std::mutex> lock(g_mu);
 	auto it = st->streams.find(stream);
 	if (it == st->streams.end()) return 0;
-	return it->second->ws_bytes + it->second->ctr_bytes;
+	return it->second->ws_bytes + it->second->ctr_bytes +
+	       (it->second->xmem ? extent_state_bytes(it->second->xcount, it->second->xblk, st->num_cus) : 0);
 }
 
 // used by the host pipeline (crc32c_pipeline.cpp)
@@ -359,7 +409,8 @@ uint64_t crc32c_gpu_varlen_workspace_bytes(uint64_t count) {
 // d_base = 0 makes the offsets absolute device addresses).
 static int batch_varlen_impl(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                              uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
-                             uint64_t workspace_bytes, void* stream, int route, uint64_t* hstat) {
+                             uint64_t workspace_bytes, void* stream, int route, uint64_t* hstat,
+                             const XState* xs = nullptr) {
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths)
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
@@ -373,7 +424,7 @@ static int batch_varlen_impl(const void* d_base, const uint64_t* d_offsets, cons
 #endif
 	launch_varlen(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, seed, d_seeds, d_out, st->tables,
 	              st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream), route, hstat,
-	              hstat ? reinterpret_cast<uint32_t*>(hstat + kHstatErr) : nullptr);
+	              hstat ? reinterpret_cast<uint32_t*>(hstat + kHstatErr) : nullptr, xs);
 #ifdef FDBCRC_DEBUG
 	(void)hipDeviceSynchronize();
 	debug_report("batch_varlen");
@@ -403,8 +454,12 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 	                              varlen_workspace_bytes(count, (uint64_t)st->num_cus * 16), &ws, &have, &hold))
 		return rc;
 	uint64_t* hstat = nullptr;
-	const int route = stream_route(st, reinterpret_cast<hipStream_t>(stream), &hstat);
-	return batch_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream, route, hstat);
+	int route = stream_route(st, reinterpret_cast<hipStream_t>(stream), &hstat);
+	XState xs;
+	const bool ext = route == kRouteExtent && stream_extent(st, reinterpret_cast<hipStream_t>(stream), count, &xs);
+	if (route == kRouteExtent && !ext) route = kRouteWindows;
+	return batch_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream, route, hstat,
+	                         ext ? &xs : nullptr);
 }
 
 // ---- grouped chains ------------------------------------------------------------

@@ -213,6 +213,18 @@ __device__ __forceinline__ uint32_t row_xor(uint32_t v) {
 	return v;
 }
 
+// Inclusive prefix XOR of v over the wave (DPP row shifts, then the row
+// broadcasts of lanes 15 and 31): lane l gets v[0] ^ ... ^ v[l].
+__device__ __forceinline__ uint32_t wave_scanx(uint32_t v) {
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+	v ^= __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+	return v;
+}
+
 // XOR of v over all 64 lanes, returned wave-uniform.
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 	v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]

@@ -28,6 +28,10 @@ struct DevTables {
 	uint32_t chunkpow[256][8][16];   // x^(8*16*(255-c)): 16-byte chunk c of a pass block to the block's end
 	// big-buffer block route: block k (from the buffer's end) -> the buffer's end
 	uint32_t bpow[4][256][8][16];    // [i][j]: x^(8*4096*j*256^i)
+	// extent route (crc32c_extent.hip)
+	uint32_t xinv64[65][8][16];      // x^(-8*64*j): a prefix positioned at the block end -> back to lane span j before it
+	uint32_t pow64[64][8][16];       // x^(8*64*c)
+	uint32_t pow1[64][8][16];        // x^(8*d)   (with pow64 and bpow: x^(8*len) for any len < 2^40)
 };
 
 // Build the tables on the host (crc32c_tables.cpp).
@@ -57,12 +61,42 @@ int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32
 // more (route_for_stats() turns them into the next batch's route: blocks
 // when 16 KiB+ spans hold most bytes -- alone if no span is under 4 KiB --,
 // else windows).
-enum : int { kRouteBoth = 0, kRouteWindows = 1, kRouteBlocks = 2 };
+// kRouteExtent: the batch looks PACKED (buffers ascending, no overlaps, small
+// gaps -- packets back to back in a receive buffer, chunks of a file): the
+// extent route (crc32c_extent.hip) streams the whole covering byte range as
+// 4 KiB blocks and derives every buffer's CRC from two prefix registers; the
+// device checks the packing, and a batch that is not packed runs on the
+// window engine (launched behind it, guarded) instead.
+enum : int { kRouteBoth = 0, kRouteWindows = 1, kRouteBlocks = 2, kRouteExtent = 3 };
+// Host-mapped per-stream words (u64 indices): [0..2] span classes of the last
+// batch's first 256 buffers, [3] extent blocks the last extent-checked batch
+// needed, [4] 1 if the last batch's first 256 buffers were packed, [5] 1 if
+// the last extent-route batch failed the full packing check, [6] refusal flag.
+constexpr int kHstatNblk = 3, kHstatPacked = 4, kHstatXfail = 5;
 inline int route_for_stats(const volatile uint64_t* s) {
+	if (s[kHstatPacked] == 1 && s[kHstatXfail] != 1) return kRouteExtent;
 	const uint64_t win = s[0], mid = s[1], large = s[2];
 	if (large == 0 || large < win + mid) return kRouteWindows;  // (nothing windowed at all: windows, the cheaper launch)
 	return win == 0 ? kRouteBlocks : kRouteBoth;
 }
+// Extent route state of one stream (device memory owned by the library):
+// xhdr[0] the epoch of the last launch whose batch was found not packed,
+// xhdr[1] the epoch of the last launch whose extent exceeded the capacity;
+// per buffer the start / end point registers; per 4 KiB block of the extent
+// its raw register and its exclusive prefix; per 4096 blocks an aggregate.
+struct XState {
+	uint32_t* xhdr;
+	uint32_t* vs;
+	uint32_t* ve;
+	uint32_t* dummy;      // 128 words per wave of the stream kernel
+	uint32_t* blk;
+	uint32_t* ysc;
+	uint32_t* tagg;
+	uint64_t cap_blk;     // blocks the arrays hold
+	uint32_t epoch;       // this launch (never 0)
+};
+uint64_t extent_state_bytes(uint64_t count, uint64_t cap_blk, int num_cus);
+void extent_state_carve(void* mem, uint64_t count, uint64_t cap_blk, int num_cus, XState* x);
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 // err (device-visible, may be null): set to 1 (never cleared here) when the
 // planner refuses the batch -- 2^32 - 1 or more 1 KiB windows or 4 KiB route
@@ -71,7 +105,8 @@ uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 // the workspace: varlen_refused_word(ws) is 1 after such a batch, else 0.
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
-                  hipStream_t stream, int route = kRouteBoth, uint64_t* hstat = nullptr, uint32_t* err = nullptr);
+                  hipStream_t stream, int route = kRouteBoth, uint64_t* hstat = nullptr, uint32_t* err = nullptr,
+                  const XState* xs = nullptr);
 inline const uint64_t* varlen_refused_word(const void* ws) { return static_cast<const uint64_t*>(ws) + 6; }
 // Fixed stride, any length/alignment (same engine, same workspace size as varlen).
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
@@ -82,7 +117,13 @@ uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                    const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat,
-                   uint32_t* err = nullptr);
+                   uint32_t* err = nullptr, const XState* xs = nullptr);
+// The extent route's streaming and finishing kernels (crc32c_extent.hip),
+// launched by launch_varlen7 for kRouteExtent after the packing check.
+int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
+                  uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
+                  const DevTables* tabs, int num_cus, const XState& xs, uint64_t* hstat, hipStream_t stream,
+                  int phase);
 // Grouped chains (crc32c_chain.hip): out[c] = fold of segments [starts[c], starts[c+1])
 // whose independent registers segcrc[j] = crc32c_append(0xffffffff, segment j).
 int launch_chain_fold(const uint64_t* starts, uint64_t nchains, const uint64_t* lengths, const uint32_t* segcrc,

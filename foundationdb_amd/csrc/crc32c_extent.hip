@@ -1,0 +1,506 @@
+// Extent route of the variable-length engine (gfx950): batches whose buffers
+// are PACKED -- ascending, no overlaps, small gaps: packets back to back in a
+// receive buffer (fdbrpc/FlowTransport.cpp:1260-1364 scans them out of one),
+// chunks of a file (fdbrpc/FileTransfer.cpp:29-37).  Reference semantics:
+// crc32c_append (contrib/crc32/crc32c.cpp:346-356) per buffer.
+//
+// The whole covering byte range -- the EXTENT [S, Eend), S = the first
+// buffer's start rounded down to 16 -- is streamed as 4 KiB blocks exactly
+// like 4 KiB pages (k_pages4k's loads, permlane swizzle, register chains), so
+// no byte is padded and nothing is masked.  Every buffer's CRC comes from two
+// PREFIX registers of that stream (CRC linearity; tests/extent_model.py is
+// the byte-exact CPU model):
+//     raw(bytes [s, e)) = R(e) ^ R(s) * x^(8(e - s)),   R(p) = raw(bytes [S, S+p))
+// so the gap bytes between buffers cancel.  For a point p (relative to S)
+// in block k = (p-1) >> 12 with cnt = (p - 4096k) >> 6 whole lane spans
+// before it:
+//     R(p64) = (Y[k] ^ V(p)) * x^(-8*64*(64-cnt)),       p64 = 4096k + 64cnt
+//     R(p)   = R(p64) fed the p - p64 < 64 bytes after p64
+// V(p) = H_k[cnt-1] is the block's lane registers weighted to the block end
+// (the page kernel's fold) XOR-prefixed up to lane cnt-1 -- the stream kernel
+// captures it for every point of its blocks -- and Y[k] is the exclusive
+// prefix of the block registers positioned at block k's end (a scan).  Then
+//     crc32c_append(seed, buffer) = ~(R(e) ^ (R(s) ^ ~seed) * x^(8 len)).
+//
+//   k_v7count (crc32c_varlen.hip)  the packing check (epoch-tagged flags) and
+//                                  the window engine's tile sums (its fallback)
+//   k_xstream   static block ranges per wave; per block: chains, lane weights,
+//               prefix XOR (DPP), the block register; the points of the block
+//               from a window of 64 buffers in the lanes (ds_bpermute)
+//   k_xs1/k_xs2 the block-register scan (tiles of 4096 blocks)
+//   k_xfin      per buffer: R(s), R(e) (the < 64-byte remainders re-read),
+//               x^(8 len), the final inversion
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_common.h"
+
+namespace fdbcrc {
+
+namespace {
+
+typedef __attribute__((address_space(1))) const uint32_t xg_u32;
+typedef __attribute__((address_space(1))) const uint64_t xg_u64;
+__device__ __forceinline__ uint32_t xld32(const uint32_t* p) { return *((xg_u32*)reinterpret_cast<uintptr_t>(p)); }
+__device__ __forceinline__ uint64_t xld64(const uint64_t* p) { return *((xg_u64*)reinterpret_cast<uintptr_t>(p)); }
+
+// Lane-parallel multiply by a constant whose nibble tables are in global
+// memory (8 gathers, L2-resident).
+__device__ __forceinline__ uint32_t xmul(const uint32_t (*tab)[16], uint32_t v) {
+	uint32_t r = 0;
+#pragma unroll
+	for (int n = 0; n < 8; ++n) r ^= xld32(&tab[n][(v >> (4 * n)) & 15u]);
+	return r;
+}
+
+struct XParams {
+	const uint8_t* base;
+	const uint64_t* offsets;   // nullptr: fixed stride
+	const uint64_t* lengths;   // nullptr: fixed length
+	uint64_t stride, length, count;
+	uint32_t seed;
+	const uint32_t* seeds;
+	uint32_t* out;
+	XState x;
+	const DevTables* tabs;
+	uint64_t* hstat;
+};
+
+__device__ __forceinline__ void x_buffer(const XParams& P, uint64_t i, uint64_t& P0, uint64_t& P1) {
+	const uint64_t off = P.offsets ? xld64(P.offsets + i) : i * P.stride;
+	const uint64_t len = P.lengths ? xld64(P.lengths + i) : P.length;
+	P0 = reinterpret_cast<uint64_t>(P.base) + off;
+	P1 = P0 + len;
+}
+
+// Wave-uniform: the batch passed the packing and capacity checks of this
+// launch (k_v7count stored the launch's epoch where it failed one).
+__device__ __forceinline__ bool x_packed(const XParams& P) {
+	const uint32_t a = rdfirst(xld32(P.x.xhdr)), b = rdfirst(xld32(P.x.xhdr + 1));
+	return a != P.x.epoch && b != P.x.epoch;
+}
+__device__ __forceinline__ bool x_unordered(const XParams& P) { return rdfirst(xld32(P.x.xhdr)) == P.x.epoch; }
+
+struct XGeo {
+	uint64_t S, Eend, nblk;
+};
+// The extent of a packed batch: its first buffer's start rounded down to 16,
+// its last buffer's end rounded up to 16.
+__device__ __forceinline__ XGeo x_geo(const XParams& P) {
+	uint64_t a0, a1, b0, b1;
+	x_buffer(P, 0, a0, a1);
+	x_buffer(P, P.count - 1, b0, b1);
+	XGeo g;
+	g.S = rdfirst64(a0 & ~uint64_t(15));
+	g.Eend = rdfirst64((b1 + 15) & ~uint64_t(15));
+	g.nblk = (g.Eend - g.S + 4095) >> 12;
+	return g;
+}
+
+// Point p (bytes from S): its block and the whole lane spans before it in
+// that block (0..64).  p = 0 maps to block 0 with no span before it: the
+// register captured there is 0, as R(0) is.
+__device__ __forceinline__ uint32_t x_blk(uint64_t p) { return p ? (uint32_t)((p - 1) >> 12) : 0u; }
+__device__ __forceinline__ uint32_t x_cnt(uint64_t p, uint32_t k) {
+	return p ? (uint32_t)((p - 4096ull * k) >> 6) : 0u;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// k_xstream: the extent as 4 KiB blocks, static block ranges per wave
+// ---------------------------------------------------------------------------
+constexpr uint32_t kXU = 2;  // blocks per unit (register chains interleaved)
+
+__global__ __launch_bounds__(1024) void k_xstream(XParams P) {
+	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat)  // for the stream's next route choice
+		P.hstat[kHstatXfail] = x_unordered(P) ? 1 : 0;
+	if (!x_packed(P)) return;  // the window engine (launched behind) checksums this batch
+	if (x_geo(P).nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
+	FillRegs fill;
+	fill_issue_1024(fill, P.tabs);  // table loads in flight while the ranges are found
+	__shared__ uint32_t lds[kLdsBytesB / 4];
+	const XGeo G = x_geo(P);
+	const LaneCtx c = make_ctx();
+	const uint32_t lane = (uint32_t)c.lane;
+	const uint32_t col4 = (lane & 31) * 4;
+	const uint32_t c4 = col4 | 0x10000u;
+	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
+	const uint32_t wi = rdfirst(threadIdx.x >> 6);
+	const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wi;
+	// static ranges of whole units (the extent's blocks are consecutive)
+	const uint64_t per = (((G.nblk + nwave - 1) / nwave) + 2 * kXU - 1) / (2 * kXU) * (2 * kXU);
+	const uint64_t k0 = w * per < G.nblk ? w * per : G.nblk;
+	const uint64_t k1 = k0 + per < G.nblk ? k0 + per : G.nblk;
+	// The extent's last block may run past its end: it is left out of the main
+	// loop (whose loads then need no clamping, and no branch: a branch around
+	// a load makes the compiler wait for every load in flight) and done at
+	// the end by its wave with clamped loads.
+	const uint64_t km = k1 < G.nblk ? k1 : G.nblk - 1;  // main-loop blocks [k0, km)
+	const uint64_t ksafe = km > k0 ? km - 1 : 0;        // (only used when km > k0)
+	auto load_blk = [&](Block& b, uint64_t k) {
+		const uint64_t kk = k < km ? k : ksafe;  // past the range: duplicates, discarded
+		load_block(b, reinterpret_cast<const uint8_t*>(G.S + 4096ull * kk), c.ld_off);
+	};
+	Block u0[kXU], u1[kXU];
+	if (km > k0) {  // (a wave without main-loop blocks loads nothing here: its block may be the last)
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) load_blk(u0[j], k0 + j);
+	}
+
+	// ---- window of 64 buffers (lane j <-> buffer q + j): its points -------
+	// the first buffer whose end lies past this range's start (64-ary narrowing)
+	const uint64_t T0 = G.S + 4096ull * k0;
+	uint64_t qa = 0, qm = P.count;
+	while (qm > 64) {
+		const uint64_t stp = (qm + 63) >> 6;
+		const uint64_t kk = (uint64_t)lane * stp;
+		bool le = false;
+		if (kk < qm) {
+			uint64_t a, b;
+			x_buffer(P, qa + (kk + stp - 1 < qm ? kk + stp - 1 : qm - 1), a, b);
+			le = b <= T0;
+		}
+		const uint64_t cnt = __builtin_popcountll(__ballot(le));
+		qa += cnt * stp;
+		qm = cnt * stp + stp <= qm ? stp : qm - cnt * stp;
+	}
+	uint64_t q;
+	{
+		bool le = false;
+		if (lane < qm) {
+			uint64_t a, b;
+			x_buffer(P, qa + lane, a, b);
+			le = b <= T0;
+		}
+		q = qa + __builtin_popcountll(__ballot(le));
+	}
+	uint32_t wbs, wbe, wcs, wce, wlast;  // per lane: start / end blocks and spans; uniform: last end block
+	uint32_t Vs = 0, Ve = 0;
+	uint64_t pf0 = 0, pf1 = 0;  // the next window's buffer (prefetched one window ahead)
+	auto prefetch = [&](uint64_t q0) {
+		const uint64_t j = q0 + lane < P.count ? q0 + lane : P.count - 1;
+		x_buffer(P, j, pf0, pf1);
+	};
+	auto make_window = [&](uint64_t q0) {
+		const bool ok = q0 + lane < P.count;
+		const uint64_t s = pf0 - G.S, e = pf1 - G.S;
+		wbs = ok ? x_blk(s) : 0xFFFFFFFEu;
+		wbe = ok ? x_blk(e) : 0xFFFFFFFEu;
+		wcs = x_cnt(s, wbs);
+		wce = x_cnt(e, wbe);
+		wlast = q0 + 64 <= P.count ? rdlane(wbe, 63) : 0xFFFFFFFFu;  // the batch's last window never retires
+		Vs = 0;
+		Ve = 0;
+	};
+	uint32_t* const dmy = P.x.dummy + 128 * w;
+	// the window's points that lie in this wave's blocks leave (the others
+	// belong to the neighbouring ranges); unconditional stores
+	auto flush = [&](uint64_t q0) {
+		const bool ok = q0 + lane < P.count;
+		const bool os = ok && wbs >= k0 && wbs < k1, oe = ok && wbe >= k0 && wbe < k1;
+		*(os ? P.x.vs + q0 + lane : dmy + lane) = Vs;
+		*(oe ? P.x.ve + q0 + lane : dmy + 64 + lane) = Ve;
+	};
+	prefetch(q);
+	make_window(q);
+	prefetch(q + 64);
+
+	fill_commit_1024(fill, lds);
+	if (k0 >= k1) return;
+
+	// ---- blocks -------------------------------------------------------------
+	uint32_t mine = 0;       // lane k - gs: register of block k of the current group
+	uint64_t gs = k0;        // first block of the group
+	auto store_group = [&](uint64_t n) {
+		*((uint64_t)lane < n ? P.x.blk + gs + lane : dmy + lane) = mine;
+	};
+	// chains, lane weights and the prefix XOR over the lanes of one unit
+	auto unit_h = [&](Block (&u)[kXU], uint32_t (&H)[kXU]) {
+		uint32_t x[kXU];
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) {
+			unswizzle(u[j]);
+			x[j] = u[j].r[0][0];
+		}
+#pragma unroll
+		for (int wd = 0; wd < 16; ++wd)
+#pragma unroll
+			for (uint32_t j = 0; j < kXU; ++j)
+				x[j] = word_step4_next(lds, x[j], wd < 15 ? u[j].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u, c4);
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) H[j] = wave_scanx(mul_nibbles(lds, x[j], c_lane));
+	};
+	// the window's points in block kb (branch-free: two permutes per block)
+	auto capture = [&](uint32_t H, uint32_t kb, bool valid) {
+		const bool hs = valid && wbs == kb, he = valid && wbe == kb;
+		const uint32_t ts = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((wcs ? wcs - 1 : 0) << 2), (int)H);
+		const uint32_t te = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((wce ? wce - 1 : 0) << 2), (int)H);
+		Vs = hs ? (wcs ? ts : 0u) : Vs;
+		Ve = he ? (wce ? te : 0u) : Ve;
+	};
+	// the registers and points of blocks k .. k + 2U - 1 (those before kend)
+	auto finish = [&](const uint32_t (&H)[2 * kXU], uint64_t k, uint64_t kend) {
+#pragma unroll
+		for (uint32_t j = 0; j < 2 * kXU; ++j) {
+			const uint32_t B = rdlane(H[j], 63);
+			mine = lane == (uint32_t)(k + j - gs) ? B : mine;
+		}
+#pragma unroll
+		for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], (uint32_t)(k + j), k + j < kend);
+		// every buffer of the window ends in these blocks: the next 64 (rare
+		// for packets of KiBs; the blocks' prefixes are still in registers)
+		while ((uint64_t)wlast < k + 2 * kXU) {
+			flush(q);
+			q += 64;
+			make_window(q);
+			prefetch(q + 64);
+#pragma unroll
+			for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], (uint32_t)(k + j), k + j < kend);
+		}
+		const uint64_t kn = k + 2 * kXU < kend ? k + 2 * kXU : kend;
+		if (kn - gs >= 64 || kn == kend) {  // a full group, or the range's end
+			store_group(kn - gs);
+			gs = kn;
+		}
+	};
+	// two units in ping-pong: one computes while the other's loads are in
+	// flight (a register copy of a block in flight would wait for its loads)
+	for (uint64_t k = k0; k < km; k += 2 * kXU) {
+		uint32_t H[2 * kXU];
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) load_blk(u1[j], k + kXU + j);
+		__builtin_amdgcn_sched_barrier(0);
+		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]));
+		__builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) load_blk(u0[j], k + 2 * kXU + j);
+		__builtin_amdgcn_sched_barrier(0);
+		unit_h(u1, reinterpret_cast<uint32_t(&)[kXU]>(H[kXU]));
+		__builtin_amdgcn_sched_barrier(0);
+		finish(H, k, km);
+	}
+	if (km < k1) {  // the extent's last block: chunks past its end re-read its last chunk (never used)
+		const uint64_t last_chunk = G.Eend - 16;
+		const uint64_t a = G.S + 4096ull * km + c.ld_off;
+#pragma unroll
+		for (int q2 = 0; q2 < 4; ++q2) {
+			const uint64_t o = a + 2048u * (q2 & 1) + 1024u * (q2 >> 1);
+			u0[0].r[q2] = ld16(reinterpret_cast<const uint8_t*>(o <= last_chunk ? o : last_chunk));
+		}
+		u0[1] = u0[0];
+		uint32_t H[2 * kXU];
+		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]));
+		H[2] = H[3] = 0;
+		finish(H, km, k1);
+	}
+	flush(q);
+}
+
+// ---------------------------------------------------------------------------
+// Block-register scan: Y[k] = X_k * M, X_0 = 0, X_{k+1} = X_k * M ^ B[k]
+// (M = x^(8*4096)), in tiles of 4096 blocks (1024 threads x 4).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kXTile = 4096;
+
+// v * M^m for 0 <= m < 2^32 blocks (bpow: x^(8*4096*j*256^i)); the levels no
+// lane needs are skipped.
+__device__ __forceinline__ uint32_t xmul_blocks(const DevTables* T, uint32_t v, uint32_t m) {
+	v = xmul(T->bpow[0][m & 255u], v);
+	if (__ballot(m >> 8)) v = xmul(T->bpow[1][(m >> 8) & 255u], v);
+	if (__ballot(m >> 16)) v = xmul(T->bpow[2][(m >> 16) & 255u], v);
+	if (__ballot(m >> 24)) v = xmul(T->bpow[3][m >> 24], v);
+	return v;
+}
+
+// XOR over the workgroup (1024 threads), returned to every thread.
+__device__ __forceinline__ uint32_t x_block_xor(uint32_t v, uint32_t* s_w) {
+	v = wave_xor(v);
+	if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+	__syncthreads();
+	uint32_t r = 0;
+	for (uint32_t k = 0; k < (blockDim.x >> 6); ++k) r ^= s_w[k];
+	__syncthreads();
+	return r;
+}
+
+__global__ __launch_bounds__(1024) void k_xs1(XParams P) {
+	__shared__ uint32_t s_w[16];
+	if (!x_packed(P)) return;
+	const XGeo G = x_geo(P);
+	const DevTables* T = P.tabs;
+	for (uint64_t t = blockIdx.x; t * kXTile < G.nblk; t += gridDim.x) {
+		const uint64_t b0 = t * kXTile + 4 * threadIdx.x;
+		uint32_t B[4];
+#pragma unroll
+		for (int j = 0; j < 4; ++j) B[j] = b0 + j < G.nblk ? xld32(P.x.blk + b0 + j) : 0u;
+		uint32_t a = B[0];
+#pragma unroll
+		for (int j = 1; j < 4; ++j) a = xmul(T->block, a) ^ B[j];
+		a = xmul_blocks(T, a, 4 * (1023 - threadIdx.x));  // to the tile's end
+		a = x_block_xor(a, s_w);
+		if (threadIdx.x == 0) P.x.tagg[t] = a;
+	}
+}
+
+__device__ void x_scan_tile(const XParams& P, const XGeo& G, const DevTables* T, uint32_t t, uint32_t* s_w) {
+	const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+	// the register at the tile's start: the earlier tiles' aggregates, each
+	// shifted over the tiles after it
+	uint32_t xt = 0;
+	for (uint32_t u = tid; u < t; u += blockDim.x) xt ^= xmul_blocks(T, xld32(P.x.tagg + u), kXTile * (t - 1 - u));
+	xt = x_block_xor(xt, s_w);
+	// this thread's four blocks: inclusive chain c_j, positioned at block 4t'+j's end
+	const uint64_t b0 = (uint64_t)t * kXTile + 4 * tid;
+	uint32_t B[4], cj[4];
+#pragma unroll
+	for (int j = 0; j < 4; ++j) B[j] = b0 + j < G.nblk ? xld32(P.x.blk + b0 + j) : 0u;
+	cj[0] = B[0];
+#pragma unroll
+	for (int j = 1; j < 4; ++j) cj[j] = xmul(T->block, cj[j - 1]) ^ B[j];
+	// prefix over the threads of the wave (each step shifts by 4 blocks per thread)
+	uint32_t in = cj[3];
+#pragma unroll
+	for (uint32_t d = 1; d < 64; d <<= 1) {
+		const uint32_t y = (uint32_t)__shfl_up((int)in, d);
+		const uint32_t ys = xmul(T->bpow[0][4 * d], y);
+		in ^= lane >= d ? ys : 0u;
+	}
+	if (lane == 63) s_w[wv] = in;
+	__syncthreads();
+	// the earlier waves of the tile: lane j < wv holds wave j's total, shifted
+	// over the 256 (wv - 1 - j) blocks between it and this wave
+	uint32_t pw = lane < wv ? xmul(T->bpow[1][wv - 1 - lane], s_w[lane]) : 0u;
+	pw = wave_xor(pw);
+	uint32_t ex = (uint32_t)__shfl_up((int)in, 1);
+	ex = lane ? ex : 0u;  // this thread's start, relative to its wave's start
+	uint32_t ts = xmul(T->bpow[0][4 * lane], pw) ^ ex;  // ... relative to the tile's start
+	uint32_t xs = xmul_blocks(T, xt, 4 * tid) ^ ts;     // the extent prefix at this thread's first block
+	// Y[4t'+j] = X_{4t'+j} * M = xs * M^(j+1) ^ c_j ^ B_j
+#pragma unroll
+	for (int j = 0; j < 4; ++j)
+		if (b0 + j < G.nblk) P.x.ysc[b0 + j] = xmul(T->bpow[0][j + 1], xs) ^ cj[j] ^ B[j];
+	__syncthreads();  // s_w is reused by the next tile
+}
+
+__global__ __launch_bounds__(1024) void k_xs2(XParams P) {
+	__shared__ uint32_t s_w[16];
+	if (!x_packed(P)) return;
+	const XGeo G = x_geo(P);
+	const DevTables* T = P.tabs;
+	for (uint64_t tt = blockIdx.x; tt * kXTile < G.nblk; tt += gridDim.x)
+		x_scan_tile(P, G, T, (uint32_t)tt, s_w);
+}
+
+// ---------------------------------------------------------------------------
+// k_xfin: one buffer per thread
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_xfin(XParams P) {
+	__shared__ uint32_t s4[4][256];
+	if (!x_packed(P)) return;
+	const DevTables* T = P.tabs;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = xld32(&T->slice4[k][threadIdx.x]);
+	const XGeo G = x_geo(P);
+	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const bool ok = i < P.count;
+	const uint64_t ic = ok ? i : P.count - 1;
+	uint64_t P0, P1;
+	x_buffer(P, ic, P0, P1);
+	const uint32_t sd = P.seeds ? xld32(P.seeds + ic) : P.seed;
+	const uint64_t sp = P0 - G.S, ep = P1 - G.S;
+	const uint32_t vs = xld32(P.x.vs + ic), ve = xld32(P.x.ve + ic);
+	__syncthreads();
+	// R(p): the prefix register at point p (0 at p = 0)
+	auto R = [&](uint64_t p, uint32_t v) -> uint32_t {
+		const uint32_t k = x_blk(p);
+		const uint32_t cnt = x_cnt(p, k);
+		const uint64_t p64 = p ? 4096ull * k + 64ull * cnt : 0;
+		const uint32_t y = p ? xld32(P.x.ysc + k) : 0u;
+		uint32_t r = xmul(T->xinv64[64 - cnt], y ^ v);  // (k = ~0 only at p = 0: y = v = 0 there... v unused)
+		r = p ? r : 0u;
+		const uint32_t rem = (uint32_t)(p - p64);  // < 64 bytes after the lane span
+		const uint8_t* src = reinterpret_cast<const uint8_t*>(G.S + p64);
+		u32x4 ch[4];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) ch[q] = 16 * q < rem ? ld16(src + 16 * q) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+		for (uint32_t q = 0; q < 16; ++q) {
+			if (4 * q + 4 <= rem) {
+				r ^= ch[q >> 2][q & 3];
+				r = s4[0][r & 255u] ^ s4[1][(r >> 8) & 255u] ^ s4[2][(r >> 16) & 255u] ^ s4[3][r >> 24];
+			}
+		}
+		const uint32_t wd = rem >> 2, nb = rem & 3u;
+		if (nb) {
+			uint32_t word = 0;
+#pragma unroll
+			for (uint32_t q = 0; q < 16; ++q) word = q == wd ? ch[q >> 2][q & 3] : word;
+			for (uint32_t b = 0; b < nb; ++b) r = (r >> 8) ^ s4[3][(r ^ (word >> (8 * b))) & 255u];
+		}
+		return r;
+	};
+	const uint32_t re = R(ep, ve);
+	uint32_t rs = R(sp, vs) ^ ~sd;
+	// rs * x^(8 len), len = 4096a + 64c + d
+	const uint64_t len = P1 - P0;
+	rs = xmul(T->pow1[len & 63u], rs);
+	rs = xmul(T->pow64[(len >> 6) & 63u], rs);
+	if (__ballot(len >> 12)) rs = xmul_blocks(T, rs, (uint32_t)(len >> 12));
+	if (ok) P.out[i] = ~(re ^ rs);
+}
+
+// ---------------------------------------------------------------------------
+// state and launch
+// ---------------------------------------------------------------------------
+static uint64_t xal(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+uint64_t extent_state_bytes(uint64_t count, uint64_t cap_blk, int num_cus) {
+	const uint64_t nwave = (uint64_t)num_cus * 16;
+	return 256 + 2 * xal(4 * count) + xal(512 * nwave) + 2 * xal(4 * cap_blk) + xal(4 * (cap_blk / kXTile + 1));
+}
+
+void extent_state_carve(void* mem, uint64_t count, uint64_t cap_blk, int num_cus, XState* x) {
+	uint8_t* p = static_cast<uint8_t*>(mem);
+	const uint64_t nwave = (uint64_t)num_cus * 16;
+	x->xhdr = reinterpret_cast<uint32_t*>(p);
+	p += 256;
+	x->vs = reinterpret_cast<uint32_t*>(p);
+	p += xal(4 * count);
+	x->ve = reinterpret_cast<uint32_t*>(p);
+	p += xal(4 * count);
+	x->dummy = reinterpret_cast<uint32_t*>(p);
+	p += xal(512 * nwave);
+	x->blk = reinterpret_cast<uint32_t*>(p);
+	p += xal(4 * cap_blk);
+	x->ysc = reinterpret_cast<uint32_t*>(p);
+	p += xal(4 * cap_blk);
+	x->tagg = reinterpret_cast<uint32_t*>(p);
+	x->cap_blk = cap_blk;
+}
+
+// phase 0: the streaming kernel; phase 1: scan + finish.  Every kernel
+// returns at once when the packing check failed.
+int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
+                  uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
+                  const DevTables* tabs, int num_cus, const XState& xs, uint64_t* hstat, hipStream_t stream,
+                  int phase) {
+	if (count == 0) return 0;
+	XParams P{};
+	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
+	P.seed = seed; P.seeds = seeds; P.out = out; P.x = xs; P.tabs = tabs; P.hstat = hstat;
+	if (phase == 0) {
+		k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+	} else {
+		// tiles past the extent: none (grid-stride over the batch's tiles)
+		uint64_t ntile = xs.cap_blk / kXTile + 1;
+		ntile = ntile < (uint64_t)num_cus ? ntile : (uint64_t)num_cus;
+		k_xs1<<<(unsigned)ntile, 1024, 0, stream>>>(P);
+		k_xs2<<<(unsigned)ntile, 1024, 0, stream>>>(P);
+		k_xfin<<<(unsigned)((count + 255) / 256), 256, 0, stream>>>(P);
+	}
+	return 0;
+}
+
+}  // namespace fdbcrc

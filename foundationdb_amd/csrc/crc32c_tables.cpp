@@ -36,6 +36,11 @@ void build_dev_tables(DevTables* t) {
 	for (int c = 0; c < 256; ++c) mul_tables_nibble(xpow8(16u * (255 - c)), t->chunkpow[c]);
 	for (int i = 0; i < 4; ++i)
 		for (int j = 0; j < 256; ++j) mul_tables_nibble(xpow8((4096ull * j) << (8 * i)), t->bpow[i][j]);
+	for (int j = 0; j <= 64; ++j) mul_tables_nibble(xpow8_inv(64u * j), t->xinv64[j]);
+	for (int c = 0; c < 64; ++c) {
+		mul_tables_nibble(xpow8(64u * c), t->pow64[c]);
+		mul_tables_nibble(xpow8(c), t->pow1[c]);
+	}
 	for (int m = 0; m < 64; ++m) {
 		// x^(8*2^m) by repeated squaring of x^8
 		uint32_t c = kOne >> 8;

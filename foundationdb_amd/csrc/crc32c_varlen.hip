@@ -380,6 +380,11 @@ struct V7Params {
 	uint32_t nbctr;            // ... words
 	uint64_t* hstat;           // route statistics of tile 0 (host-mapped, may be null): RouteStat
 	uint32_t* err;             // sticky refusal flag of the stream (host-mapped, may be null)
+	// extent route (kRouteExtent, crc32c_extent.hip): the count kernel checks
+	// the packing; prep and the window kernel run only if the check failed
+	uint32_t* xhdr;            // [0] / [1]: epoch of the last launch found not packed / over capacity
+	uint32_t epoch;
+	uint64_t xcap;             // extent blocks the route's arrays hold
 };
 // hdr[6]: 1 if the planner refused the batch (2^32 - 1 or more windows or
 // blocks: 32-bit slot indices); the streaming kernels then do nothing.
@@ -388,17 +393,76 @@ __device__ __forceinline__ void v7_buffer(const V7Params& P, uint64_t i, uint64_
 	off = P.offsets ? P.offsets[i] : i * P.stride;
 	len = P.lengths ? P.lengths[i] : P.length;
 }
+// Buffers i and i + 1 are PACKED (the extent route's condition): in order,
+// no overlap, and a gap below 4096 bytes and at most max(len_i, 256) (the gap
+// is read: bounded waste, and every gap byte lies in a page that holds buffer
+// bytes).  tests/extent_model.py: eligible().
+__device__ __forceinline__ bool v7_packed_pair(const V7Params& P, uint64_t i, uint64_t off, uint64_t len) {
+	if (i + 1 >= P.count) return true;
+	uint64_t on, ln;
+	v7_buffer(P, i + 1, on, ln);
+	(void)ln;
+	const uint64_t e = off + len;
+	const uint64_t gap = on - e;
+	return on >= e && gap < 4096 && gap <= (len > 256 ? len : 256);
+}
+// Wave-uniform: this launch routes the batch to the extent kernels (the
+// window engine's kernels then return at once).
+__device__ __forceinline__ bool v7_extent_taken(const V7Params& P) {
+	if (!P.xhdr) return false;
+	const uint32_t a = rdfirst(gld32(P.xhdr)), b = rdfirst(gld32(P.xhdr + 1));
+	return a != P.epoch && b != P.epoch;
+}
+// The first 256 buffers' bytes by span class and whether they are packed,
+// for the stream's next route choice (tile 0 of prep, or of the count kernel
+// on the extent route).  All threads of the block call it.
+__device__ void v7_route_stats(const V7Params& P, uint64_t i, uint64_t off, uint64_t len, uint64_t (*s_stat)[4]) {
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const bool ok = i < P.count;
+	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
+	const uint64_t span = ok && len >= 16 ? ((P0 + len + 15) & ~uint64_t(15)) - (P0 & ~uint64_t(15)) : 0;
+	uint64_t c[4] = {span > kSmallSpan && span < 4096 ? len : 0, span >= 4096 && span < 16384 ? len : 0,
+	                 span >= 16384 ? len : 0, (ok && !v7_packed_pair(P, i, off, len)) ? 1u : 0u};
+#pragma unroll
+	for (int k = 0; k < 4; ++k)
+		for (int o = 32; o > 0; o >>= 1) c[k] += __shfl_xor(c[k], o);
+	if (lane == 0)
+#pragma unroll
+		for (int k = 0; k < 4; ++k) s_stat[wv][k] = c[k];
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int k = 0; k < 3; ++k) P.hstat[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
+		P.hstat[kHstatPacked] = (s_stat[0][3] | s_stat[1][3] | s_stat[2][3] | s_stat[3][3]) ? 0 : 1;
+	}
+}
 __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 	__shared__ uint32_t part[3][4];
+	__shared__ uint64_t s_stat[4][4];
 	const uint64_t i = (uint64_t)blockIdx.x * kTileW + threadIdx.x;
 	uint32_t W = 0, B = 0, N = 0;
+	uint64_t off = 0, len = 0;
 	if (i < P.count) {
-		uint64_t off, len;
 		v7_buffer(P, i, off, len);
 		const Geo7 g = geo7(reinterpret_cast<uint64_t>(P.base) + off, len, P.bigmin);
 		W = g.W;
 		B = g.nb;
 		N = g.nb ? 1u : 0u;
+	}
+	if (P.xhdr) {  // extent route: the packing check, epoch-tagged (no flag is ever reset)
+		const bool bad = i < P.count && !v7_packed_pair(P, i, off, len);
+		if (__ballot(bad) && (threadIdx.x & 63) == 0) P.xhdr[0] = P.epoch;
+		if (blockIdx.x == 0 && threadIdx.x == 0) {
+			uint64_t o0, l0, o1, l1;
+			v7_buffer(P, 0, o0, l0);
+			v7_buffer(P, P.count - 1, o1, l1);
+			const uint64_t S = (reinterpret_cast<uint64_t>(P.base) + o0) & ~uint64_t(15);
+			const uint64_t E = (reinterpret_cast<uint64_t>(P.base) + o1 + l1 + 15) & ~uint64_t(15);
+			// (an unordered batch may give E < S: the packing check refuses it anyway)
+			const uint64_t nblk = E > S ? (E - S + 4095) >> 12 : 0;
+			if (nblk > P.xcap || E - S >= (1ull << 40)) P.xhdr[1] = P.epoch;
+			if (P.hstat) P.hstat[kHstatNblk] = nblk;
+		}
+		if (blockIdx.x == 0 && P.hstat) v7_route_stats(P, i, off, len, s_stat);
 	}
 	W = scan_sadd(W);
 	B = scan_sadd(B);
@@ -422,12 +486,13 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 // and entries are compiled out (fewer registers: 8 blocks per CU).
 template <bool BIG>
 __device__ __forceinline__ void v7prep(const V7Params& P) {
+	if (v7_extent_taken(P)) return;  // the extent kernels checksum this batch
 	const uint64_t bigmin = BIG ? P.bigmin : 0;
 	__shared__ uint32_t s4[4][256];    // slice4 tables (no bank replication: this kernel is not LDS-bound)
 	__shared__ uint32_t iz[16 * 128];  // inv_z nibble tables: x^(-8z), z < 16 (small buffers' trailing zeros)
 	__shared__ uint32_t wsum[3][4];
 	__shared__ uint32_t s_pre[3][4];
-	__shared__ uint64_t s_stat[4][3];
+	__shared__ uint64_t s_stat[4][4];
 	const DevTables* T = P.tabs;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	// Latency chain: the table loads, this thread's metadata and the first
@@ -586,17 +651,7 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		s_pre[2][wv] = preN;
 	}
 	const uint32_t W = ok ? g.W : 0u, B = ok ? g.nb : 0u, N = (ok && g.nb) ? 1u : 0u;
-	if (tile == 0 && P.hstat) {  // the first 256 buffers' bytes by span class, for the host's next route choice
-		const uint64_t span = ok && len >= 16 ? ((P0 + len + 15) & ~uint64_t(15)) - (P0 & ~uint64_t(15)) : 0;
-		uint64_t c[3] = {span > kSmallSpan && span < 4096 ? len : 0, span >= 4096 && span < 16384 ? len : 0,
-		                 span >= 16384 ? len : 0};
-#pragma unroll
-		for (int k = 0; k < 3; ++k)
-			for (int o = 32; o > 0; o >>= 1) c[k] += __shfl_xor(c[k], o);
-		if (lane == 0)
-#pragma unroll
-			for (int k = 0; k < 3; ++k) s_stat[wv][k] = c[k];
-	}
+	if (tile == 0 && P.hstat && !P.xhdr) v7_route_stats(P, i, off, len, s_stat);
 	const uint32_t incl = scan_sadd(W), inclB = scan_sadd(B), inclN = scan_add(N);
 	if (lane == 63) {
 		wsum[0][wv] = incl;
@@ -617,8 +672,6 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	const uint32_t exclB = sadd(sadd(s_pre[1][0], s_pre[1][1]), sadd(s_pre[1][2], s_pre[1][3]));
 	const uint32_t exclN = s_pre[2][0] + s_pre[2][1] + s_pre[2][2] + s_pre[2][3];
 	if (threadIdx.x == 0) {
-		if (tile == 0 && P.hstat)
-			for (int k = 0; k < 3; ++k) P.hstat[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
 		P.incl[tile] = (uint64_t)excl + agg;
 		if (tile + 1 == P.ntile) {
 			const uint32_t total = sadd(excl, agg), blocks = sadd(exclB, aggB);
@@ -743,6 +796,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	const uint64_t wpb = blockDim.x >> 6;
 	typedef __attribute__((address_space(1))) const uint64_t g_u64;
 	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
+	if (v7_extent_taken(P)) return;  // the extent kernels checksum this batch (prep left hdr stale)
 	const uint64_t total = rdfirst64(hp[0]), Qs = rdfirst64(hp[1]);
 	const uint64_t r_base = (uint64_t)blockIdx.x * kV7RangesPerBlock;
 	// no slots for this workgroup (e.g. every buffer went to the block route):
@@ -1079,7 +1133,7 @@ uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                    const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat,
-                   uint32_t* err) {
+                   uint32_t* err, const XState* xs) {
 	const uint64_t grid = (uint64_t)num_cus;
 	const uint64_t nwave = grid * kV7RangesPerBlock;  // one slot range per wave
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
@@ -1100,12 +1154,19 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	// kRouteBoth: spans from bigmin up go to the blocks, the rest to windows;
 	// kRouteWindows: no block launch; kRouteBlocks: every windowed span goes to
 	// the blocks and the window kernel is not launched
-	P.bigmin = count >= 0xFFFFFFFFull || route == kRouteWindows ? 0
+	P.bigmin = count >= 0xFFFFFFFFull || route == kRouteWindows || route == kRouteExtent ? 0
 	           : route == kRouteBlocks                          ? kSmallSpan + 1
 	                                                            : bigmin_env;
 	if (route == kRouteBlocks && P.bigmin == 0) route = kRouteWindows;
 	P.hstat = hstat;
 	P.err = err;
+	const bool extent = route == kRouteExtent && xs != nullptr;
+	if (route == kRouteExtent) route = kRouteWindows;  // the fallback: windows
+	if (extent) {
+		P.xhdr = xs->xhdr;
+		P.epoch = xs->epoch;
+		P.xcap = xs->cap_blk;
+	}
 	P.hdr = reinterpret_cast<uint64_t*>(wp);      // [0..3] totals and quantum, [kHdrRefused] refusal flag
 	P.tsum = reinterpret_cast<uint64_t*>(wp + 64);
 	P.incl = P.tsum + ntile + 1;
@@ -1138,7 +1199,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	// kScanTiles tiles one scan block is cheaper)
 	P.scanned = ntile > kScanTiles;
 	P.selfsum = ntile <= kSelfSumTiles;
-	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
+	if (!P.selfsum || extent) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);  // (extent: the packing check)
 	if (P.scanned)
 		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4, P.bigmin ? P.bsum : nullptr,
 		                               P.bigmin ? P.nsum : nullptr);
@@ -1152,7 +1213,13 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 		B.out = out; B.ctr = P.bctr; B.tabs = tabs;
 		launch_bigblocks(B, num_cus, stream);
 	}
+	if (extent)
+		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
+		              0);
 	if (route != kRouteBlocks) k_varlen7<<<(unsigned)grid, FDBCRC_V7_THREADS, 0, stream>>>(P);
+	if (extent)
+		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
+		              1);
 	return 0;
 }
 
@@ -1163,9 +1230,9 @@ uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) { return varlen7
 
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
-                  hipStream_t stream, int route, uint64_t* hstat, uint32_t* err) {
+                  hipStream_t stream, int route, uint64_t* hstat, uint32_t* err, const XState* xs) {
 	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream, route,
-	                      hstat, err);
+	                      hstat, err, xs);
 }
 
 // Fixed stride, any length and alignment: the same engine with metadata

@@ -1,0 +1,98 @@
+"""CPU model of k_xstream's SCHEDULE (crc32c_extent.hip), symbolic: which
+wave captures which point, from which block and lane span, and which blocks
+each wave's group stores cover.  Lane prefixes are represented by their
+(block, lane) coordinates, so the model checks the control flow -- static
+ranges of whole units, the window search, window retirement inside a unit,
+the extent's last block, the ownership of points at range boundaries --
+without any CRC arithmetic (tests/extent_model.py checks that)."""
+
+U = 2  # blocks per unit (kXU); an iteration is two units
+
+
+def x_blk(p):
+    return (p - 1) >> 12 if p else 0
+
+
+def x_cnt(p, k):
+    return (p - 4096 * k) >> 6 if p else 0
+
+
+def schedule(P0, P1, nwave):
+    """P0/P1: absolute starts/ends of a packed batch.  Returns (vs, ve, blk):
+    vs[i] / ve[i] = list of (wave, value) writes, value = None (0) or the
+    (block, lane) whose prefix was captured; blk[k] = list of waves that
+    stored block k's register."""
+    n = len(P0)
+    S = P0[0] & ~15
+    Eend = (P1[-1] + 15) & ~15
+    nblk = (Eend - S + 4095) >> 12
+    per = -(-(-(-nblk // nwave)) // (2 * U)) * (2 * U)
+    vs = [[] for _ in range(n)]
+    ve = [[] for _ in range(n)]
+    blk = [[] for _ in range(nblk)]
+    for w in range(nwave):
+        k0 = min(w * per, nblk)
+        k1 = min(k0 + per, nblk)
+        km = min(k1, nblk - 1)
+        T0 = S + 4096 * k0
+        q = sum(1 for b in P1 if b <= T0)  # first buffer ending past the range's start
+        win = {}
+
+        def make_window(q0):
+            nonlocal win
+            win = {"q": q0, "bs": [], "be": [], "cs": [], "ce": [], "Vs": [0] * 64, "Ve": [0] * 64}
+            for j in range(64):
+                if q0 + j < n:
+                    s, e = P0[q0 + j] - S, P1[q0 + j] - S
+                    win["bs"].append(x_blk(s)); win["be"].append(x_blk(e))
+                    win["cs"].append(x_cnt(s, x_blk(s))); win["ce"].append(x_cnt(e, x_blk(e)))
+                else:
+                    win["bs"].append(-2); win["be"].append(-2); win["cs"].append(0); win["ce"].append(0)
+            win["last"] = win["be"][63] if q0 + 64 <= n else float("inf")
+
+        def flush():
+            q0 = win["q"]
+            for j in range(64):
+                if q0 + j >= n:
+                    continue
+                if k0 <= win["bs"][j] < k1:
+                    vs[q0 + j].append((w, win["Vs"][j]))
+                if k0 <= win["be"][j] < k1:
+                    ve[q0 + j].append((w, win["Ve"][j]))
+
+        def capture(kb, valid):
+            for j in range(64):
+                if valid and win["bs"][j] == kb:
+                    c = win["cs"][j]
+                    win["Vs"][j] = (kb, c - 1) if c else 0
+                if valid and win["be"][j] == kb:
+                    c = win["ce"][j]
+                    win["Ve"][j] = (kb, c - 1) if c else 0
+
+        gs = [k0]
+
+        def finish(k, kend):
+            for j in range(2 * U):
+                capture(k + j, k + j < kend)
+            while win["last"] < k + 2 * U:
+                flush()
+                make_window(win["q"] + 64)
+                for j in range(2 * U):
+                    capture(k + j, k + j < kend)
+            kn = min(k + 2 * U, kend)
+            if kn - gs[0] >= 64 or kn == kend:
+                for b in range(gs[0], kn):
+                    blk[b].append(w)
+                gs[0] = kn
+
+        make_window(q)
+        if k0 >= k1:
+            continue
+        k = k0
+        while k < km:
+            finish(k, km)
+            k += 2 * U
+        if km < k1:
+            finish(km, k1)
+        flush()
+    return vs, ve, blk, S, nblk

@@ -1,0 +1,90 @@
+"""The extent route's arithmetic (tests/extent_model.py) against the oracle on
+small packed batches: packets back to back with gaps, any alignment, zero
+lengths, points on block and lane boundaries, the extent's first and last
+bytes.  CPU only."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import extent_model as X
+
+
+def sm(nbytes, state):
+    return O.splitmix64((nbytes + 7) // 8, state).view(np.uint8)[:nbytes].copy()
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_extent_model_matches_oracle(case):
+    rng = np.random.default_rng(case)
+    mem = sm(1 << 16, 0xE7 + case)
+    lens, offs, pos = [], [], int(rng.integers(0, 40))
+    while True:
+        L = int(rng.choice([0, 1, 15, 16, 17, 63, 64, 65, 200, 1000, 4095, 4096, 4097, 9000]) if case % 2
+                else rng.integers(1, 5000))
+        g = int(rng.integers(0, min(max(L, 256), 300)))
+        if pos + L > mem.size - 64:
+            break
+        offs.append(pos)
+        lens.append(L)
+        pos += L + g
+    if case == 4:  # points exactly on lane / block boundaries, starting at byte 0
+        offs, lens, pos = [], [], 0
+        for L in (64, 4032, 4096, 64, 1, 8191, 4096):
+            offs.append(pos)
+            lens.append(L)
+            pos += L
+    for seed in (0, 0xFDBEEFDB):
+        got = X.extent_crcs(mem, offs, lens, seed)
+        want = O.batch_varlen(mem, np.array(offs, np.uint64), np.array(lens, np.uint64), seed=seed)
+        assert np.array_equal(got, want), case
+
+
+def test_eligibility_rule():
+    assert X.eligible([0, 100], [100, 200])
+    assert not X.eligible([0, 50], [100, 150])          # overlap
+    assert not X.eligible([100, 0], [200, 100])         # descending
+    assert X.eligible([0, 300], [64, 400])              # gap 236 <= 256
+    assert not X.eligible([0, 1000], [64, 1100])        # gap 936 > max(64, 256)
+    assert X.eligible([0, 9000], [5000, 9100])          # gap 4000 <= len 5000
+    assert not X.eligible([0, 20000], [10000, 20100])   # gap 10000 >= 4096
+
+
+def _check_schedule(P0, P1, nwave):
+    from tests import extent_sched_model as M
+    vs, ve, blk, S, nblk = M.schedule(P0, P1, nwave)
+    assert all(len(b) == 1 for b in blk), "every block register stored exactly once"
+    for i, (a, b) in enumerate(zip(P0, P1)):
+        for p, rec in ((a - S, vs[i]), (b - S, ve[i])):
+            k = M.x_blk(p)
+            c = M.x_cnt(p, k)
+            want = (k, c - 1) if c else 0
+            if p == 0:
+                assert len(rec) <= 1 and all(v == 0 for _, v in rec)
+                continue
+            assert len(rec) == 1, (i, p, rec)
+            assert rec[0][1] == want, (i, p, rec, want)
+
+
+@pytest.mark.parametrize("nwave", [1, 3, 7, 64])
+def test_stream_schedule_captures_every_point_once(nwave):
+    """k_xstream's control flow (static unit ranges, window search and
+    retirement, the extent's last block): every point is captured exactly
+    once, by the wave whose range holds its block, from the right block and
+    lane span; every block register is stored exactly once."""
+    rng = np.random.default_rng(nwave)
+    for trial in range(12):
+        P0, P1, pos = [], [], int(rng.integers(0, 4096))
+        n = int(rng.integers(1, 600))
+        kind = trial % 4
+        for _ in range(n):
+            L = int({0: rng.integers(1, 300), 1: rng.integers(0, 20000), 2: rng.choice([0, 1, 63, 64, 65, 4096]),
+                     3: rng.integers(2000, 70000)}[kind])
+            g = int(rng.integers(0, min(max(L, 256), 4095) + 1)) if trial % 3 else 0
+            P0.append(pos)
+            P1.append(pos + L)
+            pos += L + g
+        _check_schedule(P0, P1, nwave)
+    # single buffers, aligned and not; a batch inside one block
+    _check_schedule([0], [1 << 20], nwave)
+    _check_schedule([5], [5 + 4091], nwave)
+    _check_schedule([16, 100], [50, 4000], nwave)
