@@ -249,9 +249,11 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 		}
 #pragma unroll
 		for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], (uint32_t)(k + j), k + j < kend);
-		// every buffer of the window ends in these blocks: the next 64 (rare
-		// for packets of KiBs; the blocks' prefixes are still in registers)
-		while ((uint64_t)wlast < k + 2 * kXU) {
+		const uint64_t kn = k + 2 * kXU < kend ? k + 2 * kXU : kend;
+		// every buffer of the window ends in the blocks done so far: the next 64
+		// (rare for packets of KiBs; these blocks' prefixes are still in
+		// registers).  Not past kend: a point in a later block is still to come.
+		while ((uint64_t)wlast < kn) {
 			flush(q);
 			q += 64;
 			make_window(q);
@@ -259,7 +261,6 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 #pragma unroll
 			for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], (uint32_t)(k + j), k + j < kend);
 		}
-		const uint64_t kn = k + 2 * kXU < kend ? k + 2 * kXU : kend;
 		if (kn - gs >= 64 || kn == kend) {  // a full group, or the range's end
 			store_group(kn - gs);
 			gs = kn;

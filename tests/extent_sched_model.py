@@ -74,12 +74,12 @@ def schedule(P0, P1, nwave):
         def finish(k, kend):
             for j in range(2 * U):
                 capture(k + j, k + j < kend)
-            while win["last"] < k + 2 * U:
+            kn = min(k + 2 * U, kend)
+            while win["last"] < kn:
                 flush()
                 make_window(win["q"] + 64)
                 for j in range(2 * U):
                     capture(k + j, k + j < kend)
-            kn = min(k + 2 * U, kend)
             if kn - gs[0] >= 64 or kn == kend:
                 for b in range(gs[0], kn):
                     blk[b].append(w)

@@ -88,3 +88,20 @@ def test_stream_schedule_captures_every_point_once(nwave):
     _check_schedule([0], [1 << 20], nwave)
     _check_schedule([5], [5 + 4091], nwave)
     _check_schedule([16, 100], [50, 4000], nwave)
+
+
+def test_stream_schedule_window_retired_before_the_last_block():
+    """A window whose last buffer ends in the extent's last block, reached by a
+    partial iteration of the main loop: the window must not retire before the
+    last block's points are captured (the retire bound is the iteration's last
+    block before kend, not the iteration's end)."""
+    for nblk_tail in range(1, 9):
+        # 64-buffer windows of tiny packets filling the extent up to its last block
+        P0, P1, pos = [], [], 0
+        target = 4096 * (4 + nblk_tail) - 40
+        while pos < target:
+            P0.append(pos)
+            P1.append(pos + 48)
+            pos += 64
+        for nwave in (1, 2, 3):
+            _check_schedule(P0, P1, nwave)
