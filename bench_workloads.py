@@ -40,16 +40,19 @@ def pmc_traffic(workload):
 
 class CpuSample:
     def __init__(self, desc, nbytes, buf, stride=None, length=None, count=None, offsets=None, lengths=None, seed=0,
-                 ref=None, port=None, port_only=False):
+                 ref=None, port=None, port_only=False, ref_available=None):
         self.desc, self.nbytes, self.buf = desc, nbytes, buf
         self.port_only = port_only  # no compiled reference for this path: time the oracle restatement
         self.stride, self.length, self.count = stride, length, count
         self.offsets, self.lengths, self.seed = offsets, lengths, seed
         self.ref, self.port = ref, port  # optional callables(O) for non-CRC workloads
+        self.ref_available = ref_available  # optional callable(O): is `ref` built (oracle/_ref)?
 
     def available(self, O):
         if self.port_only:
             return False
+        if self.ref_available:
+            return self.ref_available(O)
         return O.xxh3_reference_available() if self.ref else O.reference_available()
 
     def run_reference(self, O):
@@ -436,12 +439,13 @@ class SqliteVerify:
         return True
 
     def cpu_sample(self):
-        from oracle import oracle as O
-        n = 4096
+        n = 65536
         host = self.buf[:n * 4096].cpu().numpy()
-        return CpuSample(f"first {n} pages of the batch through the oracle's PageChecksumCodec::checksum "
-                         "restatement (reference-pinned CRC-32C / XXH3 / lookup3 primitives, one call per page)",
-                         n * 4096, host, port_only=True,
+        return CpuSample(f"first {n} pages of the batch through PageChecksumCodec::checksum(write=false) "
+                         "(KeyValueStoreSQLite.cpp:118-155) composed from the reference's own crc32c_append, "
+                         "XXH3_64bits and hashlittle2 compiled unmodified (oracle/ref_pagecheck.c), one page per call",
+                         n * 4096, host, ref=lambda O_: O_.ref_sqlite_verify_pages(host, 4096, n, 1),
+                         ref_available=lambda O_: O_.pagecheck_reference_available(),
                          port=lambda O_: [O_.sqlite_verify_page(host[4096 * i:4096 * (i + 1)], i + 1)
                                           for i in range(n)])
 
@@ -468,6 +472,83 @@ class SqliteVerifyHost(SqliteVerify):
     def step(self, stream):
         st, bad = self.pipe.sqlite_verify_pages(self.buf, 4096, self.count, first_pgno=1)
         self.status, self.bad = torch.from_numpy(st), torch.from_numpy(bad.view(np.int64))
+
+
+def _diskqueue_pages_on_device(dev, count):
+    """1 Mi DiskQueue pages of 4 KiB in HBM (fdbserver/kvstore/DiskQueue.cpp:1047-1120):
+    implementationVersion V2 (XXH3-64 of bytes [8, 4096), the current TLog
+    format) on 12 of every 16 pages, V1 (CRC-32C of [4, 4096), TLogVersion V3..V6)
+    on 3, and a V2 page with a wrong hash on 1; a few V0 (hashlittle2) pages
+    built on the host.  The hashes are written with the engine's own batch
+    kernels; verify() re-checks a sample with the reference composition."""
+    import foundationdb_amd.xxh3 as X
+    from oracle import oracle as O
+    buf = torch.empty(count * 4096, dtype=torch.uint8, device=dev)
+    F.fill_splitmix64(buf, STATE ^ 0xD15C)
+    pages = buf.view(count, 4096)
+    kind = torch.arange(count, device=dev) % 16
+    ver = torch.where((kind >= 12) & (kind < 15), 1, 2).to(torch.int16)
+    hdr = torch.stack([torch.full_like(ver, 0x4D51), ver], 1)  # magic, implementationVersion
+    pages[:, 8:12] = hdr.view(torch.uint8).view(count, 4)
+    h64 = X.batch_fixed(buf, 4096, 4088, count, byte_offset=8)
+    c32 = F.batch_fixed(buf, 4096, 4092, count, seed=0xFDBEEFDB, byte_offset=4)
+    h64 = h64.view(torch.int64)
+    h64 = torch.where(kind == 15, h64 ^ 0x5A5A, h64)
+    pages[:, 0:8] = torch.where((ver == 2)[:, None], h64.view(torch.uint8).view(count, 8), pages[:, 0:8])
+    pages[:, 0:4] = torch.where((ver == 1)[:, None], c32.view(torch.uint8).view(count, 4), pages[:, 0:4])
+    v0 = np.arange(7, count, 4099)  # V0 pages: hashlittle2 of [16, 4096), built on the host
+    for i in v0:
+        pg = pages[int(i)].cpu().numpy()
+        pg[8:12] = np.frombuffer((0x0FDB).to_bytes(2, "little") + (0).to_bytes(2, "little"), np.uint8)
+        pg[:16] = np.frombuffer(O.diskqueue_hash(pg, 0), np.uint8)
+        pages[int(i)] = torch.from_numpy(pg).to(dev)
+    expect = torch.where(kind == 15, 0, 1).to(torch.uint8)
+    expect[torch.from_numpy(v0).to(dev)] = 1
+    return buf, expect
+
+
+class DiskQueueVerify:
+    """DiskQueue page verification (Page::checkHash over a contiguous run of
+    pages, DiskQueue.cpp:1230-1290 / recovery :1342-1360): 1 Mi mixed 4 KiB
+    pages, device-resident (fdb_diskqueue_check_pages)."""
+    metric = "device-resident DiskQueue page verification GiB/s (1 Mi mixed 4 KiB pages); % of HBM-read peak"
+    kernel_name = "fdb_diskqueue_check_pages (classify + k_xxh3_rows list + k_pages4k list + lookup3 + compare)"
+
+    def __init__(self, dev, rank, count=1 << 20):
+        import foundationdb_amd.pagecheck as PC
+        self.PC, self.count = PC, count
+        self.buf, self.expect = _diskqueue_pages_on_device(dev, count)
+        self.bytes_per_step = count * 4096
+        self.algorithmic_bytes_per_step = count * (4096 + 1)
+        self.data_desc = (f"synthetic: splitmix64 pages in HBM, DiskQueue V2 / V1 / corrupt 12:3:1 plus V0 pages")
+        self.config = {"workload": f"{count} x 4 KiB DiskQueue pages, mixed implementationVersion, device-resident",
+                       "pages": count}
+        self.ok = torch.empty(count, dtype=torch.uint8, device=dev)
+        self.bad = torch.empty(1, dtype=torch.uint64, device=dev)
+
+    def step(self, stream):
+        self.PC.diskqueue_check_pages(self.buf, self.count, stream=stream, ok=self.ok, bad=self.bad)
+
+    def verify(self):
+        from oracle import oracle as O
+        if not torch.equal(self.ok, self.expect):
+            return False
+        if int(self.bad.cpu().numpy().view(np.uint64)[0]) != int((self.expect == 0).sum()):
+            return False
+        idx = np.random.default_rng(0).choice(self.count, 256, replace=False)
+        host = self.buf.view(self.count, 4096)[torch.from_numpy(idx).to(self.buf.device)].cpu().numpy()
+        ok = self.ok.cpu().numpy()
+        return all(O.diskqueue_check_page(host[j]) == int(ok[i]) for j, i in enumerate(idx))
+
+    def cpu_sample(self):
+        n = 65536
+        host = self.buf[:n * 4096].cpu().numpy()
+        return CpuSample(f"first {n} pages through Page::checkHash (DiskQueue.cpp:1077-1120) composed from the "
+                         "reference's own crc32c_append / XXH3_64bits / hashlittle2 (oracle/ref_pagecheck.c)",
+                         n * 4096, host, ref=lambda O_: O_.ref_diskqueue_check_pages(host, n),
+                         ref_available=lambda O_: O_.pagecheck_reference_available(),
+                         port=lambda O_: [O_.diskqueue_check_page(host[4096 * i:4096 * (i + 1)])
+                                          for i in range(n)])
 
 
 class Xxh3Zipf(VarLen):
@@ -525,4 +606,5 @@ WORKLOADS = {
     "xxh3-zipf": lambda dev, rank: Xxh3Zipf(dev, rank),
     "sqlite-verify": lambda dev, rank: SqliteVerify(dev, rank),
     "sqlite-verify-host": lambda dev, rank: SqliteVerifyHost(dev, rank),
+    "diskqueue-verify": lambda dev, rank: DiskQueueVerify(dev, rank),
 }

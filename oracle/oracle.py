@@ -182,6 +182,7 @@ def splitmix64(nwords, state):
 # the reference's flow/xxhash.c + flow/Hash3.c compiled unmodified.
 XXH3_SO = os.path.join(_HERE, "liboracle_xxh3.so")
 XXH3_REF_SO = os.path.join(_HERE, "_ref", "libxxhash_ref.so")
+PAGECHECK_REF_SO = os.path.join(_HERE, "_ref", "libpagecheck_ref.so")
 _x = None
 _xref = None
 
@@ -317,6 +318,50 @@ def ref_xxh3_batch_fixed(buf, stride, length, count, seed=0):
     out = np.zeros(count, dtype=np.uint64)
     f(buf.ctypes.data, stride, length, count, seed & 0xFFFFFFFFFFFFFFFF, out.ctypes.data)
     return out
+
+
+# ------------------------------------------------- page checks, reference-composed
+_pcref = None
+
+
+def pagecheck_reference_available():
+    return os.path.exists(PAGECHECK_REF_SO)
+
+
+def pagecheck_reference():
+    """oracle/ref_pagecheck.c over the reference's own crc32c_append, XXH3_64bits
+    and hashlittle2 (oracle/_ref/libpagecheck_ref.so): the SQLite and DiskQueue
+    page checks as FoundationDB runs them, one page at a time."""
+    global _pcref
+    if _pcref is None:
+        if not os.path.exists(PAGECHECK_REF_SO):
+            raise FileNotFoundError(PAGECHECK_REF_SO + " (run `make -C oracle` where /root/reference exists)")
+        L = ctypes.CDLL(PAGECHECK_REF_SO)
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.ref_sqlite_verify_pages.restype = u64
+        L.ref_sqlite_verify_pages.argtypes = [vp, u64, u64, ctypes.c_uint32, vp]
+        L.ref_diskqueue_check_pages.restype = u64
+        L.ref_diskqueue_check_pages.argtypes = [vp, u64, vp]
+        _pcref = L
+    return _pcref
+
+
+def ref_sqlite_verify_pages(pages, page_size, count, first_pgno=1):
+    """(status per page, bad count) from the reference primitives (single thread)."""
+    pages = np.ascontiguousarray(pages).view(np.uint8)
+    assert count * page_size <= pages.nbytes
+    st = np.zeros(count, np.uint8)
+    bad = pagecheck_reference().ref_sqlite_verify_pages(pages.ctypes.data, page_size, count, first_pgno,
+                                                        st.ctypes.data)
+    return st, int(bad)
+
+
+def ref_diskqueue_check_pages(pages, count):
+    pages = np.ascontiguousarray(pages).view(np.uint8)
+    assert count * 4096 <= pages.nbytes
+    ok = np.zeros(count, np.uint8)
+    bad = pagecheck_reference().ref_diskqueue_check_pages(pages.ctypes.data, count, ok.ctypes.data)
+    return ok, int(bad)
 
 
 # ---------------------------------------------------------------- page formats

@@ -1,0 +1,86 @@
+/*
+ * ref_pagecheck.c -- TEST/BENCH INFRASTRUCTURE ONLY (bench.py cpu_baseline leg
+ * of the verifier workloads).  The reference's page checks as FoundationDB runs
+ * them, one page at a time, composed from the reference's own primitives
+ * compiled unmodified into oracle/_ref/libpagecheck_ref.so:
+ *   crc32c_append  contrib/crc32/crc32c.cpp:346-356
+ *   XXH3_64bits    flow/xxhash.c (xxHash v0.8.0)
+ *   hashlittle2    flow/Hash3.c:566
+ *
+ * ref_sqlite_verify_pages restates PageChecksumCodec::checksum(write = false)
+ * (fdbserver/kvstore/KeyValueStoreSQLite.cpp:118-155): CRC-32C when part1 == 0,
+ * then XXH3 when part1 >> 24 == 0, then hashlittle2 seeded (pgno, 0x5ca1ab1e);
+ * status 1 / 2 / 3 for the check that accepted the page, 0 for a bad page.
+ * ref_diskqueue_check_pages restates DiskQueue Page::checkHash
+ * (fdbserver/kvstore/DiskQueue.cpp:1077-1120) by implementationVersion.
+ * Both return the number of bad pages (SQLiteDB::checkAllPageChecksums,
+ * KeyValueStoreSQLite.cpp:1378-1470, counts them).
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length);
+uint64_t XXH3_64bits(const void* data, size_t len);
+void hashlittle2(const void* key, size_t length, uint32_t* pc, uint32_t* pb);
+
+static uint32_t rd32(const uint8_t* p) {
+	uint32_t v;
+	memcpy(&v, p, 4);
+	return v;
+}
+static uint64_t rd64(const uint8_t* p) {
+	uint64_t v;
+	memcpy(&v, p, 8);
+	return v;
+}
+
+static int sqlite_check(const uint8_t* page, uint64_t page_size, uint32_t pgno) {
+	const size_t n = (size_t)page_size - 8;
+	const uint32_t part1 = rd32(page + n), part2 = rd32(page + n + 4);
+	if (part1 == 0 && part2 == crc32c_append(0xfdbeefdbu, page, n)) return 1;
+	if ((part1 >> 24) == 0) {
+		const uint64_t h = XXH3_64bits(page, n);
+		if (part1 == (uint32_t)((h >> 32) & 0x00ffffffu) && part2 == (uint32_t)h) return 2;
+	}
+	uint32_t c = pgno, b = 0x5ca1ab1eu;
+	hashlittle2(page, n, &c, &b);
+	return (c == part1 && b == part2) ? 3 : 0;
+}
+
+uint64_t ref_sqlite_verify_pages(const uint8_t* pages, uint64_t page_size, uint64_t count, uint32_t first_pgno,
+                                 uint8_t* status) {
+	uint64_t bad = 0;
+	for (uint64_t i = 0; i < count; ++i) {
+		const int s = sqlite_check(pages + i * page_size, page_size, first_pgno + (uint32_t)i);
+		status[i] = (uint8_t)s;
+		bad += s == 0;
+	}
+	return bad;
+}
+
+/* PageHeader (DiskQueue.cpp:1047-1063, packed, 36 bytes): hash64 / hash32 at 0,
+ * magic at 8, implementationVersion at 10, seq from 16. */
+static int diskqueue_check(const uint8_t* page) {
+	uint16_t ver;
+	memcpy(&ver, page + 10, 2);
+	switch (ver) {
+	case 0: {
+		uint32_t part[2] = {0x12345678u, 0xbeefabcdu};
+		hashlittle2(page + 16, 4096 - 16, &part[0], &part[1]);
+		return rd64(page) == (((uint64_t)part[0] << 32) | part[1]) && rd64(page + 8) == 0xFDBull;
+	}
+	case 1: return rd32(page) == crc32c_append(0xfdbeefdbu, page + 4, 4096 - 4);
+	case 2: return rd64(page) == XXH3_64bits(page + 8, 4096 - 8);
+	default: return 0;
+	}
+}
+
+uint64_t ref_diskqueue_check_pages(const uint8_t* pages, uint64_t count, uint8_t* ok) {
+	uint64_t bad = 0;
+	for (uint64_t i = 0; i < count; ++i) {
+		ok[i] = (uint8_t)diskqueue_check(pages + 4096 * i);
+		bad += !ok[i];
+	}
+	return bad;
+}

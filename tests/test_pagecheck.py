@@ -71,6 +71,22 @@ def make_dq_batch(n, seed):
     return pages, exp
 
 
+@pytest.mark.skipif(not O.pagecheck_reference_available(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("page_size", [4096, 8192, 512])
+def test_oracle_page_checks_match_reference_composition(page_size):
+    """The oracle's page-format restatements agree, page by page, with
+    oracle/ref_pagecheck.c: the same checks composed from the reference's own
+    crc32c_append, XXH3_64bits and hashlittle2 compiled unmodified
+    (KeyValueStoreSQLite.cpp:118-155, DiskQueue.cpp:1077-1120) -- the C
+    baseline the verifier bench lines time."""
+    pages, exp = make_sqlite_batch(600, page_size, 9, page_size + 1)
+    st, bad = O.ref_sqlite_verify_pages(pages, page_size, 600, first_pgno=9)
+    assert np.array_equal(st, exp) and bad == int((exp == 0).sum())
+    dq, dexp = make_dq_batch(400, page_size)
+    ok, dbad = O.ref_diskqueue_check_pages(dq, 400)
+    assert np.array_equal(ok, dexp) and dbad == int((dexp == 0).sum())
+
+
 def test_oracle_diskqueue_roundtrip():
     pages, exp = make_dq_batch(200, 3)
     assert 0 < exp.sum() < exp.size
