@@ -589,6 +589,35 @@ class Xxh3Zipf(VarLen):
                          port=lambda O_: O_.xxh3_batch_varlen(host, offs, lens, threads=1))
 
 
+class Xxh3Chunks(Xxh3Zipf):
+    """XXH3-64 of every chunk of the configs[4] backup-chunk batch (4 KiB - 1 MiB,
+    log-uniform), device-resident: the split route for every chunk over 16 KiB
+    (xxh3_split.hip), the row kernel for the rest."""
+    metric = "device-resident XXH3-64 GiB/s on 4 KiB-1 MiB chunk batches; % of HBM-read peak"
+    kernel_name = "fdbxxh planner + k_xsplit_a (stripe sums) + k_xsplit_b (chains) + k_xxh3_vrows"
+
+    def __init__(self, dev, rank):
+        import foundationdb_amd.xxh3 as X
+        VarLen.__init__(self, dev, rank, chunk_lengths(), 4096,
+                        "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch, XXH3-64 per chunk")
+        self.X = X
+        self.metric = Xxh3Chunks.metric
+        self.out = torch.empty(self.h_lengths.size, dtype=torch.uint64, device=dev)
+        self.algorithmic_bytes_per_step = self.bytes_per_step + 24 * self.h_lengths.size
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        csum = np.cumsum(self.h_lengths)
+        k = min(int(np.searchsorted(csum, 256 << 20)) + 1, self.h_lengths.size)
+        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        host = self.buf[:end].cpu().numpy()
+        offs, lens = self.h_offsets[:k], self.h_lengths[:k]
+        return CpuSample(f"first {k} chunks ({int(lens.sum()) >> 20} MiB), reference flow/xxhash.c XXH3_64bits",
+                         int(lens.sum()), host,
+                         ref=lambda O_: O_.ref_xxh3_batch_varlen(host, offs, lens),
+                         port=lambda O_: O_.xxh3_batch_varlen(host, offs, lens, threads=1))
+
+
 WORKLOADS = {
     "pages4k": lambda dev, rank: Pages(dev, rank, 4096, 1 << 20, 0),
     "pages8k": lambda dev, rank: Pages(dev, rank, 8192, 1 << 19, 0xFDBEEFDB),
@@ -604,6 +633,7 @@ WORKLOADS = {
     "pages4k-host": lambda dev, rank: HostPages(dev, rank),
     "xxh3-pages4k": lambda dev, rank: Xxh3Pages(dev, rank),
     "xxh3-zipf": lambda dev, rank: Xxh3Zipf(dev, rank),
+    "xxh3-chunks": lambda dev, rank: Xxh3Chunks(dev, rank),
     "sqlite-verify": lambda dev, rank: SqliteVerify(dev, rank),
     "sqlite-verify-host": lambda dev, rank: SqliteVerifyHost(dev, rank),
     "diskqueue-verify": lambda dev, rank: DiskQueueVerify(dev, rank),

@@ -22,6 +22,7 @@ namespace {
 
 constexpr int kMaxDevices = 64;
 constexpr int kHstatErr = 6;  // u64 word of the stream's host-mapped block holding its refusal flag
+constexpr int kHstatXxhNeed = 7;  // ... the long-buffer blocks of its last XXH3 varlen batch (split route room)
 
 // Library-owned state of one (device, stream).  `mu` is held from the
 // workspace lookup through the enqueue of the kernels that use it, so a
@@ -535,6 +536,22 @@ int xxh3_gpu_batch_fixed(const void* d_base, uint64_t stride, uint64_t length, u
 	P.seed = seed;
 	P.seeds = d_seeds;
 	P.out = d_out;
+	if (length > fdbxxh::kXSplitMin) {
+		// long buffers: the split route (every 1 KiB block of the batch in
+		// parallel), planned in the stream's workspace
+		const uint64_t nw = fdbxxh::xxh3_nwave(st->num_cus);
+		const uint64_t nb = count * (((length - 1) >> 10) + 1);
+		void* ws = nullptr;
+		uint64_t have = 0;
+		std::unique_lock<std::mutex> hold;
+		if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
+		                              fdbxxh::xxh3_workspace_bytes_for(count, nw, nb), &ws, &have, &hold))
+			return rc;
+		P.ws_bytes = have;
+		if (fdbxxh::launch_xxh3(P, st->num_cus, ws, reinterpret_cast<hipStream_t>(stream)))
+			return fail(FDB_CRC32C_EHIP, "xxh3_gpu_batch_fixed: launch setup failed");
+		return check_launch("xxh3_gpu_batch_fixed launch");
+	}
 	if (fdbxxh::launch_xxh3(P, st->num_cus, nullptr, reinterpret_cast<hipStream_t>(stream)))
 		return fail(FDB_CRC32C_EHIP, "xxh3_gpu_batch_fixed: launch setup failed");
 	return check_launch("xxh3_gpu_batch_fixed launch");
@@ -546,9 +563,16 @@ uint64_t xxh3_gpu_varlen_workspace_bytes(uint64_t count) {
 	return fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus));
 }
 
-int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
-                             uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
-                             uint64_t workspace_bytes, void* stream) {
+uint64_t xxh3_gpu_varlen_workspace_bytes_for(uint64_t count, uint64_t total_bytes) {
+	DeviceState* st = nullptr;
+	if (device_state(&st)) return 0;
+	return fdbxxh::xxh3_workspace_bytes_for(count, fdbxxh::xxh3_nwave(st->num_cus),
+	                                        fdbxxh::xxh3_long_blocks_bound(total_bytes));
+}
+
+static int xxh3_varlen_impl(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                            uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
+                            uint64_t workspace_bytes, void* stream, uint64_t* hneed) {
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths || !d_base)
 		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: null pointer");
@@ -565,11 +589,24 @@ int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, cons
 	P.seed = seed;
 	P.seeds = d_seeds;
 	P.out = d_out;
+	P.ws_bytes = workspace_bytes;
+	P.hneed = hneed;
 	if (fdbxxh::launch_xxh3(P, st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream)))
 		return fail(FDB_CRC32C_EHIP, "xxh3_gpu_batch_varlen: launch setup failed");
 	return check_launch("xxh3_gpu_batch_varlen launch");
 }
 
+int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
+                             uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
+                             uint64_t workspace_bytes, void* stream) {
+	return xxh3_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, d_workspace, workspace_bytes,
+	                        stream, nullptr);
+}
+
+// The library's workspace for the stream: the planner's arrays plus room for
+// the split route sized from the long blocks the stream's last batch needed
+// (recorded by the device in host-mapped memory; a batch needing more than
+// the room runs its long buffers on the row kernel, and the next call grows).
 int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                           uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
 	if (count == 0) return 0;
@@ -577,14 +614,23 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
 		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: null pointer");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
+	const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+	StreamState* ss = stream_state(st, s);
+	bool mapped;
+	{
+		std::lock_guard<std::mutex> lock(g_mu);
+		mapped = stream_mapped(ss);
+	}
+	const uint64_t last = mapped ? *reinterpret_cast<volatile uint64_t*>(ss->hst_h + kHstatXxhNeed) : 0;
+	const uint64_t room = last + last / 4;
 	void* ws = nullptr;
 	uint64_t have = 0;
 	std::unique_lock<std::mutex> hold;
-	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
-	                              fdbxxh::xxh3_workspace_bytes(count, fdbxxh::xxh3_nwave(st->num_cus)), &ws, &have,
-	                              &hold))
+	if (int rc = stream_workspace(st, s, fdbxxh::xxh3_workspace_bytes_for(count, fdbxxh::xxh3_nwave(st->num_cus), room),
+	                              &ws, &have, &hold))
 		return rc;
-	return xxh3_gpu_batch_varlen_ws(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream);
+	return xxh3_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream,
+	                        mapped ? ss->hst_d + kHstatXxhNeed : nullptr);
 }
 
 uint64_t xxh3_gpu_chained_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes) {

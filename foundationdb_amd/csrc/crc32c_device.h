@@ -83,15 +83,15 @@ inline int route_for_stats(const volatile uint64_t* s) {
 // xhdr[0] the epoch of the last launch whose batch was found not packed,
 // xhdr[1] the epoch of the last launch whose extent exceeded the capacity;
 // per buffer the start / end point registers; per 4 KiB block of the extent
-// its raw register and its exclusive prefix; per 4096 blocks an aggregate.
+// the range-local prefix Z; per wave of the streaming kernel its range's
+// aggregate register.
 struct XState {
 	uint32_t* xhdr;
 	uint32_t* vs;
 	uint32_t* ve;
 	uint32_t* dummy;      // 128 words per wave of the stream kernel
-	uint32_t* blk;
-	uint32_t* ysc;
-	uint32_t* tagg;
+	uint32_t* zb;         // per block: X_k * x^(8*4096), X_k the range-local prefix at the block's start
+	uint32_t* ragg;       // per stream wave: the range-local prefix at its range's end
 	uint64_t cap_blk;     // blocks the arrays hold
 	uint32_t epoch;       // this launch (never 0)
 };

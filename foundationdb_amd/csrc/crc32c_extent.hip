@@ -9,17 +9,23 @@
 // like 4 KiB pages (k_pages4k's loads, permlane swizzle, register chains), so
 // no byte is padded and nothing is masked.  Every buffer's CRC comes from two
 // PREFIX registers of that stream (CRC linearity; tests/extent_model.py is
-// the byte-exact CPU model):
-//     raw(bytes [s, e)) = R(e) ^ R(s) * x^(8(e - s)),   R(p) = raw(bytes [S, S+p))
-// so the gap bytes between buffers cancel.  For a point p (relative to S)
-// in block k = (p-1) >> 12 with cnt = (p - 4096k) >> 6 whole lane spans
-// before it:
-//     R(p64) = (Y[k] ^ V(p)) * x^(-8*64*(64-cnt)),       p64 = 4096k + 64cnt
-//     R(p)   = R(p64) fed the p - p64 < 64 bytes after p64
-// V(p) = H_k[cnt-1] is the block's lane registers weighted to the block end
-// (the page kernel's fold) XOR-prefixed up to lane cnt-1 -- the stream kernel
-// captures it for every point of its blocks -- and Y[k] is the exclusive
-// prefix of the block registers positioned at block k's end (a scan).  Then
+// the byte-exact CPU model, extent_crcs_ranges the form implemented here):
+//     raw(bytes [s, e)) = R(e) ^ R(s) * x^(8(e - s))
+// so the gap bytes between buffers cancel.  Wave w streams the blocks
+// [k0, k1) = [w*per, (w+1)*per) of its RANGE and keeps R relative to the
+// range's start: X_k (0 at k0), Z[k] = X_k * M (M = x^(8*4096)), stored per
+// block, X_{k+1} = Z[k] ^ B[k] (B: the block register), the range's end value
+// A[w] = X_{k1}.  A point p in block k = (p-1) >> 12 with cnt = (p - 4096k) >> 6
+// whole lane spans before it has, positioned at block k's end,
+//     G(p) = Z[k] ^ H_k[cnt-1]
+// (H_k: the block's lane registers weighted to the block end -- the page
+// kernel's fold -- XOR-prefixed over the lanes; the stream kernel captures
+// H_k[cnt-1] for every point of its blocks), and
+//     R(p64) = G(p) * x^(-8*64*(64-cnt)),   R(p) = R(p64) fed the p - p64 < 64 bytes after p64.
+// A buffer whose two points lie in one range needs nothing else (the range's
+// global start register cancels); one spanning ranges ws < we adds
+// D = (A[ws] M^per ^ A[ws+1]) M^per ... ^ A[we-1] to its end point's prefix,
+// positioned there: G(e) ^= D * M^(ke - k0(we) + 1).  Then
 //     crc32c_append(seed, buffer) = ~(R(e) ^ (R(s) ^ ~seed) * x^(8 len)).
 //
 //   k_v7count (crc32c_varlen.hip)  the packing check (epoch-tagged flags) and
@@ -27,9 +33,10 @@
 //   k_xstream   static block ranges per wave; per block: chains, lane weights,
 //               prefix XOR (DPP), the block register; the points of the block
 //               from a window of 64 buffers in the lanes (ds_bpermute)
-//   k_xs1/k_xs2 the block-register scan (tiles of 4096 blocks)
+//   k_xz        per range: the block registers turned into the range-local
+//               prefixes Z (a lane-parallel weighted scan, LDS tables)
 //   k_xfin      per buffer: R(s), R(e) (the < 64-byte remainders re-read),
-//               x^(8 len), the final inversion
+//               the range aggregates between them, x^(8 len), the inversion
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -64,6 +71,7 @@ struct XParams {
 	XState x;
 	const DevTables* tabs;
 	uint64_t* hstat;
+	uint64_t nwave;  // waves of k_xstream (its static ranges)
 };
 
 __device__ __forceinline__ void x_buffer(const XParams& P, uint64_t i, uint64_t& P0, uint64_t& P1) {
@@ -95,6 +103,11 @@ __device__ __forceinline__ XGeo x_geo(const XParams& P) {
 	g.Eend = rdfirst64((b1 + 15) & ~uint64_t(15));
 	g.nblk = (g.Eend - g.S + 4095) >> 12;
 	return g;
+}
+
+// Blocks per wave of k_xstream's static ranges: whole units of 2U blocks.
+__device__ __forceinline__ uint64_t x_per(uint64_t nblk, uint64_t nwave) {
+	return (((nblk + nwave - 1) / nwave) + 3) / 4 * 4;
 }
 
 // Point p (bytes from S): its block and the whole lane spans before it in
@@ -130,7 +143,8 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 	const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
 	const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wi;
 	// static ranges of whole units (the extent's blocks are consecutive)
-	const uint64_t per = (((G.nblk + nwave - 1) / nwave) + 2 * kXU - 1) / (2 * kXU) * (2 * kXU);
+	static_assert(2 * kXU == 4, "x_per: ranges of whole units");
+	const uint64_t per = x_per(G.nblk, nwave);
 	const uint64_t k0 = w * per < G.nblk ? w * per : G.nblk;
 	const uint64_t k1 = k0 + per < G.nblk ? k0 + per : G.nblk;
 	// The extent's last block may run past its end: it is left out of the main
@@ -213,8 +227,8 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 	// ---- blocks -------------------------------------------------------------
 	uint32_t mine = 0;       // lane k - gs: register of block k of the current group
 	uint64_t gs = k0;        // first block of the group
-	auto store_group = [&](uint64_t n) {
-		*((uint64_t)lane < n ? P.x.blk + gs + lane : dmy + lane) = mine;
+	auto store_group = [&](uint64_t n) {  // the block registers B (k_xz turns them into Z in place)
+		*((uint64_t)lane < n ? P.x.zb + gs + lane : dmy + lane) = mine;
 	};
 	// chains, lane weights and the prefix XOR over the lanes of one unit
 	auto unit_h = [&](Block (&u)[kXU], uint32_t (&H)[kXU]) {
@@ -300,11 +314,58 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 }
 
 // ---------------------------------------------------------------------------
-// Block-register scan: Y[k] = X_k * M, X_0 = 0, X_{k+1} = X_k * M ^ B[k]
-// (M = x^(8*4096)), in tiles of 4096 blocks (1024 threads x 4).
+// k_xz: the range-local prefixes, one wave per stream wave's range (the same
+// numbering), lane-parallel per group of 64 blocks from LDS copies of the
+// M^j tables (j <= 32; every lane of a step reads the same table: broadcast,
+// no bank conflicts).  The carry X_gs enters lane 0 as carry * M; a 6-step
+// weighted scan I_j = XOR_{m<=j} v_m * M^(j-m) gives X_{gs+j+1}, so
+//     Z[gs+j] = X_{gs+j+1} ^ B[gs+j]      (in place of B),   A[w] = X_{k1}.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kXTile = 4096;
+constexpr uint32_t kZTabs = 33;  // bpow[0][0..32]: M^j
 
+__device__ __forceinline__ uint32_t lmulz(const uint32_t* lds, uint32_t j, uint32_t v) {
+	uint32_t r = 0;
+#pragma unroll
+	for (int n = 0; n < 8; ++n) r ^= lds[128 * j + 16 * n + ((v >> (4 * n)) & 15u)];
+	return r;
+}
+
+__global__ __launch_bounds__(1024) void k_xz(XParams P) {
+	__shared__ uint32_t lds[kZTabs * 128];
+	if (!x_packed(P)) return;
+	const XGeo G = x_geo(P);
+	if (G.nblk == 0) return;
+	{
+		typedef __attribute__((address_space(1))) const u32x4 gq;
+		const gq* src = (const gq*)reinterpret_cast<uintptr_t>(&P.tabs->bpow[0][0][0][0]);
+		u32x4* dst = reinterpret_cast<u32x4*>(lds);
+		for (uint32_t q = threadIdx.x; q < kZTabs * 32; q += blockDim.x) dst[q] = src[q];
+	}
+	__syncthreads();
+	const uint32_t lane = threadIdx.x & 63;
+	const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rdfirst(threadIdx.x >> 6);
+	const uint64_t per = x_per(G.nblk, P.nwave);
+	const uint64_t k0 = w * per < G.nblk ? w * per : G.nblk;
+	const uint64_t k1 = k0 + per < G.nblk ? k0 + per : G.nblk;
+	uint32_t carry = 0;
+	for (uint64_t gs = k0; gs < k1; gs += 64) {
+		const uint64_t n = k1 - gs < 64 ? k1 - gs : 64;
+		const bool in = lane < n;
+		const uint32_t B = xld32(P.x.zb + (in ? gs + lane : gs));
+		uint32_t I = lane == 0 ? B ^ lmulz(lds, 1, carry) : B;
+#pragma unroll
+		for (uint32_t d = 1; d < 64; d <<= 1) {
+			const uint32_t y = (uint32_t)__shfl_up((int)I, d);
+			const uint32_t ym = lmulz(lds, d, y);
+			I ^= lane >= d ? ym : 0u;
+		}
+		if (in) P.x.zb[gs + lane] = I ^ B;
+		carry = rdlane(I, (int)n - 1);
+	}
+	if (lane == 0) P.x.ragg[w] = carry;  // A[w]: the range-local prefix at the range's end
+}
+
+// ---------------------------------------------------------------------------
 // v * M^m for 0 <= m < 2^32 blocks (bpow: x^(8*4096*j*256^i)); the levels no
 // lane needs are skipped.
 __device__ __forceinline__ uint32_t xmul_blocks(const DevTables* T, uint32_t v, uint32_t m) {
@@ -315,141 +376,113 @@ __device__ __forceinline__ uint32_t xmul_blocks(const DevTables* T, uint32_t v, 
 	return v;
 }
 
-// XOR over the workgroup (1024 threads), returned to every thread.
-__device__ __forceinline__ uint32_t x_block_xor(uint32_t v, uint32_t* s_w) {
-	v = wave_xor(v);
-	if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
-	__syncthreads();
+// ---------------------------------------------------------------------------
+// k_xfin: one buffer per thread, persistent (one 1024-thread workgroup per
+// CU).  The constant multiplies run from LDS copies of the nibble tables the
+// finishing math uses (x^(-8*64j), x^(8d), x^(8*64c), M^j for j < 64, and the
+// slicing tables): two dependent global round trips per buffer (metadata,
+// then the point registers and remainder bytes) instead of one per multiply.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kFinThreads = 1024;
+constexpr uint32_t kFinXinv = 0;                        // xinv64[65]
+constexpr uint32_t kFinPow1 = kFinXinv + 65 * 128;      // pow1[64]
+constexpr uint32_t kFinPow64 = kFinPow1 + 64 * 128;     // pow64[64]
+constexpr uint32_t kFinBp0 = kFinPow64 + 64 * 128;      // bpow[0][0..63]
+constexpr uint32_t kFinS4 = kFinBp0 + 64 * 128;         // slice4[4][256]
+constexpr uint32_t kFinWords = kFinS4 + 4 * 256;        // 33920 words = 132.5 KiB
+
+__device__ __forceinline__ uint32_t lmul(const uint32_t* lds, uint32_t tab, uint32_t v) {
 	uint32_t r = 0;
-	for (uint32_t k = 0; k < (blockDim.x >> 6); ++k) r ^= s_w[k];
-	__syncthreads();
+#pragma unroll
+	for (int n = 0; n < 8; ++n) r ^= lds[tab + 16 * n + ((v >> (4 * n)) & 15u)];
 	return r;
 }
 
-__global__ __launch_bounds__(1024) void k_xs1(XParams P) {
-	__shared__ uint32_t s_w[16];
-	if (!x_packed(P)) return;
-	const XGeo G = x_geo(P);
-	const DevTables* T = P.tabs;
-	for (uint64_t t = blockIdx.x; t * kXTile < G.nblk; t += gridDim.x) {
-		const uint64_t b0 = t * kXTile + 4 * threadIdx.x;
-		uint32_t B[4];
-#pragma unroll
-		for (int j = 0; j < 4; ++j) B[j] = b0 + j < G.nblk ? xld32(P.x.blk + b0 + j) : 0u;
-		uint32_t a = B[0];
-#pragma unroll
-		for (int j = 1; j < 4; ++j) a = xmul(T->block, a) ^ B[j];
-		a = xmul_blocks(T, a, 4 * (1023 - threadIdx.x));  // to the tile's end
-		a = x_block_xor(a, s_w);
-		if (threadIdx.x == 0) P.x.tagg[t] = a;
-	}
-}
-
-__device__ void x_scan_tile(const XParams& P, const XGeo& G, const DevTables* T, uint32_t t, uint32_t* s_w) {
-	const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-	// the register at the tile's start: the earlier tiles' aggregates, each
-	// shifted over the tiles after it
-	uint32_t xt = 0;
-	for (uint32_t u = tid; u < t; u += blockDim.x) xt ^= xmul_blocks(T, xld32(P.x.tagg + u), kXTile * (t - 1 - u));
-	xt = x_block_xor(xt, s_w);
-	// this thread's four blocks: inclusive chain c_j, positioned at block 4t'+j's end
-	const uint64_t b0 = (uint64_t)t * kXTile + 4 * tid;
-	uint32_t B[4], cj[4];
-#pragma unroll
-	for (int j = 0; j < 4; ++j) B[j] = b0 + j < G.nblk ? xld32(P.x.blk + b0 + j) : 0u;
-	cj[0] = B[0];
-#pragma unroll
-	for (int j = 1; j < 4; ++j) cj[j] = xmul(T->block, cj[j - 1]) ^ B[j];
-	// prefix over the threads of the wave (each step shifts by 4 blocks per thread)
-	uint32_t in = cj[3];
-#pragma unroll
-	for (uint32_t d = 1; d < 64; d <<= 1) {
-		const uint32_t y = (uint32_t)__shfl_up((int)in, d);
-		const uint32_t ys = xmul(T->bpow[0][4 * d], y);
-		in ^= lane >= d ? ys : 0u;
-	}
-	if (lane == 63) s_w[wv] = in;
-	__syncthreads();
-	// the earlier waves of the tile: lane j < wv holds wave j's total, shifted
-	// over the 256 (wv - 1 - j) blocks between it and this wave
-	uint32_t pw = lane < wv ? xmul(T->bpow[1][wv - 1 - lane], s_w[lane]) : 0u;
-	pw = wave_xor(pw);
-	uint32_t ex = (uint32_t)__shfl_up((int)in, 1);
-	ex = lane ? ex : 0u;  // this thread's start, relative to its wave's start
-	uint32_t ts = xmul(T->bpow[0][4 * lane], pw) ^ ex;  // ... relative to the tile's start
-	uint32_t xs = xmul_blocks(T, xt, 4 * tid) ^ ts;     // the extent prefix at this thread's first block
-	// Y[4t'+j] = X_{4t'+j} * M = xs * M^(j+1) ^ c_j ^ B_j
-#pragma unroll
-	for (int j = 0; j < 4; ++j)
-		if (b0 + j < G.nblk) P.x.ysc[b0 + j] = xmul(T->bpow[0][j + 1], xs) ^ cj[j] ^ B[j];
-	__syncthreads();  // s_w is reused by the next tile
-}
-
-__global__ __launch_bounds__(1024) void k_xs2(XParams P) {
-	__shared__ uint32_t s_w[16];
-	if (!x_packed(P)) return;
-	const XGeo G = x_geo(P);
-	const DevTables* T = P.tabs;
-	for (uint64_t tt = blockIdx.x; tt * kXTile < G.nblk; tt += gridDim.x)
-		x_scan_tile(P, G, T, (uint32_t)tt, s_w);
-}
-
-// ---------------------------------------------------------------------------
-// k_xfin: one buffer per thread
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_xfin(XParams P) {
-	__shared__ uint32_t s4[4][256];
-	if (!x_packed(P)) return;
-	const DevTables* T = P.tabs;
-#pragma unroll
-	for (int k = 0; k < 4; ++k) s4[k][threadIdx.x] = xld32(&T->slice4[k][threadIdx.x]);
-	const XGeo G = x_geo(P);
-	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-	const bool ok = i < P.count;
-	const uint64_t ic = ok ? i : P.count - 1;
-	uint64_t P0, P1;
-	x_buffer(P, ic, P0, P1);
-	const uint32_t sd = P.seeds ? xld32(P.seeds + ic) : P.seed;
-	const uint64_t sp = P0 - G.S, ep = P1 - G.S;
-	const uint32_t vs = xld32(P.x.vs + ic), ve = xld32(P.x.ve + ic);
-	__syncthreads();
-	// R(p): the prefix register at point p (0 at p = 0)
-	auto R = [&](uint64_t p, uint32_t v) -> uint32_t {
-		const uint32_t k = x_blk(p);
-		const uint32_t cnt = x_cnt(p, k);
-		const uint64_t p64 = p ? 4096ull * k + 64ull * cnt : 0;
-		const uint32_t y = p ? xld32(P.x.ysc + k) : 0u;
-		uint32_t r = xmul(T->xinv64[64 - cnt], y ^ v);  // (k = ~0 only at p = 0: y = v = 0 there... v unused)
-		r = p ? r : 0u;
-		const uint32_t rem = (uint32_t)(p - p64);  // < 64 bytes after the lane span
-		const uint8_t* src = reinterpret_cast<const uint8_t*>(G.S + p64);
-		u32x4 ch[4];
-#pragma unroll
-		for (uint32_t q = 0; q < 4; ++q) ch[q] = 16 * q < rem ? ld16(src + 16 * q) : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-		for (uint32_t q = 0; q < 16; ++q) {
-			if (4 * q + 4 <= rem) {
-				r ^= ch[q >> 2][q & 3];
-				r = s4[0][r & 255u] ^ s4[1][(r >> 8) & 255u] ^ s4[2][(r >> 16) & 255u] ^ s4[3][r >> 24];
-			}
-		}
-		const uint32_t wd = rem >> 2, nb = rem & 3u;
-		if (nb) {
-			uint32_t word = 0;
-#pragma unroll
-			for (uint32_t q = 0; q < 16; ++q) word = q == wd ? ch[q >> 2][q & 3] : word;
-			for (uint32_t b = 0; b < nb; ++b) r = (r >> 8) ^ s4[3][(r ^ (word >> (8 * b))) & 255u];
-		}
-		return r;
+__device__ __forceinline__ void fin_fill(uint32_t* lds, const DevTables* T) {
+	typedef __attribute__((address_space(1))) const u32x4 gq;
+	auto cp = [&](uint32_t dst, const uint32_t* src, uint32_t words) {
+		u32x4* d = reinterpret_cast<u32x4*>(lds + dst);
+		const gq* sq = (const gq*)reinterpret_cast<uintptr_t>(src);
+		for (uint32_t q = threadIdx.x; q < words / 4; q += blockDim.x) d[q] = sq[q];
 	};
-	const uint32_t re = R(ep, ve);
-	uint32_t rs = R(sp, vs) ^ ~sd;
-	// rs * x^(8 len), len = 4096a + 64c + d
-	const uint64_t len = P1 - P0;
-	rs = xmul(T->pow1[len & 63u], rs);
-	rs = xmul(T->pow64[(len >> 6) & 63u], rs);
-	if (__ballot(len >> 12)) rs = xmul_blocks(T, rs, (uint32_t)(len >> 12));
-	if (ok) P.out[i] = ~(re ^ rs);
+	cp(kFinXinv, &T->xinv64[0][0][0], 65 * 128);
+	cp(kFinPow1, &T->pow1[0][0][0], 64 * 128);
+	cp(kFinPow64, &T->pow64[0][0][0], 64 * 128);
+	cp(kFinBp0, &T->bpow[0][0][0][0], 64 * 128);
+	cp(kFinS4, &T->slice4[0][0], 4 * 256);
+	__syncthreads();
+}
+
+__global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
+	__shared__ uint32_t lds[kFinWords];
+	if (!x_packed(P)) return;
+	const DevTables* T = P.tabs;
+	const XGeo G = x_geo(P);
+	const uint64_t per = x_per(G.nblk, P.nwave);
+	const uint32_t* s4 = lds + kFinS4;
+	fin_fill(lds, T);
+	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t i = i0 + threadIdx.x;
+		const bool ok = i < P.count;
+		const uint64_t ic = ok ? i : P.count - 1;
+		uint64_t P0, P1;
+		x_buffer(P, ic, P0, P1);
+		const uint32_t sd = P.seeds ? xld32(P.seeds + ic) : P.seed;
+		const uint64_t sp = P0 - G.S, ep = P1 - G.S;
+		const uint32_t vs = xld32(P.x.vs + ic), ve = xld32(P.x.ve + ic);
+		const uint32_t ks = x_blk(sp), ke = x_blk(ep);
+		// G(p): the range-local prefix at p64, positioned at its block's end
+		uint32_t gs = sp ? xld32(P.x.zb + ks) ^ vs : 0u;
+		uint32_t ge = ep ? xld32(P.x.zb + ke) ^ ve : 0u;
+		// A buffer spanning ranges ws < we: the end point takes the aggregates of
+		// the ranges from ws to we - 1 (the start point's range start is the origin)
+		const uint64_t ws = ks / per, we = ke / per;
+		if (ws != we) {
+			uint32_t D = 0;
+			for (uint64_t v = ws; v < we; ++v) D = (v == ws ? 0u : xmul_blocks(T, D, (uint32_t)per)) ^ xld32(P.x.ragg + v);
+			ge ^= xmul_blocks(T, D, (uint32_t)(ke - we * per + 1));
+		}
+		// R(p): the prefix register at point p (0 at p = 0)
+		auto R = [&](uint64_t p, uint32_t g) -> uint32_t {
+			const uint32_t k = x_blk(p);
+			const uint32_t cnt = x_cnt(p, k);
+			const uint64_t p64 = p ? 4096ull * k + 64ull * cnt : 0;
+			uint32_t r = lmul(lds, kFinXinv + 128 * (64 - cnt), g);
+			r = p ? r : 0u;
+			const uint32_t rem = (uint32_t)(p - p64);  // < 64 bytes after the lane span
+			const uint8_t* src = reinterpret_cast<const uint8_t*>(G.S + p64);
+			u32x4 ch[4];
+#pragma unroll
+			for (uint32_t q = 0; q < 4; ++q) ch[q] = 16 * q < rem ? ld16(src + 16 * q) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+			for (uint32_t q = 0; q < 16; ++q) {
+				if (4 * q + 4 <= rem) {
+					r ^= ch[q >> 2][q & 3];
+					r = s4[r & 255u] ^ s4[256 + ((r >> 8) & 255u)] ^ s4[512 + ((r >> 16) & 255u)] ^ s4[768 + (r >> 24)];
+				}
+			}
+			const uint32_t wd = rem >> 2, nb = rem & 3u;
+			if (nb) {
+				uint32_t word = 0;
+#pragma unroll
+				for (uint32_t q = 0; q < 16; ++q) word = q == wd ? ch[q >> 2][q & 3] : word;
+				for (uint32_t b = 0; b < nb; ++b) r = (r >> 8) ^ s4[768 + ((r ^ (word >> (8 * b))) & 255u)];
+			}
+			return r;
+		};
+		const uint32_t re = R(ep, ge);
+		uint32_t rs = R(sp, gs) ^ ~sd;
+		// rs * x^(8 len), len = 4096a + 64c + d
+		const uint64_t len = P1 - P0;
+		rs = lmul(lds, kFinPow1 + 128 * (uint32_t)(len & 63u), rs);
+		rs = lmul(lds, kFinPow64 + 128 * (uint32_t)((len >> 6) & 63u), rs);
+		const uint64_t nbk = len >> 12;
+		if (nbk >= 64)
+			rs = xmul_blocks(T, rs, (uint32_t)nbk);
+		else if (nbk)
+			rs = lmul(lds, kFinBp0 + 128 * (uint32_t)nbk, rs);
+		if (ok) P.out[i] = ~(re ^ rs);
+	}
 }
 
 // ---------------------------------------------------------------------------
@@ -459,7 +492,7 @@ static uint64_t xal(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
 uint64_t extent_state_bytes(uint64_t count, uint64_t cap_blk, int num_cus) {
 	const uint64_t nwave = (uint64_t)num_cus * 16;
-	return 256 + 2 * xal(4 * count) + xal(512 * nwave) + 2 * xal(4 * cap_blk) + xal(4 * (cap_blk / kXTile + 1));
+	return 256 + 2 * xal(4 * count) + xal(512 * nwave) + xal(4 * cap_blk) + xal(4 * nwave);
 }
 
 void extent_state_carve(void* mem, uint64_t count, uint64_t cap_blk, int num_cus, XState* x) {
@@ -473,16 +506,14 @@ void extent_state_carve(void* mem, uint64_t count, uint64_t cap_blk, int num_cus
 	p += xal(4 * count);
 	x->dummy = reinterpret_cast<uint32_t*>(p);
 	p += xal(512 * nwave);
-	x->blk = reinterpret_cast<uint32_t*>(p);
+	x->zb = reinterpret_cast<uint32_t*>(p);
 	p += xal(4 * cap_blk);
-	x->ysc = reinterpret_cast<uint32_t*>(p);
-	p += xal(4 * cap_blk);
-	x->tagg = reinterpret_cast<uint32_t*>(p);
+	x->ragg = reinterpret_cast<uint32_t*>(p);
 	x->cap_blk = cap_blk;
 }
 
-// phase 0: the streaming kernel; phase 1: scan + finish.  Every kernel
-// returns at once when the packing check failed.
+// phase 0: the streaming kernel; phase 1: the finishing kernel.  Both return
+// at once when the packing check failed.
 int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                   uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                   const DevTables* tabs, int num_cus, const XState& xs, uint64_t* hstat, hipStream_t stream,
@@ -491,15 +522,12 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 	XParams P{};
 	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
 	P.seed = seed; P.seeds = seeds; P.out = out; P.x = xs; P.tabs = tabs; P.hstat = hstat;
-	if (phase == 0) {
+	P.nwave = (uint64_t)num_cus * 16;  // k_xstream: one 1024-thread workgroup per CU
+	if (phase == 0)
 		k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
-	} else {
-		// tiles past the extent: none (grid-stride over the batch's tiles)
-		uint64_t ntile = xs.cap_blk / kXTile + 1;
-		ntile = ntile < (uint64_t)num_cus ? ntile : (uint64_t)num_cus;
-		k_xs1<<<(unsigned)ntile, 1024, 0, stream>>>(P);
-		k_xs2<<<(unsigned)ntile, 1024, 0, stream>>>(P);
-		k_xfin<<<(unsigned)((count + 255) / 256), 256, 0, stream>>>(P);
+	else {
+		k_xz<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+		k_xfin<<<(unsigned)num_cus, kFinThreads, 0, stream>>>(P);
 	}
 	return 0;
 }

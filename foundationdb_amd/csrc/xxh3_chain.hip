@@ -149,7 +149,7 @@ static uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 uint64_t xxh3_chain_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes, uint64_t nwave) {
 	const uint64_t nb = nsegs / kScanSpan + 1;  // the scan covers nsegs + 1 entries (pre[nsegs] = total)
 	return al16(8 * (nb + 1)) + al16(8 * (nsegs + 1)) + 2 * al16(8 * nchains) + al16(total_bytes + 16) +
-	       al16(xxh3_workspace_bytes(nchains ? nchains : 1, nwave));
+	       al16(xxh3_workspace_bytes_for(nchains ? nchains : 1, nwave, xxh3_long_blocks_bound(total_bytes)));
 }
 
 int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint64_t* seg_len, uint64_t nsegs,
@@ -187,6 +187,8 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	P.seed = seed;
 	P.seeds = seeds;
 	P.out = out;
+	P.ws_bytes = xxh3_workspace_bytes_for(nchains ? nchains : 1, (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock,
+	                                      xxh3_long_blocks_bound(total_bytes));
 	return launch_xxh3(P, num_cus, eng, s);
 }
 

@@ -15,13 +15,48 @@ struct XxhParams {
 	const uint64_t* wave_first;  // varlen: first buffer of every wave [nwave + 1] (planner output)
 	const uint32_t* idx;         // fixed list mode: buffer i = base + idx[i]*stride, count = *d_count
 	const uint64_t* d_count;
+	uint64_t ws_bytes;           // varlen: workspace size (room past the planner's arrays: the split route)
+	uint64_t* hneed;             // varlen: host-mapped word for the blocks the long buffers needed (may be null)
+	const uint64_t* sh;          // (set by launch_xxh3) split header: long buffers are not the row kernel's
 };
 
 constexpr unsigned kWavesPerBlock = 4;
+
+// Split route for long buffers (xxh3_split.hip): buffers longer than
+// kXSplitMin whose 1 KiB blocks' stripe sums are computed in parallel
+// (phase A, PIECES of up to kXPieceBlocks blocks) and chained per buffer
+// (phase B).  Planner output in the workspace:
+constexpr uint64_t kXSplitMin = 16384;
+constexpr uint32_t kXPieceBlocks = 64;
+struct XEnt {       // one long buffer
+	uint64_t F;     // its first block in the flat stripe-sum array D
+	uint64_t len, seed, idx;
+};
+struct XPiece {     // kXPieceBlocks consecutive blocks of one long buffer (fewer at its end)
+	uint64_t p;     // the buffer's address
+	uint64_t len, d, seed;  // d: flat index of block b0 in D
+	uint32_t b0, nb;
+	uint64_t pad;
+};
+struct XSplit {
+	const uint64_t* sh;   // header: [0] split on, [1] long buffers, [2] blocks, [3] pieces
+	const XEnt* ents;
+	const XPiece* pcs;
+	uint64_t* D;          // 8 x u64 per block
+	uint64_t* out;
+	uint64_t seed;        // uniform seed (per-buffer seeds travel in the entries)
+};
+// Per block of capacity: D (64 B) + entries and pieces (<= 8 B): 72 B.
+constexpr uint64_t kXSplitBytesPerBlock = 72;
+int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stream);
 // Resident 256-thread blocks per CU of the main kernel (occupancy query, cached).
 int xxh3_blocks_per_cu();
 inline uint64_t xxh3_nwave(int num_cus) { return (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock; }
 uint64_t xxh3_workspace_bytes(uint64_t count, uint64_t nwave);
+// ... with room for the split route's `long_blocks` stripe-sum blocks (a
+// bound: total bytes / 1024 + total bytes / 16384 + 2 covers any batch).
+uint64_t xxh3_workspace_bytes_for(uint64_t count, uint64_t nwave, uint64_t long_blocks);
+inline uint64_t xxh3_long_blocks_bound(uint64_t total_bytes) { return total_bytes / 1024 + total_bytes / 16384 + 2; }
 int launch_xxh3(const XxhParams& P, int num_cus, void* ws, hipStream_t stream);
 // Fixed-length (> 240 B, 16-byte aligned base and stride) pages over a device
 // list: buffer j = base + idx[j]*stride, j < *d_count; P.count bounds the grid.

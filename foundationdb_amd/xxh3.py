@@ -26,6 +26,8 @@ def _lib():
         L.xxh3_gpu_batch_varlen.argtypes = [vp, vp, vp, u64, u64, vp, vp, vp]
         L.xxh3_gpu_varlen_workspace_bytes.restype = u64
         L.xxh3_gpu_varlen_workspace_bytes.argtypes = [u64]
+        L.xxh3_gpu_varlen_workspace_bytes_for.restype = u64
+        L.xxh3_gpu_varlen_workspace_bytes_for.argtypes = [u64, u64]
         L.xxh3_gpu_batch_varlen_ws.restype = ctypes.c_int
         L.xxh3_gpu_batch_varlen_ws.argtypes = [vp, vp, vp, u64, u64, vp, vp, vp, u64, vp]
         L.xxh3_gpu_batch_chained.restype = ctypes.c_int
@@ -58,8 +60,13 @@ def batch_fixed(buf, stride, length, count, seed=0, seeds=None, out=None, stream
     return out
 
 
-def varlen_workspace_bytes(count):
-    return int(_lib().xxh3_gpu_varlen_workspace_bytes(int(count)))
+def varlen_workspace_bytes(count, total_bytes=None):
+    """Workspace bytes for batch_varlen(workspace=...) of `count` buffers; with
+    `total_bytes` (>= the sum of the lengths), room for the split route of
+    buffers longer than 16 KiB as well."""
+    if total_bytes is None:
+        return int(_lib().xxh3_gpu_varlen_workspace_bytes(int(count)))
+    return int(_lib().xxh3_gpu_varlen_workspace_bytes_for(int(count), int(total_bytes)))
 
 
 def batch_varlen(buf, offsets, lengths, seed=0, seeds=None, out=None, stream=None, workspace=None):

@@ -41,8 +41,17 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
                           uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* stream);
 
 /* Same with a caller-owned device workspace (16-byte aligned, size from
- * xxh3_gpu_varlen_workspace_bytes): no allocation, capture-safe. */
+ * xxh3_gpu_varlen_workspace_bytes): no allocation, capture-safe.
+ * Buffers longer than 16 KiB take the SPLIT route -- the stripe sums of every
+ * 1 KiB block computed in parallel over the whole GPU, then one short
+ * sequential pass of scrambles per buffer (xxhash.h:3641-3718) -- when the
+ * workspace has room for them: xxh3_gpu_varlen_workspace_bytes_for(count,
+ * total_bytes) bytes (total_bytes >= the sum of the lengths) always do;
+ * with less room they run one buffer per 16-lane row (same digests).
+ * The convenience form sizes the library's workspace from the stream's last
+ * batch. */
 uint64_t xxh3_gpu_varlen_workspace_bytes(uint64_t count);
+uint64_t xxh3_gpu_varlen_workspace_bytes_for(uint64_t count, uint64_t total_bytes);
 int xxh3_gpu_batch_varlen_ws(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                              uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
                              uint64_t workspace_bytes, void* stream);

@@ -126,3 +126,95 @@ def extent_crcs(mem, offsets, lengths, seed):
         raw = R(e) ^ gf2_mul(R(s) ^ (~seed & 0xFFFFFFFF), xpow8(b - a))
         out.append(~raw & 0xFFFFFFFF)
     return np.array(out, dtype=np.uint32)
+
+
+def _span_registers(ext):
+    """raw register of every 64-byte span of ext (fed into 0), through the C
+    oracle: feed(0, d) = ~crc32c_append(0xFFFFFFFF, d)."""
+    from oracle import oracle as O
+    n = len(ext) // 64
+    buf = np.frombuffer(ext, np.uint8)
+    offs = np.arange(n, dtype=np.uint64) * 64
+    return ~O.batch_varlen(buf, offs, np.full(n, 64, np.uint64), seed=0xFFFFFFFF)
+
+
+def ranges_per(nblk, nwave, unit=4):
+    """Blocks per wave of k_xstream's static ranges (a multiple of `unit`)."""
+    per = (nblk + nwave - 1) // nwave
+    return (per + unit - 1) // unit * unit
+
+
+def extent_crcs_ranges(mem, offsets, lengths, seed, nwave):
+    """The same CRCs the way the kernels compute them since round 3, without a
+    scan over all blocks: wave w streams the blocks [k0, k1) = [w*per, ...) of
+    its RANGE and keeps the range-local prefix X (0 at k0):
+        Z[k] = X_k * M  (stored per block),  X_{k+1} = Z[k] ^ B[k],  A[w] = X_{k1}
+    computed by k_xz once per group of 64 blocks, lane-parallel (the carry
+    enters lane 0 as carry * M, then a 6-step weighted scan over the lanes;
+    modelled here group by group).  The ranges' global start registers are
+    X0[w+1] = X0[w] * M^per ^ A[w].  A point
+    p in block k of range w, with cnt lane spans before it, has
+        G(p) = Z[k] ^ H_k[cnt-1]    (its range-local prefix at p64, positioned
+                                     at block k's end)
+    and, positioned the same way, the global prefix G(p) ^ X0[w] * M^(k-k0+1).
+    A buffer whose two points lie in one range needs only the local values
+    (X0[w] cancels); others take the global ones."""
+    P0 = [int(o) for o in offsets]
+    P1 = [int(o) + int(l) for o, l in zip(offsets, lengths)]
+    assert eligible(P0, P1)
+    S = P0[0] & ~15
+    Eend = (P1[-1] + 15) & ~15
+    nblk = (Eend - S + 4095) // 4096
+    ext = bytes(mem[S:Eend]) + bytes(nblk * 4096 - (Eend - S))
+    lane_w = [xpow8(64 * (63 - l)) for l in range(64)]
+    spans = _span_registers(ext)
+    H = []
+    for k in range(nblk):
+        h, acc = [], 0
+        for l in range(64):
+            acc ^= gf2_mul(int(spans[64 * k + l]), lane_w[l])
+            h.append(acc)
+        H.append(h)
+    per = ranges_per(nblk, nwave) if nblk else 4
+    Z, A = [0] * nblk, []
+    for w in range(nwave):
+        k0, k1 = min(w * per, nblk), min(w * per + per, nblk)
+        X = 0
+        for g0 in range(k0, k1, 64):  # groups of 64 blocks, as k_xz does them
+            n = min(64, k1 - g0)
+            B = [H[g0 + j][63] for j in range(n)]
+            I = [B[0] ^ gf2_mul(X, M)] + B[1:]
+            d = 1
+            while d < 64:  # weighted scan: I_j ^= I_(j-d) * M^d
+                I = [I[j] ^ (gf2_mul(I[j - d], xpow8(4096 * d)) if j >= d else 0) for j in range(n)]
+                d *= 2
+            for j in range(n):
+                Z[g0 + j] = I[j] ^ B[j]  # X_{g0+j+1} ^ B = X_{g0+j} * M
+            X = I[n - 1]
+        A.append(X)
+    X0 = [0]
+    for w in range(nwave - 1):
+        X0.append(gf2_mul(X0[-1], xpow8(4096 * per)) ^ A[w])
+
+    def point(p):
+        k = (p - 1) >> 12 if p else 0
+        cnt = (p - 4096 * k) >> 6 if p else 0
+        return k, cnt, k // per
+
+    def R(p, glob):
+        if p == 0:
+            return 0
+        k, cnt, w = point(p)
+        G = Z[k] ^ (H[k][cnt - 1] if cnt else 0)
+        if glob:
+            G ^= gf2_mul(X0[w], xpow8(4096 * (k - w * per + 1)))
+        p64 = 4096 * k + 64 * cnt
+        return feed(gf2_mul(G, xpow8_inv(64 * (64 - cnt))), ext[p64:p])
+
+    out = []
+    for a, b in zip(P0, P1):
+        s, e = a - S, b - S
+        glob = point(s)[2] != point(e)[2]
+        raw = R(e, glob) ^ gf2_mul(R(s, glob) ^ (~seed & 0xFFFFFFFF), xpow8(b - a))
+        out.append(~raw & 0xFFFFFFFF)
+    return np.array(out, dtype=np.uint32)

@@ -37,6 +37,10 @@ def test_extent_model_matches_oracle(case):
         got = X.extent_crcs(mem, offs, lens, seed)
         want = O.batch_varlen(mem, np.array(offs, np.uint64), np.array(lens, np.uint64), seed=seed)
         assert np.array_equal(got, want), case
+        # the range-local form (per-wave prefixes, a scan over waves only)
+        for nwave in (1, 2, 5):
+            got = X.extent_crcs_ranges(mem, offs, lens, seed, nwave)
+            assert np.array_equal(got, want), (case, nwave)
 
 
 def test_eligibility_rule():
@@ -105,3 +109,22 @@ def test_stream_schedule_window_retired_before_the_last_block():
             pos += 64
         for nwave in (1, 2, 3):
             _check_schedule(P0, P1, nwave)
+
+
+@pytest.mark.parametrize("nwave", [1, 2, 3])
+def test_range_form_across_block_groups(nwave):
+    """Ranges of more than 64 blocks (several lane-parallel groups per range,
+    the carry between them) and buffers straddling ranges."""
+    rng = np.random.default_rng(40 + nwave)
+    mem = sm(700 << 10, 0x9A + nwave)
+    offs, lens, pos = [], [], 5
+    while True:
+        L = int(rng.integers(0, 30000)) if rng.random() < 0.8 else int(rng.integers(60000, 200000))
+        if pos + L > mem.size - 64:
+            break
+        offs.append(pos)
+        lens.append(L)
+        pos += L + int(rng.integers(0, min(max(L, 256), 4095) + 1))
+    want = O.batch_varlen(mem, np.array(offs, np.uint64), np.array(lens, np.uint64), seed=7)
+    got = X.extent_crcs_ranges(mem, offs, lens, 7, nwave)
+    assert np.array_equal(got, want)

@@ -259,3 +259,80 @@ def test_gpu_xxh3_chained_underestimated_total(cuda):
     torch.cuda.synchronize()
     cat = b"".join(h[o:o + l].tobytes() for o, l in zip(offs[:4], lens[:4]))
     assert int(got.cpu().numpy().view(np.uint64)[0]) == O.ref_xxh3_64(cat)
+
+
+@pytest.mark.gpu
+def test_gpu_xxh3_split_route_long_buffers(cuda):
+    """Buffers longer than 16 KiB on the split route (xxh3_split.hip: every
+    1 KiB block's stripe sums in parallel, then one chain of scrambles per
+    buffer): 1 MiB, 16 MiB and 100 MiB (FlowTransport's PACKET_LIMIT,
+    flow/Knobs.cpp:237) buffers at unaligned offsets, the 16 KiB threshold and
+    block-boundary lengths, mixed with short and mid-size buffers; uniform and
+    per-buffer seeds; through a caller workspace sized for the route, and
+    through the convenience form on a fresh stream (its first batch has no
+    room yet and runs on the row kernel, the next ones take the split route).
+    The three big buffers are also checked against the reference's own
+    flow/xxhash.c."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    rng = np.random.default_rng(3641)
+    h = O.splitmix64((150 << 20) // 8, 0x3718).view(np.uint8)
+    d = torch.from_numpy(h).to(cuda)
+    big = [(1 << 20) + 3, 16 << 20, 100 << 20]
+    edge = [16384, 16385, 17408, 17409, 20000, 65536, 65537, 1 << 20, 3, 0, 240, 241, 1024, 4096]
+    mid = [int(x) for x in rng.integers(16000, 300000, 300)] + [int(x) for x in rng.integers(0, 5000, 300)]
+    lens = np.array(big + edge + mid, dtype=np.int64)
+    offs = np.array([int(rng.integers(0, h.size - L + 1)) for L in lens], dtype=np.int64)
+    offs[:3] = [7, 101 << 20 | 5, 1 << 20 | 9]
+    seeds = rng.integers(0, 2 ** 63, lens.size, dtype=np.int64)
+    want = O.xxh3_batch_varlen(h, offs, lens)
+    want_s = O.xxh3_batch_varlen(h, offs, lens, seeds=seeds.view(np.uint64))
+    if O.xxh3_reference_available():
+        for j in range(3):
+            assert int(want[j]) == O.ref_xxh3_64(h[offs[j]:offs[j] + lens[j]].tobytes())
+            assert int(want_s[j]) == O.ref_xxh3_64(h[offs[j]:offs[j] + lens[j]].tobytes(), int(seeds[j]))
+    o, l, sd = i64(offs, cuda), i64(lens, cuda), torch.from_numpy(seeds).to(cuda)
+    ws = torch.empty(X.varlen_workspace_bytes(lens.size, int(lens.sum())), dtype=torch.uint8, device=cuda)
+    assert np.array_equal(host(X.batch_varlen(d, o, l, workspace=ws)), want)
+    assert np.array_equal(host(X.batch_varlen(d, o, l, seeds=sd, workspace=ws)), want_s)
+    s = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            got = X.batch_varlen(d, o, l, stream=s)
+            got_s = X.batch_varlen(d, o, l, seeds=sd, stream=s)
+            s.synchronize()
+            assert np.array_equal(host(got), want)
+            assert np.array_equal(host(got_s), want_s)
+
+
+@pytest.mark.gpu
+def test_gpu_xxh3_split_route_fixed_and_chained(cuda):
+    """Fixed-length long buffers (batch_fixed > 16 KiB: the split route with
+    the library's workspace) and one 100 MiB packet over a PacketBuffer chain
+    of segments (fdbrpc/FlowTransport.cpp:2025-2068) with small chains around
+    it, against the oracle / the reference."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    h = O.splitmix64((110 << 20) // 8, 0x2068).view(np.uint8)
+    d = torch.from_numpy(h).to(cuda)
+    for length, stride, count in ((65536 + 5, 65536 + 16, 300), (16385, 16400, 1000), (1 << 20, 1 << 20, 60)):
+        for seed in (0, 0xFDBEEFDB):
+            got = host(X.batch_fixed(d, stride, length, count, seed=seed, byte_offset=3))
+            assert np.array_equal(got, O.xxh3_batch_fixed(h[3:], stride, length, count, seed=seed)), (length, seed)
+    seeds = torch.arange(300, dtype=torch.int64, device=cuda) * 0x9E3779B97F4A7C15
+    got = host(X.batch_fixed(d, 65536 + 16, 65536 + 5, 300, seeds=seeds))
+    assert np.array_equal(got, O.xxh3_batch_fixed(h, 65536 + 16, 65536 + 5, 300, seeds=seeds.cpu().numpy().view(np.uint64)))
+    rng = np.random.default_rng(9)
+    nseg = 1000
+    seg = rng.integers(1, 2 * (100 << 20) // nseg, nseg)
+    seg[-1] = max(1, (100 << 20) - int(seg[:-1].sum())) if seg[:-1].sum() < (100 << 20) else 1
+    so = rng.integers(0, h.size - int(seg.max()), nseg)
+    offs = list(so) + [5, 77, 1000]
+    lens = list(seg) + [300, 20000, 0]
+    starts = [0, nseg, nseg + 1, nseg + 3]
+    t = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device=cuda)
+    got = X.batch_chained(d, t(offs), t(lens), t(starts)).cpu().numpy().view(np.uint64)
+    cat = lambda c: b"".join(h[o:o + n].tobytes() for o, n in zip(offs[starts[c]:starts[c + 1]], lens[starts[c]:starts[c + 1]]))
+    ref = O.ref_xxh3_64 if O.xxh3_reference_available() else (lambda b: O.xxh3_64(np.frombuffer(b, np.uint8)))
+    for c in range(3):
+        assert int(got[c]) == ref(cat(c)), c

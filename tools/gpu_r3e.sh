@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 3: XXH3 split route + extent route (k_xz, LDS fin): parity, bench lines, kernel stats
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_xxh3.py tests/test_gpu_parity.py -v -x --timeout 200 --timeout-method thread -k "xxh3 or extent or varlen_configs or route_choice" > gpurun_out/pytest_r3e.txt 2>&1
+rc=$?
+tail -12 gpurun_out/pytest_r3e.txt
+[ $rc -ne 0 ] && exit $rc
+for w in zipf chunks xxh3-chunks xxh3-zipf; do
+  timeout -k 10 300 python -u bench.py --workload $w --cpu-seconds 0 > gpurun_out/bench_$w.json 2>gpurun_out/bench_$w.err || exit 7
+  python -c "import json,sys; d=json.loads(open('gpurun_out/bench_$w.json').read()); print('$w', d['value'], d['ms_per_step'], d['roofline']['frac'], d['parity_ok'])"
+done
+CFGS="3:4096" WORKLOADS="zipf chunks" bash tools/prof_routes.sh || exit 1
+WORKLOADS="xxh3-chunks" bash tools/prof_quick.sh || exit 1
