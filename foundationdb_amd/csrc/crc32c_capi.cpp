@@ -623,14 +623,14 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
 	}
 	const uint64_t last = mapped ? *reinterpret_cast<volatile uint64_t*>(ss->hst_h + kHstatXxhNeed) : 0;
 	const uint64_t room = last + last / 4;
+	const uint64_t want = fdbxxh::xxh3_workspace_bytes_for(count, fdbxxh::xxh3_nwave(st->num_cus), room);
 	void* ws = nullptr;
 	uint64_t have = 0;
 	std::unique_lock<std::mutex> hold;
-	if (int rc = stream_workspace(st, s, fdbxxh::xxh3_workspace_bytes_for(count, fdbxxh::xxh3_nwave(st->num_cus), room),
-	                              &ws, &have, &hold))
-		return rc;
-	return xxh3_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream,
-	                        mapped ? ss->hst_d + kHstatXxhNeed : nullptr);
+	if (int rc = stream_workspace(st, s, want, &ws, &have, &hold)) return rc;
+	// (the room asked for, not the whole workspace: no long buffers last time, no split launches now)
+	return xxh3_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, want < have ? want : have,
+	                        stream, mapped ? ss->hst_d + kHstatXxhNeed : nullptr);
 }
 
 uint64_t xxh3_gpu_chained_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes) {

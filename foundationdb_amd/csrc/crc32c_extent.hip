@@ -28,15 +28,17 @@
 // positioned there: G(e) ^= D * M^(ke - k0(we) + 1).  Then
 //     crc32c_append(seed, buffer) = ~(R(e) ^ (R(s) ^ ~seed) * x^(8 len)).
 //
-//   k_v7count (crc32c_varlen.hip)  the packing check (epoch-tagged flags) and
-//                                  the window engine's tile sums (its fallback)
+//   k_v7count (crc32c_varlen.hip)  the packing and capacity checks (epoch-tagged
+//                                  flags) and the stream's route statistics
 //   k_xstream   static block ranges per wave; per block: chains, lane weights,
 //               prefix XOR (DPP), the block register; the points of the block
 //               from a window of 64 buffers in the lanes (ds_bpermute)
 //   k_xz        per range: the block registers turned into the range-local
 //               prefixes Z (a lane-parallel weighted scan, LDS tables)
 //   k_xfin      per buffer: R(s), R(e) (the < 64-byte remainders re-read),
-//               the range aggregates between them, x^(8 len), the inversion
+//               the range aggregates between them, x^(8 len), the inversion;
+//               a batch that failed the checks: every buffer directly, one
+//               lane each (x_fallback)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -126,9 +128,7 @@ __device__ __forceinline__ uint32_t x_cnt(uint64_t p, uint32_t k) {
 constexpr uint32_t kXU = 2;  // blocks per unit (register chains interleaved)
 
 __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
-	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat)  // for the stream's next route choice
-		P.hstat[kHstatXfail] = x_unordered(P) ? 1 : 0;
-	if (!x_packed(P)) return;  // the window engine (launched behind) checksums this batch
+	if (!x_packed(P)) return;  // k_xfin checksums this batch buffer by buffer
 	if (x_geo(P).nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
 	FillRegs fill;
 	fill_issue_1024(fill, P.tabs);  // table loads in flight while the ranges are found
@@ -389,7 +389,8 @@ constexpr uint32_t kFinPow1 = kFinXinv + 65 * 128;      // pow1[64]
 constexpr uint32_t kFinPow64 = kFinPow1 + 64 * 128;     // pow64[64]
 constexpr uint32_t kFinBp0 = kFinPow64 + 64 * 128;      // bpow[0][0..63]
 constexpr uint32_t kFinS4 = kFinBp0 + 64 * 128;         // slice4[4][256]
-constexpr uint32_t kFinWords = kFinS4 + 4 * 256;        // 33920 words = 132.5 KiB
+constexpr uint32_t kFinC = kFinS4 + 4 * 256;            // M^per (built per launch)
+constexpr uint32_t kFinWords = kFinC + 128;             // 34048 words = 133 KiB
 
 __device__ __forceinline__ uint32_t lmul(const uint32_t* lds, uint32_t tab, uint32_t v) {
 	uint32_t r = 0;
@@ -413,13 +414,63 @@ __device__ __forceinline__ void fin_fill(uint32_t* lds, const DevTables* T) {
 	__syncthreads();
 }
 
+// The batch failed the packing or capacity check (k_v7count): every lane
+// checksums its buffers directly -- crc32c_append's register loop
+// (contrib/crc32/crc32c.cpp:346-356) with 4-byte slicing from LDS, 16-byte
+// loads -- correct for any batch, slow (the stream's next batches take the
+// window engine: kHstatXfail).
+__device__ void x_fallback(const XParams& P, const uint32_t* s4) {
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.count;
+	     i += (uint64_t)gridDim.x * blockDim.x) {
+		uint64_t P0, P1;
+		x_buffer(P, i, P0, P1);
+		uint32_t r = ~(P.seeds ? xld32(P.seeds + i) : P.seed);
+		auto byte = [&](uint64_t a) { r = (r >> 8) ^ s4[768 + ((r ^ ld1(reinterpret_cast<const uint8_t*>(a))) & 255u)]; };
+		auto word = [&](uint32_t w) {
+			r ^= w;
+			r = s4[r & 255u] ^ s4[256 + ((r >> 8) & 255u)] ^ s4[512 + ((r >> 16) & 255u)] ^ s4[768 + (r >> 24)];
+		};
+		uint64_t a = P0;
+		for (; a < P1 && (a & 15); ++a) byte(a);
+		for (; a + 16 <= P1; a += 16) {
+			const u32x4 v = ld16(reinterpret_cast<const uint8_t*>(a));
+			word(v[0]);
+			word(v[1]);
+			word(v[2]);
+			word(v[3]);
+		}
+		for (; a < P1; ++a) byte(a);
+		P.out[i] = ~r;
+	}
+}
+
 __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	__shared__ uint32_t lds[kFinWords];
-	if (!x_packed(P)) return;
+	const bool packed = x_packed(P);
+	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat)  // for the stream's next route choice
+		P.hstat[kHstatXfail] = x_unordered(P) ? 1 : 0;
 	const DevTables* T = P.tabs;
+	if (!packed) {
+		for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) lds[kFinS4 + k] = xld32(&T->slice4[0][0] + k);
+		__syncthreads();
+		x_fallback(P, lds + kFinS4);
+		return;
+	}
 	const XGeo G = x_geo(P);
 	const uint64_t per = x_per(G.nblk, P.nwave);
 	const uint32_t* s4 = lds + kFinS4;
+	// nibble tables of C = M^per (the range stride), for the straddling
+	// buffers' aggregate chains: entry [n][v] = (v x^4n) * C, bit by bit
+	if (threadIdx.x < 128) {
+		const uint32_t C = xmul_blocks(T, 0x80000000u, (uint32_t)per);
+		uint32_t a = (threadIdx.x & 15u) << (4 * (threadIdx.x >> 4)), b = C, r = 0;
+		for (int q = 0; q < 32; ++q) {
+			r ^= (a & 0x80000000u) ? b : 0u;
+			a <<= 1;
+			b = (b & 1u) ? (b >> 1) ^ 0x82f63b78u : (b >> 1);
+		}
+		lds[kFinC + threadIdx.x] = r;
+	}
 	fin_fill(lds, T);
 	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t i = i0 + threadIdx.x;
@@ -439,8 +490,9 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		const uint64_t ws = ks / per, we = ke / per;
 		if (ws != we) {
 			uint32_t D = 0;
-			for (uint64_t v = ws; v < we; ++v) D = (v == ws ? 0u : xmul_blocks(T, D, (uint32_t)per)) ^ xld32(P.x.ragg + v);
-			ge ^= xmul_blocks(T, D, (uint32_t)(ke - we * per + 1));
+			for (uint64_t v = ws; v < we; ++v) D = lmul(lds, kFinC, D) ^ xld32(P.x.ragg + v);
+			const uint32_t j = (uint32_t)(ke - we * per + 1);
+			ge ^= j < 64 ? lmul(lds, kFinBp0 + 128 * j, D) : xmul_blocks(T, D, j);
 		}
 		// R(p): the prefix register at point p (0 at p = 0)
 		auto R = [&](uint64_t p, uint32_t g) -> uint32_t {
@@ -527,7 +579,9 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 		k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
 	else {
 		k_xz<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
-		k_xfin<<<(unsigned)num_cus, kFinThreads, 0, stream>>>(P);
+		// persistent, but no more workgroups than the buffers fill (each fills 133 KiB of LDS)
+		const uint64_t g = (count + kFinThreads - 1) / kFinThreads;
+		k_xfin<<<(unsigned)(g < (uint64_t)num_cus ? g : (uint64_t)num_cus), kFinThreads, 0, stream>>>(P);
 	}
 	return 0;
 }

@@ -381,7 +381,8 @@ struct V7Params {
 	uint64_t* hstat;           // route statistics of tile 0 (host-mapped, may be null): RouteStat
 	uint32_t* err;             // sticky refusal flag of the stream (host-mapped, may be null)
 	// extent route (kRouteExtent, crc32c_extent.hip): the count kernel checks
-	// the packing; prep and the window kernel run only if the check failed
+	// the packing (the extent kernels follow it; prep and the window kernel
+	// are not launched)
 	uint32_t* xhdr;            // [0] / [1]: epoch of the last launch found not packed / over capacity
 	uint32_t epoch;
 	uint64_t xcap;             // extent blocks the route's arrays hold
@@ -405,13 +406,6 @@ __device__ __forceinline__ bool v7_packed_pair(const V7Params& P, uint64_t i, ui
 	const uint64_t e = off + len;
 	const uint64_t gap = on - e;
 	return on >= e && gap < 4096 && gap <= (len > 256 ? len : 256);
-}
-// Wave-uniform: this launch routes the batch to the extent kernels (the
-// window engine's kernels then return at once).
-__device__ __forceinline__ bool v7_extent_taken(const V7Params& P) {
-	if (!P.xhdr) return false;
-	const uint32_t a = rdfirst(gld32(P.xhdr)), b = rdfirst(gld32(P.xhdr + 1));
-	return a != P.epoch && b != P.epoch;
 }
 // The first 256 buffers' bytes by span class and whether they are packed,
 // for the stream's next route choice (tile 0 of prep, or of the count kernel
@@ -486,7 +480,6 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 // and entries are compiled out (fewer registers: 8 blocks per CU).
 template <bool BIG>
 __device__ __forceinline__ void v7prep(const V7Params& P) {
-	if (v7_extent_taken(P)) return;  // the extent kernels checksum this batch
 	const uint64_t bigmin = BIG ? P.bigmin : 0;
 	__shared__ uint32_t s4[4][256];    // slice4 tables (no bank replication: this kernel is not LDS-bound)
 	__shared__ uint32_t iz[16 * 128];  // inv_z nibble tables: x^(-8z), z < 16 (small buffers' trailing zeros)
@@ -796,7 +789,6 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	const uint64_t wpb = blockDim.x >> 6;
 	typedef __attribute__((address_space(1))) const uint64_t g_u64;
 	const g_u64* hp = (const g_u64*)reinterpret_cast<uintptr_t>(P.hdr);
-	if (v7_extent_taken(P)) return;  // the extent kernels checksum this batch (prep left hdr stale)
 	const uint64_t total = rdfirst64(hp[0]), Qs = rdfirst64(hp[1]);
 	const uint64_t r_base = (uint64_t)blockIdx.x * kV7RangesPerBlock;
 	// no slots for this workgroup (e.g. every buffer went to the block route):
@@ -1200,6 +1192,13 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.scanned = ntile > kScanTiles;
 	P.selfsum = ntile <= kSelfSumTiles;
 	if (!P.selfsum || extent) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);  // (extent: the packing check)
+	if (extent) {
+		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
+		              0);
+		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
+		              1);
+		return 0;
+	}
 	if (P.scanned)
 		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4, P.bigmin ? P.bsum : nullptr,
 		                               P.bigmin ? P.nsum : nullptr);
@@ -1213,13 +1212,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 		B.out = out; B.ctr = P.bctr; B.tabs = tabs;
 		launch_bigblocks(B, num_cus, stream);
 	}
-	if (extent)
-		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
-		              0);
 	if (route != kRouteBlocks) k_varlen7<<<(unsigned)grid, FDBCRC_V7_THREADS, 0, stream>>>(P);
-	if (extent)
-		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
-		              1);
 	return 0;
 }
 

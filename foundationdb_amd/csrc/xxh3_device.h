@@ -17,7 +17,7 @@ struct XxhParams {
 	const uint64_t* d_count;
 	uint64_t ws_bytes;           // varlen: workspace size (room past the planner's arrays: the split route)
 	uint64_t* hneed;             // varlen: host-mapped word for the blocks the long buffers needed (may be null)
-	const uint64_t* sh;          // (set by launch_xxh3) split header: long buffers are not the row kernel's
+	const uint8_t* lflag;        // (set by launch_xxh3) per buffer: the split route took it (not the row kernel's)
 };
 
 constexpr unsigned kWavesPerBlock = 4;
@@ -39,14 +39,15 @@ struct XPiece {     // kXPieceBlocks consecutive blocks of one long buffer (fewe
 	uint64_t pad;
 };
 struct XSplit {
-	const uint64_t* sh;   // header: [0] split on, [1] long buffers, [2] blocks, [3] pieces
+	const uint64_t* sh;   // counters: [0] long buffers, [1] blocks claimed, [2] pieces
 	const XEnt* ents;
 	const XPiece* pcs;
 	uint64_t* D;          // 8 x u64 per block
 	uint64_t* out;
 	uint64_t seed;        // uniform seed (per-buffer seeds travel in the entries)
 };
-// Per block of capacity: D (64 B) + entries and pieces (<= 8 B): 72 B.
+// Per block of capacity: D (64 B) + entries and pieces (<= 8 B): 72 B (plus a
+// flag byte per buffer).
 constexpr uint64_t kXSplitBytesPerBlock = 72;
 int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stream);
 // Resident 256-thread blocks per CU of the main kernel (occupancy query, cached).

@@ -625,7 +625,7 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 	uint64_t* __restrict__ out = P.out;
 	const uint64_t seed0 = P.seed;
 	// long buffers on the split route (xxh3_split.hip) are not this kernel's
-	const uint64_t lmax = (P.sh && *P.sh) ? kXSplitMin : ~uint64_t(0);
+	const uint8_t* __restrict__ lflag = P.lflag;
 
 
 	// ---- long buffers: rows
@@ -643,7 +643,8 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 			blen = in ? lengths[i] : 0;
 			boff = in ? offsets[i] : 0;
 			if (SEEDS) bseed = in ? seeds[i] : 0;
-			bm = __ballot(blen > 240 && blen <= lmax);
+			const bool sp = lflag && in && blen > kXSplitMin && lflag[i];
+			bm = __ballot(blen > 240 && !sp);
 		}
 		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): bank B complete
 	};
@@ -837,10 +838,12 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 // ---------------------------------------------------------------------------
 // Varlen planning: whole buffers per wave, balanced by bytes.  Wave w takes
 // the buffers whose start lies in [w*Q, (w+1)*Q) of the concatenated stream
-// (cost = length + 64).  With split capacity in the workspace, buffers longer
-// than kXSplitMin go to the split route (xxh3_split.hip) instead: their cost
-// here drops to 64, and the planner lays out their entries, pieces and
-// stripe-sum blocks (per-tile sums, one scan, then every buffer writes its own).
+// (cost = length + 64).  With room for the split route in the workspace,
+// k_xplan also hands every buffer longer than kXSplitMin its stripe-sum
+// blocks, entry and pieces (xxh3_split.hip) by claiming them from three
+// counters (one atomic per wave and counter); a buffer whose claim does not
+// fit stays on the row kernel.  Its flag byte tells the cost scan and the row
+// kernel which buffers the split route took (their cost here drops to 64).
 // ---------------------------------------------------------------------------
 struct XPlanP {
 	const uint64_t* lengths;  // nullptr: fixed length
@@ -849,202 +852,176 @@ struct XPlanP {
 	const uint8_t* base;
 	uint64_t stride, length, count, seed;
 	uint64_t* tiles;          // [ntile + 2]: cost prefixes, total, quantum
-	uint64_t* ts;             // [4][ntile]: split cost, long buffers, blocks, pieces (sums, then prefixes)
-	uint64_t* sh;             // split header (XSplit::sh)
+	uint64_t* tneed;          // [ntile]: blocks of the tile's long buffers (the host's room estimate)
+	uint64_t* sh;             // split counters (XSplit::sh): [0] long buffers, [1] blocks, [2] pieces (zeroed before)
+	uint8_t* flag;            // per buffer: 1 if the split route took it
 	uint64_t* wave_first;
 	uint64_t ntile, nwave;
 	XEnt* ents;
 	XPiece* pcs;
-	uint64_t capD, capS, capP;
+	uint64_t capD;
 	uint64_t* hneed;          // host-mapped word (may be null): blocks the batch's long buffers need
 };
 __device__ __forceinline__ uint64_t xp_len(const XPlanP& Q, uint64_t i) { return Q.lengths ? Q.lengths[i] : Q.length; }
 __device__ __forceinline__ uint64_t xp_off(const XPlanP& Q, uint64_t i) { return Q.offsets ? Q.offsets[i] : i * Q.stride; }
-__device__ __forceinline__ bool xp_long(uint64_t len) { return len > kXSplitMin; }
 __device__ __forceinline__ uint64_t xp_blocks(uint64_t len) { return ((len - 1) >> 10) + 1; }
+__device__ __forceinline__ uint64_t xp_cost(uint64_t len, bool split) { return split ? 64 : len + 64; }
+
+// Exclusive prefix of v over the wave's active lanes and the wave's total.
+__device__ __forceinline__ uint64_t wave_excl(uint64_t v, uint64_t* tot) {
+	const int lane = threadIdx.x & 63;
+	uint64_t inc = v;
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint64_t y = __shfl_up(inc, o);
+		if (lane >= o) inc += y;
+	}
+	*tot = __shfl(inc, 63);
+	return inc - v;
+}
 
 __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
-	__shared__ uint64_t part[4][5];
+	__shared__ uint64_t part[8];
 	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-	uint64_t v[5] = {0, 0, 0, 0, 0};
-	if (i < Q.count) {
-		const uint64_t len = xp_len(Q, i);
-		const bool lg = xp_long(len);
+	const int lane = threadIdx.x & 63;
+	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
+	bool split = false;
+	const uint64_t need = i < Q.count && len > kXSplitMin ? xp_blocks(len) : 0;
+	if (Q.capD && __ballot(need != 0)) {  // (rare: waves holding long buffers)
+		const bool lg = i < Q.count && len > kXSplitMin;
 		const uint64_t nb = lg ? xp_blocks(len) : 0;
-		v[0] = len + 64;  // +64: per-buffer cost floor
-		v[1] = lg ? 64 : len + 64;
-		v[2] = lg ? 1 : 0;
-		v[3] = nb;
-		v[4] = (nb + kXPieceBlocks - 1) / kXPieceBlocks;
+		uint64_t tot;
+		const uint64_t ex = wave_excl(nb, &tot);
+		uint64_t F0 = 0;
+		if (lane == 0) F0 = atomicAdd((unsigned long long*)&Q.sh[1], (unsigned long long)tot);
+		const uint64_t F = __shfl(F0, 0) + ex;
+		split = lg && F + nb <= Q.capD;  // (a claim past the room leaves a hole, never an overlap)
+		const uint64_t np = split ? (nb + kXPieceBlocks - 1) / kXPieceBlocks : 0;
+		uint64_t tp, ts;
+		const uint64_t exp_ = wave_excl(np, &tp);
+		const uint64_t exs = wave_excl(split ? 1 : 0, &ts);
+		uint64_t P0 = 0, S0 = 0;
+		if (lane == 0 && ts) {
+			P0 = atomicAdd((unsigned long long*)&Q.sh[2], (unsigned long long)tp);
+			S0 = atomicAdd((unsigned long long*)&Q.sh[0], (unsigned long long)ts);
+		}
+		// broadcast with every lane active (a shuffle inside the branch below
+		// could read lane 0 while lane 0 is masked off)
+		const uint64_t pcb = __shfl(P0, 0), sb = __shfl(S0, 0);
+		if (split) {
+			const uint64_t pc = pcb + exp_, sidx = sb + exs;
+			const uint64_t sd = Q.seeds ? Q.seeds[i] : Q.seed;
+			Q.ents[sidx] = XEnt{F, len, sd, i};
+			const uint64_t p = reinterpret_cast<uint64_t>(Q.base) + xp_off(Q, i);
+			for (uint64_t j = 0; j < np; ++j) {
+				const uint32_t b0 = (uint32_t)(j * kXPieceBlocks);
+				const uint32_t n = (uint32_t)(nb - b0 < kXPieceBlocks ? nb - b0 : kXPieceBlocks);
+				Q.pcs[pc + j] = XPiece{p, len, F + b0, sd, b0, n, 0};
+			}
+		}
 	}
-#pragma unroll
-	for (int k = 0; k < 5; ++k)
-		for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
-	if ((threadIdx.x & 63) == 0)
-#pragma unroll
-		for (int k = 0; k < 5; ++k) part[threadIdx.x >> 6][k] = v[k];
+	if (Q.capD && i < Q.count) Q.flag[i] = split ? 1 : 0;
+	uint64_t v = i < Q.count ? xp_cost(len, split) : 0;  // +64: per-buffer cost floor
+	uint64_t nd = need;
+	for (int o = 32; o > 0; o >>= 1) {
+		v += __shfl_xor(v, o);
+		nd += __shfl_xor(nd, o);
+	}
+	if (lane == 0) {
+		part[threadIdx.x >> 6] = v;
+		part[4 + (threadIdx.x >> 6)] = nd;
+	}
 	__syncthreads();
-	if (threadIdx.x < 5) {
-		const int k = threadIdx.x;
-		const uint64_t t = part[0][k] + part[1][k] + part[2][k] + part[3][k];
-		if (k == 0)
-			Q.tiles[blockIdx.x] = t;
-		else
-			Q.ts[(uint64_t)(k - 1) * Q.ntile + blockIdx.x] = t;
+	if (threadIdx.x == 0) {
+		Q.tiles[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+		Q.tneed[blockIdx.x] = part[4] + part[5] + part[6] + part[7];
 	}
 }
 
-// Exclusive scan of one value per thread over a 1024-thread workgroup;
-// returns the exclusive prefix, *tot the workgroup's total.
-__device__ __forceinline__ uint64_t wg_scan(uint64_t x, uint64_t* wsum, uint64_t* tot) {
+// Single workgroup: in-place exclusive scan of the tile sums; tiles[ntile] =
+// total cost, tiles[ntile + 1] = quantum Q = ceil(total / nwave).
+__global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
+	__shared__ uint64_t wsum[16];
+	__shared__ uint64_t carry_s;
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-	uint64_t inc = x;
+	const uint64_t ntile = Q.ntile;
+	uint64_t* tiles = Q.tiles;
+	__shared__ uint64_t nsum[16];
+	if (t == 0) carry_s = 0;
+	uint64_t nd = 0;  // the batch's long blocks, for the host (room for the next batch)
+	if (Q.hneed)
+		for (uint64_t k = t; k < ntile; k += 1024) nd += Q.tneed[k];
+	__syncthreads();
+	for (uint64_t c0 = 0; c0 < ntile; c0 += 1024) {
+		const uint64_t k = c0 + t;
+		const uint64_t x = k < ntile ? tiles[k] : 0;
+		uint64_t inc = x;
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint64_t y = __shfl_up(inc, o);
+			if ((int)lane >= o) inc += y;
+		}
+		if (lane == 63) wsum[wv] = inc;
+		__syncthreads();
+		uint64_t wb = 0;
+		for (uint32_t q = 0; q < wv; ++q) wb += wsum[q];
+		const uint64_t carry = carry_s;
+		if (k < ntile) tiles[k] = carry + wb + inc - x;
+		__syncthreads();
+		if (t == 1023) carry_s = carry + wb + inc;
+		__syncthreads();
+	}
+	if (Q.hneed) {
+		for (int o = 32; o > 0; o >>= 1) nd += __shfl_xor(nd, o);
+		if (lane == 0) nsum[wv] = nd;
+	}
+	__syncthreads();
+	if (t == 0) {
+		const uint64_t total = carry_s;
+		tiles[ntile] = total;
+		tiles[ntile + 1] = (total + Q.nwave - 1) / Q.nwave;
+		if (Q.hneed) {
+			uint64_t a = 0;
+			for (int q = 0; q < 16; ++q) a += nsum[q];
+			*(volatile uint64_t*)Q.hneed = a;
+		}
+	}
+}
+
+// One workgroup per tile of 256 buffers: buffer i (cost c_i, start s_i) is
+// the first buffer of every wave w with s_{i-1} < w*Q <= s_i; waves past
+// the last buffer get `count`.
+__global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
+	__shared__ uint64_t wsum[4];
+	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+	const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+	auto cost_of = [&](uint64_t b) -> uint64_t { return xp_cost(xp_len(Q, b), Q.capD && Q.flag[b]); };
+	const uint64_t cost = i < Q.count ? cost_of(i) : 0;
+	uint64_t inc = cost;
 	for (int o = 1; o < 64; o <<= 1) {
 		const uint64_t y = __shfl_up(inc, o);
 		if ((int)lane >= o) inc += y;
 	}
 	if (lane == 63) wsum[wv] = inc;
 	__syncthreads();
-	uint64_t wb = 0, all = 0;
-	for (uint32_t q = 0; q < 16; ++q) {
-		const uint64_t s = wsum[q];
-		wb += q < wv ? s : 0;
-		all += s;
-	}
-	__syncthreads();
-	*tot = all;
-	return wb + inc - x;
-}
-
-// Single workgroup: decides whether the batch takes the split route (every
-// long buffer fits the capacity), then scans the tile sums in place:
-// tiles[ntile] = total cost, tiles[ntile + 1] = quantum Q = ceil(total / nwave).
-__global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
-	__shared__ uint64_t wsum[16];
-	const uint32_t t = threadIdx.x;
-	const uint64_t nt = Q.ntile;
-	uint64_t tS = 0, tB = 0, tP = 0;
-	{
-		uint64_t a = 0, b = 0, c = 0;
-		for (uint64_t k = t; k < nt; k += 1024) {
-			a += Q.ts[nt + k];
-			b += Q.ts[2 * nt + k];
-			c += Q.ts[3 * nt + k];
-		}
-		wg_scan(a, wsum, &tS);
-		wg_scan(b, wsum, &tB);
-		wg_scan(c, wsum, &tP);
-	}
-	// (the totals are recorded for the host even without room: it grows the
-	// stream's workspace for the next batch)
-	const bool on = tB != 0 && tB <= Q.capD && tS <= Q.capS && tP <= Q.capP;
-	if (t == 0) {
-		Q.sh[0] = on ? 1 : 0;
-		Q.sh[1] = tS;
-		Q.sh[2] = tB;
-		Q.sh[3] = tP;
-		if (Q.hneed) *(volatile uint64_t*)Q.hneed = tB;
-	}
-	uint64_t carry[4] = {0, 0, 0, 0};
-	for (uint64_t c0 = 0; c0 < nt; c0 += 1024) {
-		const uint64_t k = c0 + t;
-		const bool in = k < nt;
-		uint64_t x0 = in ? (on ? Q.ts[k] : Q.tiles[k]) : 0, tot;
-		const uint64_t e0 = wg_scan(x0, wsum, &tot);
-		if (in) Q.tiles[k] = carry[0] + e0;
-		carry[0] += tot;
-		if (on) {
-#pragma unroll
-			for (int j = 1; j < 4; ++j) {
-				const uint64_t x = in ? Q.ts[j * nt + k] : 0;
-				const uint64_t e = wg_scan(x, wsum, &tot);
-				if (in) Q.ts[j * nt + k] = carry[j] + e;
-				carry[j] += tot;
-			}
-		}
-	}
-	if (t == 0) {
-		Q.tiles[nt] = carry[0];
-		Q.tiles[nt + 1] = (carry[0] + Q.nwave - 1) / Q.nwave;
-	}
-}
-
-// One workgroup per tile of 256 buffers: buffer i (cost c_i, start s_i) is
-// the first buffer of every wave w with s_{i-1} < w*Q <= s_i; waves past
-// the last buffer get `count`.  On the split route every long buffer writes
-// its entry and its pieces.
-__global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
-	__shared__ uint64_t wsum[4][4];
-	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-	const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
-	const bool on = Q.sh[0] != 0;
-	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
-	const bool lg = on && i < Q.count && xp_long(len);
-	const uint64_t nb = lg ? xp_blocks(len) : 0;
-	const uint64_t np = (nb + kXPieceBlocks - 1) / kXPieceBlocks;
-	uint64_t x[4] = {i < Q.count ? (lg ? 64 : len + 64) : 0, lg ? 1u : 0u, nb, np};
-	uint64_t inc[4] = {x[0], x[1], x[2], x[3]};
-	for (int o = 1; o < 64; o <<= 1) {
-#pragma unroll
-		for (int j = 0; j < 4; ++j) {
-			const uint64_t y = __shfl_up(inc[j], o);
-			if ((int)lane >= o) inc[j] += y;
-		}
-	}
-	if (lane == 63)
-#pragma unroll
-		for (int j = 0; j < 4; ++j) wsum[wv][j] = inc[j];
-	__syncthreads();
-	uint64_t ex[4];
-#pragma unroll
-	for (int j = 0; j < 4; ++j) {
-		uint64_t wb = 0;
-		for (uint32_t q = 0; q < wv; ++q) wb += wsum[q][j];
-		ex[j] = wb + inc[j] - x[j];
-	}
+	uint64_t wb = 0;
+	for (uint32_t q = 0; q < wv; ++q) wb += wsum[q];
 	const uint64_t q = Q.tiles[Q.ntile + 1];
-	const uint64_t cost = x[0];
-	const uint64_t start = Q.tiles[blockIdx.x] + ex[0];
+	const uint64_t start = Q.tiles[blockIdx.x] + wb + inc - cost;
 	if (i < Q.count) {
 		// waves w with s_{i-1} < w*q <= s_i, i.e. [floor(s_{i-1}/q) + 1, floor(s_i/q)];
-		// buffer 0 takes w = 0 (the previous buffer's cost: start - cost_{i-1}, from
-		// the inclusive scan one lane down or the previous tile's last)
-		(void)cost;
-		const uint64_t prev_inc = start;  // s_i = exclusive prefix = inclusive prefix of i - 1
-		uint64_t prev_cost;
-		if (i == 0) {
-			prev_cost = 0;
-		} else {
-			const uint64_t pl = xp_len(Q, i - 1);
-			prev_cost = (on && xp_long(pl)) ? 64 : pl + 64;
-		}
-		const uint64_t prev = i == 0 ? 0 : prev_inc - prev_cost;
+		// buffer 0 takes w = 0
+		const uint64_t prev = i == 0 ? 0 : start - cost_of(i - 1);
 		const uint64_t w_lo = i == 0 ? 0 : prev / q + 1;
 		const uint64_t w_hi = start / q;
 		for (uint64_t w = w_lo; w <= w_hi && w < Q.nwave; ++w) Q.wave_first[w] = i;
 		if (i + 1 == Q.count)  // waves whose first byte lies past the last buffer's start: none
 			for (uint64_t w = start / q + 1; w <= Q.nwave; ++w) Q.wave_first[w] = Q.count;
 	}
-	if (lg) {
-		const uint64_t nt = Q.ntile;
-		const uint64_t sidx = Q.ts[nt + blockIdx.x] + ex[1];
-		const uint64_t F = Q.ts[2 * nt + blockIdx.x] + ex[2];
-		const uint64_t pc = Q.ts[3 * nt + blockIdx.x] + ex[3];
-		const uint64_t sd = Q.seeds ? Q.seeds[i] : Q.seed;
-		Q.ents[sidx] = XEnt{F, len, sd, i};
-		const uint64_t p = reinterpret_cast<uint64_t>(Q.base) + xp_off(Q, i);
-		for (uint64_t j = 0; j < np; ++j) {
-			const uint32_t b0 = (uint32_t)(j * kXPieceBlocks);
-			const uint32_t n = (uint32_t)(nb - b0 < kXPieceBlocks ? nb - b0 : kXPieceBlocks);
-			Q.pcs[pc + j] = XPiece{p, len, F + b0, sd, b0, n, 0};
-		}
-	}
 }
 
 // Workspace of the varlen path: the planner arrays, then (given more room)
-// the split route's entries, pieces and stripe sums.
+// the split route's flags, entries, pieces and stripe sums.
 struct XLayout {
-	uint64_t tiles, wave_first, sh, ts, ents, pcs, D, base;
+	uint64_t tiles, tneed, wave_first, sh, flag, ents, pcs, D, base;
 	uint64_t capD, capS, capP;
 };
 static uint64_t al64(uint64_t x) { return (x + 63) & ~uint64_t(63); }
@@ -1052,16 +1029,19 @@ static XLayout xlayout(uint64_t count, uint64_t nwave, uint64_t ws_bytes) {
 	const uint64_t ntile = (count + 255) / 256;
 	XLayout L{};
 	L.tiles = 0;
-	L.wave_first = al64(8 * (ntile + 2));
+	L.tneed = al64(8 * (ntile + 2));
+	L.wave_first = al64(L.tneed + 8 * ntile);
 	L.sh = al64(L.wave_first + 8 * (nwave + 1) + 64);
-	L.ts = L.sh + 64;
-	L.base = al64(L.ts + 32 * ntile);
-	uint64_t capD = ws_bytes > L.base ? (ws_bytes - L.base) / kXSplitBytesPerBlock : 0;
+	L.base = L.sh + 64;
+	// split room: flags (1 B per buffer), then per block of capacity 72 B
+	const uint64_t fl = al64(count);
+	uint64_t capD = ws_bytes > L.base + fl ? (ws_bytes - L.base - fl) / kXSplitBytesPerBlock : 0;
 	if (capD < 256) capD = 0;
 	L.capD = capD;
-	L.capS = capD ? capD / 16 + 1 : 0;
+	L.capS = capD ? capD / 16 + 1 : 0;               // long buffers have > 16 blocks
 	L.capP = capD ? capD / kXPieceBlocks + L.capS : 0;
-	L.ents = L.base;
+	L.flag = L.base;
+	L.ents = L.flag + fl;
 	L.pcs = al64(L.ents + sizeof(XEnt) * L.capS);
 	L.D = al64(L.pcs + sizeof(XPiece) * L.capP);
 	return L;
@@ -1071,7 +1051,7 @@ uint64_t xxh3_workspace_bytes(uint64_t count, uint64_t nwave) { return xlayout(c
 uint64_t xxh3_workspace_bytes_for(uint64_t count, uint64_t nwave, uint64_t long_blocks) {
 	if (long_blocks == 0) return xxh3_workspace_bytes(count, nwave);
 	const uint64_t capD = long_blocks < 256 ? 256 : long_blocks;
-	return xlayout(count, nwave, 0).base + kXSplitBytesPerBlock * capD + 256;
+	return xlayout(count, nwave, 0).base + al64(count) + kXSplitBytesPerBlock * capD + 256;
 }
 
 int xxh3_blocks_per_cu() {
@@ -1114,17 +1094,17 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		Q.count = P.count;
 		Q.seed = P.seed;
 		Q.tiles = reinterpret_cast<uint64_t*>(w8 + L.tiles);
-		Q.ts = reinterpret_cast<uint64_t*>(w8 + L.ts);
+		Q.tneed = reinterpret_cast<uint64_t*>(w8 + L.tneed);
 		Q.sh = reinterpret_cast<uint64_t*>(w8 + L.sh);
+		Q.flag = w8 + L.flag;
 		Q.wave_first = reinterpret_cast<uint64_t*>(w8 + L.wave_first);
 		Q.ntile = ntile;
 		Q.nwave = nwave;
 		Q.ents = reinterpret_cast<XEnt*>(w8 + L.ents);
 		Q.pcs = reinterpret_cast<XPiece*>(w8 + L.pcs);
 		Q.capD = L.capD;
-		Q.capS = L.capS;
-		Q.capP = L.capP;
 		Q.hneed = P.hneed;
+		if (L.capD && hipMemsetAsync(Q.sh, 0, 64, stream) != hipSuccess) return -1;
 		k_xplan<<<(unsigned)ntile, 256, 0, stream>>>(Q);
 		k_xscan<<<1, 1024, 0, stream>>>(Q);
 		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(Q);
@@ -1140,7 +1120,7 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		}
 		if (fixed_split) return 0;  // every buffer is long: the split route did them all
 		P.wave_first = Q.wave_first;
-		P.sh = Q.sh;
+		P.lflag = L.capD ? Q.flag : nullptr;
 		if (P.seeds)
 			k_xxh3_vrows<true><<<(unsigned)grid, 256, 0, stream>>>(P);
 		else

@@ -18,9 +18,9 @@
 //            pieces per wave; the row layout of k_xxh3_rows (a 16-lane row per
 //            block: four coalesced 256-byte loads, 32x32->64 products, two DPP
 //            row rotates) writes D[b] (64 B per KiB) to the workspace.
-//   phase B  k_xsplit_b: one wave per long buffer: 4 KiB of D per coalesced
-//            load round (two rounds in flight), through LDS to eight chain
-//            lanes (one accumulator each), 64 scrambles per round, the merge.
+//   phase B  k_xsplit_b: eight long buffers per wave, eight lanes each (one
+//            accumulator per lane), the stripe sums read straight into a
+//            register ring kXRing blocks deep, one scramble per block, the merge.
 // The planner (xxh3_kernels.hip: k_xplan / k_xscan / k_xassign) picks the
 // long buffers, lays out the pieces and D, and takes them off the row kernel.
 #include <hip/hip_runtime.h>
@@ -99,8 +99,8 @@ struct AStep {
 
 template <bool SEEDS>
 __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
-	if (rdf64(gld64(S.sh + 0)) == 0) return;  // no split this batch
-	const uint64_t npc = rdf64(gld64(S.sh + 3));
+	const uint64_t npc = rdf64(gld64(S.sh + 2));
+	if (npc == 0) return;  // no long buffer this batch
 	const int lane = threadIdx.x & 63;
 	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
 	const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -243,78 +243,89 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 }
 
 // ---------------------------------------------------------------------------
-// Phase B: the chains, one wave per long buffer (64-thread workgroups,
-// grid-stride over the buffers).  Lane j < 8 holds acc[j].
+// Phase B: the chains.  Eight chains per wave: lane (c, j) = (lane / 8,
+// lane % 8) holds acc[j] of long buffer 8w + c and reads its stripe sums
+// straight into registers (the 8 lanes of a chain read 64 contiguous bytes
+// per block), kXRing blocks ahead: the sums were written by phase A and come
+// from L2 / MALL, and the ring covers their latency while the chain runs one
+// scramble per block (the only sequential part of XXH3).
 // ---------------------------------------------------------------------------
+constexpr int kXRing = 16;
+
 __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
-	__shared__ uint64_t sd[64 * 8];  // one round: 64 blocks x 8 lanes
-	if (rdf64(gld64(S.sh + 0)) == 0) return;
-	const uint64_t nsplit = rdf64(gld64(S.sh + 1));
-	const uint32_t lane = threadIdx.x;
-	const uint32_t j = lane & 7;
+	const uint64_t nsplit = rdf64(gld64(S.sh + 0));
+	const uint32_t lane = threadIdx.x, c = lane >> 3, j = lane & 7;
 	const uint64_t init = j == 0 ? P32_3 : j == 1 ? P64_1 : j == 2 ? P64_2 : j == 3 ? P64_3
 	                    : j == 4 ? P64_4 : j == 5 ? P32_2 : j == 6 ? P64_5 : P32_1;
-	for (uint64_t sidx = blockIdx.x; sidx < nsplit; sidx += gridDim.x) {
-		const XEnt E = S.ents[sidx];
-		const uint64_t len = rdf64(E.len), seed = rdf64(E.seed);
+	for (uint64_t s0 = (uint64_t)blockIdx.x * 8; s0 < nsplit; s0 += (uint64_t)gridDim.x * 8) {
+		const uint64_t s = s0 + c < nsplit ? s0 + c : nsplit - 1;  // (lanes past the end repeat the last buffer, discarded)
+		const bool own = s0 + c < nsplit;
+		const XEnt E = S.ents[s];
+		const uint64_t len = E.len, seed = E.seed;
 		const uint64_t nfull = (len - 1) >> 10, nb = nfull + 1;
-		const uint8_t* base = reinterpret_cast<const uint8_t*>(S.D + 8 * rdf64(E.F));
-		const uint64_t last16 = 64 * nb - 16;  // the last 16 bytes of this buffer's stripe sums
-		const uint64_t nround = (nb + 63) >> 6;
+		const uint64_t* dp = S.D + 8 * E.F + j;
 		const uint64_t ck = swd(16 + (int)j, seed);  // scramble key: secret + 128 + 8j
+		const uint64_t gk = sat(1 + (int)j, 3, seed);  // merge key: secret + 11 + 8j
+		const uint32_t cklo = (uint32_t)ck, ckhi = (uint32_t)(ck >> 32);
+		// scrambleAcc (xxhash.h:3702-3718) in 32-bit halves: the high half's
+		// product is off the dependent path (a ^= a >> 47 changes only the low
+		// half): shift, xor3, one 32x32->64 mad and one add per block
+		auto scr = [&](uint64_t a) __attribute__((always_inline)) -> uint64_t {
+			const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+			const uint32_t lo2 = lo ^ (hi >> 15) ^ cklo, hi2 = hi ^ ckhi;
+			const uint64_t m = (uint64_t)lo2 * (uint32_t)P32_1;
+			return m + ((uint64_t)(hi2 * (uint32_t)P32_1) << 32);
+		};
+		uint64_t nbmax = nb;  // the wave's longest chain (uniform trip count)
+#pragma unroll
+		for (int o = 8; o < 64; o <<= 1) {
+			const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(nbmax >> 32), o) << 32) |
+			                   (uint32_t)__shfl_xor((int)(uint32_t)nbmax, o);
+			nbmax = y > nbmax ? y : nbmax;
+		}
+		nbmax = rdf64(nbmax);
 		uint64_t acc = init;
-		u64x2 A[4], B[4];
-		auto ld = [&](u64x2 (&R)[4], uint64_t c) __attribute__((always_inline)) {
-#pragma unroll
-			for (int q = 0; q < 4; ++q) {
-				const uint64_t o = 4096 * c + 1024 * q + 16 * lane;
-				R[q] = *((g_u64x2*)reinterpret_cast<uintptr_t>(base + (o < last16 ? o : last16)));
-			}
+		auto ld = [&](uint64_t b) -> uint64_t { return gld64(dp + 8 * (b < nb ? b : nb - 1)); };
+		auto step = [&](uint64_t b, uint64_t v) __attribute__((always_inline)) {
+			const uint64_t a1 = acc + v, s1 = scr(a1);  // (selects, no branch: the loop stays unrolled)
+			acc = b < nfull ? s1 : (b == nfull ? a1 : acc);
 		};
-		auto round = [&](u64x2 (&R)[4], uint64_t c) __attribute__((always_inline)) {
+		// three register sets of kXRing blocks: one is consumed while the next
+		// two are in flight, then refilled (sched barriers keep the refill
+		// after the consumption: hoisted above it, the loads would need copies,
+		// and a copy of a load in flight waits for it)
+		uint64_t ra[kXRing], rb[kXRing], rc[kXRing];
+		auto fill = [&](uint64_t (&R)[kXRing], uint64_t r) __attribute__((always_inline)) {
 #pragma unroll
-			for (int q = 0; q < 4; ++q) {
-				sd[128 * q + 2 * lane] = R[q][0];
-				sd[128 * q + 2 * lane + 1] = R[q][1];
-			}
-			ld(R, c + 2);  // two rounds ahead (clamped: the values past the end are never used)
-			__syncthreads();
-			if (lane < 8) {
-				const uint64_t b0 = 64 * c;
-				if (b0 + 64 <= nfull) {
-#pragma unroll 16
-					for (int t = 0; t < 64; ++t) {
-						uint64_t a = acc + sd[8 * t + j];
-						a ^= a >> 47;
-						acc = (a ^ ck) * P32_1;
-					}
-				} else {
-					for (uint64_t t = 0; b0 + t < nb; ++t) {
-						const uint64_t x = sd[8 * t + j];
-						if (b0 + t < nfull) {
-							uint64_t a = acc + x;
-							a ^= a >> 47;
-							acc = (a ^ ck) * P32_1;
-						} else {
-							acc += x;
-						}
-					}
-				}
-			}
-			__syncthreads();
+			for (int t = 0; t < kXRing; ++t) R[t] = ld(r * kXRing + t);  // (clamped past the end: never used)
 		};
-		ld(A, 0);
-		ld(B, 1);
-		for (uint64_t c = 0; c < nround; c += 2) {
-			round(A, c);
-			if (c + 1 < nround) round(B, c + 1);
+		auto eat = [&](const uint64_t (&R)[kXRing], uint64_t r) __attribute__((always_inline)) {
+#pragma unroll
+			for (int t = 0; t < kXRing; ++t) step(r * kXRing + t, R[t]);
+		};
+		fill(ra, 0);
+		fill(rb, 1);
+		fill(rc, 2);
+		const uint64_t nround = (nbmax + kXRing - 1) / kXRing;
+		for (uint64_t r = 0; r < nround; r += 3) {
+			eat(ra, r);
+			__builtin_amdgcn_sched_barrier(0);
+			fill(ra, r + 3);
+			__builtin_amdgcn_sched_barrier(0);
+			eat(rb, r + 1);
+			__builtin_amdgcn_sched_barrier(0);
+			fill(rb, r + 4);
+			__builtin_amdgcn_sched_barrier(0);
+			eat(rc, r + 2);
+			__builtin_amdgcn_sched_barrier(0);
+			fill(rc, r + 5);
+			__builtin_amdgcn_sched_barrier(0);
 		}
 		// mergeAccs (xxhash.h:3678-3700): lanes 2k, 2k+1 -> mulfold, summed over k
-		const uint64_t gk = sat(1 + (int)j, 3, seed);  // secret + 11 + 8j
 		const uint64_t a = acc ^ gk;
 		const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)a, 1), phi = (uint32_t)__shfl_xor((int)(uint32_t)(a >> 32), 1);
-		const uint64_t b = ((uint64_t)phi << 32) | plo;
-		uint64_t m = (lane < 8 && !(j & 1)) ? (a * b ^ __umul64hi(a, b)) : 0;
+		const uint64_t bq = ((uint64_t)phi << 32) | plo;
+		uint64_t m = !(j & 1) ? (a * bq ^ __umul64hi(a, bq)) : 0;
 #pragma unroll
 		for (int o = 2; o < 8; o <<= 1) {
 			const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), o);
@@ -324,7 +335,7 @@ __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
 		h ^= h >> 37;
 		h *= 0x165667919E3779F9ull;
 		h ^= h >> 32;
-		if (lane == 0) S.out[rdf64(E.idx)] = h;
+		if (j == 0 && own) S.out[E.idx] = h;
 	}
 }
 
@@ -341,7 +352,7 @@ int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stre
 		k_xsplit_a<true><<<ga, 256, 0, stream>>>(S);
 	else
 		k_xsplit_a<false><<<ga, 256, 0, stream>>>(S);
-	k_xsplit_b<<<(unsigned)num_cus * 32, 64, 0, stream>>>(S);
+	k_xsplit_b<<<(unsigned)num_cus * 4, 64, 0, stream>>>(S);  // 8 chains per wave: 8192 long buffers at once
 	return 0;
 }
 
