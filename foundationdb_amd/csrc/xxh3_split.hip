@@ -18,9 +18,9 @@
 //            pieces per wave; the row layout of k_xxh3_rows (a 16-lane row per
 //            block: four coalesced 256-byte loads, 32x32->64 products, two DPP
 //            row rotates) writes D[b] (64 B per KiB) to the workspace.
-//   phase B  k_xsplit_b: eight long buffers per wave, eight lanes each (one
-//            accumulator per lane), the stripe sums read straight into a
-//            register ring kXRing blocks deep, one scramble per block, the merge.
+//   phase B  k_xsplit_b: one wave per long buffer: 4 KiB of stripe sums per
+//            round by LDS-DMA (the next round in flight), eight chain lanes
+//            (one accumulator each), one scramble per block, the merge.
 // The planner (xxh3_kernels.hip: k_xplan / k_xscan / k_xassign) picks the
 // long buffers, lays out the pieces and D, and takes them off the row kernel.
 #include <hip/hip_runtime.h>
@@ -243,27 +243,31 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 }
 
 // ---------------------------------------------------------------------------
-// Phase B: the chains.  Eight chains per wave: lane (c, j) = (lane / 8,
-// lane % 8) holds acc[j] of long buffer 8w + c and reads its stripe sums
-// straight into registers (the 8 lanes of a chain read 64 contiguous bytes
-// per block), kXRing blocks ahead: the sums were written by phase A and come
-// from L2 / MALL, and the ring covers their latency while the chain runs one
-// scramble per block (the only sequential part of XXH3).
+// Phase B: the chains, one wave per long buffer (64-thread workgroups,
+// grid-stride over the buffers); lane j < 8 holds acc[j].  The stripe sums
+// arrive 64 blocks (4 KiB) per round by LDS-DMA (global_load_lds: no VGPR
+// staging for the compiler to wait on), the next round in flight while the
+// chain runs; two 4 KiB buffers per wave keep every long buffer of a batch
+// resident at once.  The chain is the only sequential part of XXH3: one
+// scramble per 1 KiB block, so the batch's longest buffer sets this kernel's
+// time (about 30 ns per KiB).
 // ---------------------------------------------------------------------------
-constexpr int kXRing = 16;
-
 __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
+	__shared__ uint64_t sd[2 * 512];
 	const uint64_t nsplit = rdf64(gld64(S.sh + 0));
-	const uint32_t lane = threadIdx.x, c = lane >> 3, j = lane & 7;
+	const uint32_t lane = threadIdx.x;
+	const uint32_t j = lane & 7;
 	const uint64_t init = j == 0 ? P32_3 : j == 1 ? P64_1 : j == 2 ? P64_2 : j == 3 ? P64_3
 	                    : j == 4 ? P64_4 : j == 5 ? P32_2 : j == 6 ? P64_5 : P32_1;
-	for (uint64_t s0 = (uint64_t)blockIdx.x * 8; s0 < nsplit; s0 += (uint64_t)gridDim.x * 8) {
-		const uint64_t s = s0 + c < nsplit ? s0 + c : nsplit - 1;  // (lanes past the end repeat the last buffer, discarded)
-		const bool own = s0 + c < nsplit;
-		const XEnt E = S.ents[s];
-		const uint64_t len = E.len, seed = E.seed;
+	typedef __attribute__((address_space(1))) const void* gp;
+	typedef __attribute__((address_space(3))) void* lp;
+	for (uint64_t sidx = blockIdx.x; sidx < nsplit; sidx += gridDim.x) {
+		const XEnt E = S.ents[sidx];
+		const uint64_t len = rdf64(E.len), seed = rdf64(E.seed), idx = rdf64(E.idx);
 		const uint64_t nfull = (len - 1) >> 10, nb = nfull + 1;
-		const uint64_t* dp = S.D + 8 * E.F + j;
+		const uint8_t* base = reinterpret_cast<const uint8_t*>(S.D + 8 * rdf64(E.F));
+		const uint64_t last16 = 64 * nb - 16;  // the last 16 bytes of this buffer's stripe sums
+		const uint64_t nround = (nb + 63) >> 6;
 		const uint64_t ck = swd(16 + (int)j, seed);  // scramble key: secret + 128 + 8j
 		const uint64_t gk = sat(1 + (int)j, 3, seed);  // merge key: secret + 11 + 8j
 		const uint32_t cklo = (uint32_t)ck, ckhi = (uint32_t)(ck >> 32);
@@ -276,56 +280,47 @@ __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
 			const uint64_t m = (uint64_t)lo2 * (uint32_t)P32_1;
 			return m + ((uint64_t)(hi2 * (uint32_t)P32_1) << 32);
 		};
-		uint64_t nbmax = nb;  // the wave's longest chain (uniform trip count)
-#pragma unroll
-		for (int o = 8; o < 64; o <<= 1) {
-			const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(nbmax >> 32), o) << 32) |
-			                   (uint32_t)__shfl_xor((int)(uint32_t)nbmax, o);
-			nbmax = y > nbmax ? y : nbmax;
-		}
-		nbmax = rdf64(nbmax);
 		uint64_t acc = init;
-		auto ld = [&](uint64_t b) -> uint64_t { return gld64(dp + 8 * (b < nb ? b : nb - 1)); };
-		auto step = [&](uint64_t b, uint64_t v) __attribute__((always_inline)) {
-			const uint64_t a1 = acc + v, s1 = scr(a1);  // (selects, no branch: the loop stays unrolled)
-			acc = b < nfull ? s1 : (b == nfull ? a1 : acc);
-		};
-		// three register sets of kXRing blocks: one is consumed while the next
-		// two are in flight, then refilled (sched barriers keep the refill
-		// after the consumption: hoisted above it, the loads would need copies,
-		// and a copy of a load in flight waits for it)
-		uint64_t ra[kXRing], rb[kXRing], rc[kXRing];
-		auto fill = [&](uint64_t (&R)[kXRing], uint64_t r) __attribute__((always_inline)) {
+		// round c -> sd[(c % 2) * 512]: lane L's 16 bytes of quarter q land at
+		// 1024 q + 16 L (the wave-uniform base + lane x 16 of the DMA)
+		auto issue = [&](uint64_t c) __attribute__((always_inline)) {
+			uint64_t* dst = sd + 512 * (uint32_t)(c & 1);
 #pragma unroll
-			for (int t = 0; t < kXRing; ++t) R[t] = ld(r * kXRing + t);  // (clamped past the end: never used)
+			for (int q = 0; q < 4; ++q) {
+				const uint64_t o = 4096 * c + 1024 * q + 16 * lane;
+				__builtin_amdgcn_global_load_lds((gp)(base + (o < last16 ? o : last16)), (lp)(dst + 128 * q), 16, 0, 0);
+			}
 		};
-		auto eat = [&](const uint64_t (&R)[kXRing], uint64_t r) __attribute__((always_inline)) {
-#pragma unroll
-			for (int t = 0; t < kXRing; ++t) step(r * kXRing + t, R[t]);
-		};
-		fill(ra, 0);
-		fill(rb, 1);
-		fill(rc, 2);
-		const uint64_t nround = (nbmax + kXRing - 1) / kXRing;
-		for (uint64_t r = 0; r < nround; r += 3) {
-			eat(ra, r);
-			__builtin_amdgcn_sched_barrier(0);
-			fill(ra, r + 3);
-			__builtin_amdgcn_sched_barrier(0);
-			eat(rb, r + 1);
-			__builtin_amdgcn_sched_barrier(0);
-			fill(rb, r + 4);
-			__builtin_amdgcn_sched_barrier(0);
-			eat(rc, r + 2);
-			__builtin_amdgcn_sched_barrier(0);
-			fill(rc, r + 5);
-			__builtin_amdgcn_sched_barrier(0);
+		// the entry's loads complete here, before any DMA is in flight (a use of
+		// an ordinary load's result behind a DMA would wait for the DMA too)
+		__builtin_amdgcn_s_waitcnt(0);
+		__builtin_amdgcn_sched_barrier(0);
+		issue(0);
+		for (uint64_t c = 0; c < nround; ++c) {
+			issue(c + 1);  // (clamped: values past the end are never used)
+			__builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): round c has landed, c + 1 in flight
+			const uint64_t* r = sd + 512 * (uint32_t)(c & 1);
+			if (lane < 8) {
+				const uint64_t b0 = 64 * c;
+				if (b0 + 64 <= nfull) {
+#pragma unroll 16
+					for (int t = 0; t < 64; ++t) acc = scr(acc + r[8 * t + j]);
+				} else {
+					for (uint64_t t = 0; b0 + t < nb; ++t) {
+						const uint64_t x = r[8 * t + j];
+						acc = b0 + t < nfull ? scr(acc + x) : acc + x;
+					}
+				}
+			}
+			// the reads of round c complete before round c + 2 is issued into its buffer
+			__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
 		}
+		__builtin_amdgcn_s_waitcnt(0);  // every DMA of this buffer landed before the next one reuses the buffers
 		// mergeAccs (xxhash.h:3678-3700): lanes 2k, 2k+1 -> mulfold, summed over k
 		const uint64_t a = acc ^ gk;
 		const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)a, 1), phi = (uint32_t)__shfl_xor((int)(uint32_t)(a >> 32), 1);
 		const uint64_t bq = ((uint64_t)phi << 32) | plo;
-		uint64_t m = !(j & 1) ? (a * bq ^ __umul64hi(a, bq)) : 0;
+		uint64_t m = (lane < 8 && !(j & 1)) ? (a * bq ^ __umul64hi(a, bq)) : 0;
 #pragma unroll
 		for (int o = 2; o < 8; o <<= 1) {
 			const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), o);
@@ -335,7 +330,7 @@ __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
 		h ^= h >> 37;
 		h *= 0x165667919E3779F9ull;
 		h ^= h >> 32;
-		if (j == 0 && own) S.out[E.idx] = h;
+		if (lane == 0) S.out[idx] = h;
 	}
 }
 
@@ -352,7 +347,7 @@ int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stre
 		k_xsplit_a<true><<<ga, 256, 0, stream>>>(S);
 	else
 		k_xsplit_a<false><<<ga, 256, 0, stream>>>(S);
-	k_xsplit_b<<<(unsigned)num_cus * 4, 64, 0, stream>>>(S);  // 8 chains per wave: 8192 long buffers at once
+	k_xsplit_b<<<(unsigned)num_cus * 20, 64, 0, stream>>>(S);  // 8 KiB of LDS each: 20 per CU
 	return 0;
 }
 

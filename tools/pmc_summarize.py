@@ -91,7 +91,7 @@ def _varlen(fn):
     return f
 
 
-VARLEN_KERNELS = ("k_v7count", "k_v7prep", "k_scan", "k_varlen7", "k_bigblocks")
+VARLEN_KERNELS = ("k_v7count", "k_v7prep", "k_scan", "k_varlen7", "k_bigblocks", "k_xstream", "k_xz", "k_xfin")
 PRESETS = {
     "pages4k": ("pages4k", "pages4k", ("k_pages4k",), (1 << 20) * 4100, 1 << 20),
     "pages8k": ("pages8k", "pages8k", ("k_pages4k",), (1 << 19) * 8196, 1 << 19),

@@ -7,7 +7,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-ROUND=${ROUND:-round2}
+ROUND=${ROUND:-round3}
 R=gpurun_out/$ROUND
 P=gpurun_out/pmc
 mkdir -p $R $P
@@ -18,17 +18,20 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-me
 tail -1 $R/pytest_gpu.txt
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $R/smoke.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $R/bench_pages4k.json 2> $R/bench_pages4k.err || exit 1
-for w in pages8k zipf chunks chunks-host pages4k-host xxh3-pages4k xxh3-zipf sqlite-verify sqlite-verify-host; do
+for w in pages8k zipf chunks chunks-host pages4k-host xxh3-pages4k xxh3-zipf xxh3-chunks sqlite-verify sqlite-verify-host diskqueue-verify; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --cpu-seconds 5 > $R/bench_$w.json 2> $R/bench_$w.err || { tail -3 $R/bench_$w.err; exit 1; }
 done
 echo benches done
+# the headline's first launches in a fresh process (bench.py runs --warmup 5)
+timeout -k 10 120 python -u tools/probe_warmup.py 60 0 > $R/warmup0.json 2> $R/warmup0.err || exit 1
+timeout -k 10 120 python -u tools/probe_warmup.py 60 2000 > $R/warmup2000.json 2> $R/warmup2000.err || exit 1
 gcc -O2 -o /tmp/bench_scalar tools/bench_scalar.c -ldl && timeout -k 10 200 /tmp/bench_scalar > $R/bench_scalar.jsonl || exit 1
 grep "model name" /proc/cpuinfo | head -1 > $R/host_cpu.txt
 for f in $R/bench_*.json; do echo "$f $(cut -c1-200 $f)"; done
 exit 0
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_pages4k -o pages4k -- python bench.py --cpu-seconds 0 > $R/prof_pages4k.log 2>&1 || exit 1
-for w in pages8k zipf chunks xxh3-pages4k xxh3-zipf sqlite-verify; do
+for w in pages8k zipf chunks xxh3-pages4k xxh3-zipf xxh3-chunks sqlite-verify diskqueue-verify; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_$w -o $w -- python bench.py --workload $w --steps 20 --cpu-seconds 0 --no-verify > $R/prof_$w.log 2>&1 || exit 1
 done
 echo rocprof done
