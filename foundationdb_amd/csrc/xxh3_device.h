@@ -28,6 +28,7 @@ constexpr unsigned kWavesPerBlock = 4;
 // (phase B).  Planner output in the workspace:
 constexpr uint64_t kXSplitMin = 16384;
 constexpr uint32_t kXPieceBlocks = 64;
+constexpr uint64_t kXBig = 256;  // phase B starts the chains of this many blocks or more first
 struct XEnt {       // one long buffer
 	uint64_t F;     // its first block in the flat stripe-sum array D
 	uint64_t len, seed, idx;
@@ -39,7 +40,10 @@ struct XPiece {     // kXPieceBlocks consecutive blocks of one long buffer (fewe
 	uint64_t pad;
 };
 struct XSplit {
-	const uint64_t* sh;   // counters: [0] long buffers, [1] blocks claimed, [2] pieces
+	const uint64_t* sh;   // planner totals: [0] long buffers, [1] blocks, [2] pieces, [3] blocks per phase-A wave, [4] big entries
+	const uint64_t* astart;  // [nwa]: phase-A wave w's first piece << 6 | its first block in that piece (~0: none)
+	uint64_t nwa;            // phase-A waves the planner divided D among
+	const uint64_t* big;     // [sh[4]]: the entries of kXBig blocks or more (any order)
 	const XEnt* ents;
 	const XPiece* pcs;
 	uint64_t* D;          // 8 x u64 per block
@@ -50,6 +54,8 @@ struct XSplit {
 // flag byte per buffer).
 constexpr uint64_t kXSplitBytesPerBlock = 72;
 int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stream);
+// Waves of the phase-A launch (the planner's share of D per wave).
+uint64_t xxh3_split_waves(int num_cus);
 // Resident 256-thread blocks per CU of the main kernel (occupancy query, cached).
 int xxh3_blocks_per_cu();
 inline uint64_t xxh3_nwave(int num_cus) { return (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock; }

@@ -838,12 +838,15 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 // ---------------------------------------------------------------------------
 // Varlen planning: whole buffers per wave, balanced by bytes.  Wave w takes
 // the buffers whose start lies in [w*Q, (w+1)*Q) of the concatenated stream
-// (cost = length + 64).  With room for the split route in the workspace,
-// k_xplan also hands every buffer longer than kXSplitMin its stripe-sum
-// blocks, entry and pieces (xxh3_split.hip) by claiming them from three
-// counters (one atomic per wave and counter); a buffer whose claim does not
-// fit stays on the row kernel.  Its flag byte tells the cost scan and the row
-// kernel which buffers the split route took (their cost here drops to 64).
+// (cost = length + 64).  With room for the split route in the workspace, the
+// buffers longer than kXSplitMin take it (xxh3_split.hip) if all of their
+// stripe-sum blocks, pieces and entries fit the room (else the row kernel
+// takes the whole batch).  No counters: k_xplan writes per-tile sums, k_xscan
+// scans them (the route, the cost prefixes, the split route's totals), k_xassign
+// gives every buffer its place -- the row kernel's waves, the flag byte that
+// takes a split buffer off the row kernel (cost 64 there), the split
+// buffer's entry, its pieces in buffer order at their flat D positions, and
+// the start of every phase-A wave whose equal share of D begins inside it.
 // ---------------------------------------------------------------------------
 struct XPlanP {
 	const uint64_t* lengths;  // nullptr: fixed length
@@ -851,187 +854,252 @@ struct XPlanP {
 	const uint64_t* seeds;
 	const uint8_t* base;
 	uint64_t stride, length, count, seed;
-	uint64_t* tiles;          // [ntile + 2]: cost prefixes, total, quantum
-	uint64_t* tneed;          // [ntile]: blocks of the tile's long buffers (the host's room estimate)
-	uint64_t* sh;             // split counters (XSplit::sh): [0] long buffers, [1] blocks, [2] pieces (zeroed before)
+	uint64_t* tiles;          // [ntile + 2]: cost if split (k_xplan) -> exclusive cost prefixes, total, quantum
+	uint64_t* tneed;          // [ntile]: long blocks (k_xplan) -> exclusive prefix | kTileFits (k_xscan)
+	uint64_t* tcns;           // [ntile]: cost if not split
+	uint64_t* tpc;            // [ntile]: long pieces -> exclusive prefix
+	uint64_t* tnl;            // [ntile]: long buffers -> exclusive prefix
+	uint64_t* sh;             // split totals (XSplit::sh): [0] entries, [1] blocks, [2] pieces, [3] blocks per phase-A wave
 	uint8_t* flag;            // per buffer: 1 if the split route took it
 	uint64_t* wave_first;
-	uint64_t ntile, nwave;
+	uint64_t* astart;         // [nwa]: phase-A wave w's first piece << 6 | block within it (~0: no work)
+	uint64_t ntile, nwave, nwa;
 	XEnt* ents;
+	uint64_t* big;            // entries of kXBig blocks or more, appended (sh[4] counts them)
 	XPiece* pcs;
-	uint64_t capD;
+	uint64_t capD, capS, capP;
 	uint64_t* hneed;          // host-mapped word (may be null): blocks the batch's long buffers need
 };
+constexpr uint64_t kTileFits = 1ull << 63;
 __device__ __forceinline__ uint64_t xp_len(const XPlanP& Q, uint64_t i) { return Q.lengths ? Q.lengths[i] : Q.length; }
 __device__ __forceinline__ uint64_t xp_off(const XPlanP& Q, uint64_t i) { return Q.offsets ? Q.offsets[i] : i * Q.stride; }
 __device__ __forceinline__ uint64_t xp_blocks(uint64_t len) { return ((len - 1) >> 10) + 1; }
 __device__ __forceinline__ uint64_t xp_cost(uint64_t len, bool split) { return split ? 64 : len + 64; }
+// a split candidate (its blocks count in the stream's need whether or not there is room)
+__device__ __forceinline__ bool xp_long(uint64_t len) { return len > kXSplitMin; }
 
-// Exclusive prefix of v over the wave's active lanes and the wave's total.
-__device__ __forceinline__ uint64_t wave_excl(uint64_t v, uint64_t* tot) {
-	const int lane = threadIdx.x & 63;
-	uint64_t inc = v;
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint64_t y = __shfl_up(inc, o);
-		if (lane >= o) inc += y;
+// Inclusive prefix sum of a 64-bit value over the wave on DPP (row shifts,
+// then the row broadcasts of lanes 15 and 31; every lane active).
+__device__ __forceinline__ uint64_t dpp_incl64(uint64_t v) {
+#define XDPP_STEP(ctrl, rm)                                                                          \
+	{                                                                                                \
+		const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)v, ctrl, rm, 0xF, false);         \
+		const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(v >> 32), ctrl, rm, 0xF, false); \
+		v += ((uint64_t)hi << 32) | lo;                                                              \
 	}
-	*tot = __shfl(inc, 63);
-	return inc - v;
+	XDPP_STEP(0x111, 0xF)  // row_shr:1
+	XDPP_STEP(0x112, 0xF)  // row_shr:2
+	XDPP_STEP(0x114, 0xF)  // row_shr:4
+	XDPP_STEP(0x118, 0xF)  // row_shr:8
+	XDPP_STEP(0x142, 0xA)  // row_bcast:15 -> rows 1, 3
+	XDPP_STEP(0x143, 0xC)  // row_bcast:31 -> rows 2, 3
+#undef XDPP_STEP
+	return v;
+}
+__device__ __forceinline__ uint64_t rdlane63(uint64_t v) {
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+	return ((uint64_t)hi << 32) | lo;
 }
 
+// One workgroup per tile of 256 buffers: the tile's sums.
 __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
-	__shared__ uint64_t part[8];
+	__shared__ uint64_t part[4][5];
 	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-	const int lane = threadIdx.x & 63;
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
-	bool split = false;
-	const uint64_t need = i < Q.count && len > kXSplitMin ? xp_blocks(len) : 0;
-	if (Q.capD && __ballot(need != 0)) {  // (rare: waves holding long buffers)
-		const bool lg = i < Q.count && len > kXSplitMin;
-		const uint64_t nb = lg ? xp_blocks(len) : 0;
-		uint64_t tot;
-		const uint64_t ex = wave_excl(nb, &tot);
-		uint64_t F0 = 0;
-		if (lane == 0) F0 = atomicAdd((unsigned long long*)&Q.sh[1], (unsigned long long)tot);
-		const uint64_t F = __shfl(F0, 0) + ex;
-		split = lg && F + nb <= Q.capD;  // (a claim past the room leaves a hole, never an overlap)
-		const uint64_t np = split ? (nb + kXPieceBlocks - 1) / kXPieceBlocks : 0;
-		uint64_t tp, ts;
-		const uint64_t exp_ = wave_excl(np, &tp);
-		const uint64_t exs = wave_excl(split ? 1 : 0, &ts);
-		uint64_t P0 = 0, S0 = 0;
-		if (lane == 0 && ts) {
-			P0 = atomicAdd((unsigned long long*)&Q.sh[2], (unsigned long long)tp);
-			S0 = atomicAdd((unsigned long long*)&Q.sh[0], (unsigned long long)ts);
-		}
-		// broadcast with every lane active (a shuffle inside the branch below
-		// could read lane 0 while lane 0 is masked off)
-		const uint64_t pcb = __shfl(P0, 0), sb = __shfl(S0, 0);
-		if (split) {
-			const uint64_t pc = pcb + exp_, sidx = sb + exs;
-			const uint64_t sd = Q.seeds ? Q.seeds[i] : Q.seed;
-			Q.ents[sidx] = XEnt{F, len, sd, i};
-			const uint64_t p = reinterpret_cast<uint64_t>(Q.base) + xp_off(Q, i);
-			for (uint64_t j = 0; j < np; ++j) {
-				const uint32_t b0 = (uint32_t)(j * kXPieceBlocks);
-				const uint32_t n = (uint32_t)(nb - b0 < kXPieceBlocks ? nb - b0 : kXPieceBlocks);
-				Q.pcs[pc + j] = XPiece{p, len, F + b0, sd, b0, n, 0};
-			}
-		}
-	}
-	if (Q.capD && i < Q.count) Q.flag[i] = split ? 1 : 0;
-	uint64_t v = i < Q.count ? xp_cost(len, split) : 0;  // +64: per-buffer cost floor
-	uint64_t nd = need;
-	for (int o = 32; o > 0; o >>= 1) {
-		v += __shfl_xor(v, o);
-		nd += __shfl_xor(nd, o);
-	}
-	if (lane == 0) {
-		part[threadIdx.x >> 6] = v;
-		part[4 + (threadIdx.x >> 6)] = nd;
-	}
+	const bool lg = i < Q.count && xp_long(len);
+	const uint64_t nb = lg ? xp_blocks(len) : 0;
+	uint64_t v[5] = {i < Q.count ? xp_cost(len, lg) : 0, i < Q.count ? len + 64 : 0, nb,
+	                 (nb + kXPieceBlocks - 1) / kXPieceBlocks, lg ? 1u : 0u};
+#pragma unroll
+	for (int q = 0; q < 5; ++q) v[q] = rdlane63(dpp_incl64(v[q]));
+	if (lane == 0)
+#pragma unroll
+		for (int q = 0; q < 5; ++q) part[wv][q] = v[q];
 	__syncthreads();
-	if (threadIdx.x == 0) {
-		Q.tiles[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
-		Q.tneed[blockIdx.x] = part[4] + part[5] + part[6] + part[7];
+	if (threadIdx.x < 5) {
+		const int q = threadIdx.x;
+		const uint64_t s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
+		uint64_t* dst = q == 0 ? Q.tiles : q == 1 ? Q.tcns : q == 2 ? Q.tneed : q == 3 ? Q.tpc : Q.tnl;
+		dst[blockIdx.x] = s;
 	}
 }
 
-// Single workgroup: in-place exclusive scan of the tile sums; tiles[ntile] =
-// total cost, tiles[ntile + 1] = quantum Q = ceil(total / nwave).
+// Single workgroup.  The split route takes every split candidate or none:
+// all of them if their blocks, pieces and entries fit the room (the library
+// sizes the room from the stream's last need; the _ws form's caller sizes it
+// with xxh3_gpu_varlen_workspace_bytes_for), else the row kernel takes the
+// whole batch.  In place: the exclusive prefixes of the routed tile costs,
+// tiles[ntile] = total cost, tiles[ntile + 1] = quantum Q = ceil(total /
+// nwave), and (routed) the prefixes of the blocks, pieces and entries, the
+// route flag in tneed; the split route's totals in sh[]; every phase-A
+// wave's start set to "no work" (k_xassign fills in the waves that have some).
 __global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
-	__shared__ uint64_t wsum[16];
-	__shared__ uint64_t carry_s;
+	__shared__ uint64_t red[4][16];
+	__shared__ uint64_t carry_s[4];
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
 	const uint64_t ntile = Q.ntile;
 	uint64_t* tiles = Q.tiles;
-	__shared__ uint64_t nsum[16];
-	if (t == 0) carry_s = 0;
-	uint64_t nd = 0;  // the batch's long blocks, for the host (room for the next batch)
-	if (Q.hneed)
-		for (uint64_t k = t; k < ntile; k += 1024) nd += Q.tneed[k];
+	for (uint64_t w = t; w < Q.nwa; w += 1024) Q.astart[w] = ~0ull;
+	uint64_t a[3] = {0, 0, 0};
+	for (uint64_t k = t; k < ntile; k += 1024) {
+		a[0] += Q.tneed[k];
+		a[1] += Q.tpc[k];
+		a[2] += Q.tnl[k];
+	}
+#pragma unroll
+	for (int q = 0; q < 3; ++q) {
+		const uint64_t s = rdlane63(dpp_incl64(a[q]));
+		if (lane == 0) red[q][wv] = s;
+	}
+	if (t < 4) carry_s[t] = 0;
 	__syncthreads();
+	uint64_t tot[3] = {0, 0, 0};
+	for (uint32_t u = 0; u < 16; ++u)
+#pragma unroll
+		for (int q = 0; q < 3; ++q) tot[q] += red[q][u];
+	const bool fits = tot[0] == 0 || (Q.capD && tot[0] <= Q.capD && tot[1] <= Q.capP && tot[2] <= Q.capS);
+	const bool split = fits && tot[0] != 0;
+	__syncthreads();  // (red is reused below)
 	for (uint64_t c0 = 0; c0 < ntile; c0 += 1024) {
 		const uint64_t k = c0 + t;
-		const uint64_t x = k < ntile ? tiles[k] : 0;
-		uint64_t inc = x;
-		for (int o = 1; o < 64; o <<= 1) {
-			const uint64_t y = __shfl_up(inc, o);
-			if ((int)lane >= o) inc += y;
+		const bool in = k < ntile;
+		uint64_t x[4] = {in ? (fits ? tiles[k] : Q.tcns[k]) : 0, 0, 0, 0};
+		if (split && in) {
+			x[1] = Q.tneed[k];
+			x[2] = Q.tpc[k];
+			x[3] = Q.tnl[k];
 		}
-		if (lane == 63) wsum[wv] = inc;
+		uint64_t inc[4];
+		inc[0] = dpp_incl64(x[0]);
+		if (lane == 63) red[0][wv] = inc[0];
+		if (split) {
+#pragma unroll
+			for (int q = 1; q < 4; ++q) {
+				inc[q] = dpp_incl64(x[q]);
+				if (lane == 63) red[q][wv] = inc[q];
+			}
+		}
 		__syncthreads();
-		uint64_t wb = 0;
-		for (uint32_t q = 0; q < wv; ++q) wb += wsum[q];
-		const uint64_t carry = carry_s;
-		if (k < ntile) tiles[k] = carry + wb + inc - x;
+		uint64_t ex[4];
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			uint64_t wb = carry_s[q];
+			if (q == 0 || split)
+				for (uint32_t u = 0; u < wv; ++u) wb += red[q][u];
+			ex[q] = wb + ((q == 0 || split) ? inc[q] - x[q] : 0);
+		}
+		if (in) {
+			tiles[k] = ex[0];
+			Q.tneed[k] = ex[1] | (split ? kTileFits : 0);
+			Q.tpc[k] = ex[2];
+			Q.tnl[k] = ex[3];
+		}
 		__syncthreads();
-		if (t == 1023) carry_s = carry + wb + inc;
+		if (t == 1023)
+#pragma unroll
+			for (int q = 0; q < 4; ++q) carry_s[q] = ex[q] + x[q];
 		__syncthreads();
 	}
-	if (Q.hneed) {
-		for (int o = 32; o > 0; o >>= 1) nd += __shfl_xor(nd, o);
-		if (lane == 0) nsum[wv] = nd;
-	}
-	__syncthreads();
 	if (t == 0) {
-		const uint64_t total = carry_s;
+		const uint64_t total = carry_s[0];
 		tiles[ntile] = total;
 		tiles[ntile + 1] = (total + Q.nwave - 1) / Q.nwave;
-		if (Q.hneed) {
-			uint64_t a = 0;
-			for (int q = 0; q < 16; ++q) a += nsum[q];
-			*(volatile uint64_t*)Q.hneed = a;
-		}
+		const uint64_t tb = split ? tot[0] : 0;
+		Q.sh[0] = split ? tot[2] : 0;
+		Q.sh[1] = tb;
+		Q.sh[2] = split ? tot[1] : 0;
+		Q.sh[3] = Q.nwa ? (tb + Q.nwa - 1) / Q.nwa : 0;
+		Q.sh[4] = 0;
+		if (Q.hneed) *(volatile uint64_t*)Q.hneed = tot[0];  // every split candidate's blocks, routed or not
 	}
 }
 
 // One workgroup per tile of 256 buffers: buffer i (cost c_i, start s_i) is
 // the first buffer of every wave w with s_{i-1} < w*Q <= s_i; waves past
-// the last buffer get `count`.
+// the last buffer get `count`.  A split buffer writes its entry, its pieces
+// and the starts of the phase-A waves whose share begins in its blocks.
 __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
-	__shared__ uint64_t wsum[4];
+	__shared__ uint64_t wsum[4][4];
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
 	const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
-	auto cost_of = [&](uint64_t b) -> uint64_t { return xp_cost(xp_len(Q, b), Q.capD && Q.flag[b]); };
-	const uint64_t cost = i < Q.count ? cost_of(i) : 0;
-	uint64_t inc = cost;
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint64_t y = __shfl_up(inc, o);
-		if ((int)lane >= o) inc += y;
+	const bool fit = (Q.tneed[blockIdx.x] & kTileFits) != 0;
+	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
+	const bool split = i < Q.count && fit && xp_long(len);
+	if (Q.capD && i < Q.count) Q.flag[i] = split ? 1 : 0;
+	const uint64_t cost = i < Q.count ? xp_cost(len, split) : 0;
+	const uint64_t nb = split ? xp_blocks(len) : 0;
+	const uint64_t np = (nb + kXPieceBlocks - 1) / kXPieceBlocks;
+	uint64_t x[4] = {cost, nb, np, split ? 1u : 0u}, ex[4];
+#pragma unroll
+	for (int q = 0; q < 4; ++q) {
+		const uint64_t inc = dpp_incl64(x[q]);
+		if (lane == 63) wsum[q][wv] = inc;
+		ex[q] = inc - x[q];
 	}
-	if (lane == 63) wsum[wv] = inc;
 	__syncthreads();
-	uint64_t wb = 0;
-	for (uint32_t q = 0; q < wv; ++q) wb += wsum[q];
+#pragma unroll
+	for (int q = 0; q < 4; ++q)
+		for (uint32_t u = 0; u < wv; ++u) ex[q] += wsum[q][u];
 	const uint64_t q = Q.tiles[Q.ntile + 1];
-	const uint64_t start = Q.tiles[blockIdx.x] + wb + inc - cost;
+	const uint64_t start = Q.tiles[blockIdx.x] + ex[0];
 	if (i < Q.count) {
 		// waves w with s_{i-1} < w*q <= s_i, i.e. [floor(s_{i-1}/q) + 1, floor(s_i/q)];
 		// buffer 0 takes w = 0
-		const uint64_t prev = i == 0 ? 0 : start - cost_of(i - 1);
+		uint64_t prev = 0;
+		if (i != 0) {
+			const uint64_t lp = xp_len(Q, i - 1);
+			const bool fp = (Q.tneed[(i - 1) >> 8] & kTileFits) != 0;
+			prev = start - xp_cost(lp, fp && xp_long(lp));
+		}
 		const uint64_t w_lo = i == 0 ? 0 : prev / q + 1;
 		const uint64_t w_hi = start / q;
 		for (uint64_t w = w_lo; w <= w_hi && w < Q.nwave; ++w) Q.wave_first[w] = i;
 		if (i + 1 == Q.count)  // waves whose first byte lies past the last buffer's start: none
 			for (uint64_t w = start / q + 1; w <= Q.nwave; ++w) Q.wave_first[w] = Q.count;
 	}
+	if (split) {
+		const uint64_t F = (Q.tneed[blockIdx.x] & ~kTileFits) + ex[1];
+		const uint64_t pc = Q.tpc[blockIdx.x] + ex[2];
+		const uint64_t sidx = Q.tnl[blockIdx.x] + ex[3];
+		const uint64_t sd = Q.seeds ? Q.seeds[i] : Q.seed;
+		Q.ents[sidx] = XEnt{F, len, sd, i};
+		if (nb >= kXBig) Q.big[atomicAdd((unsigned long long*)&Q.sh[4], 1ull)] = sidx;
+		const uint64_t p = reinterpret_cast<uint64_t>(Q.base) + xp_off(Q, i);
+		for (uint64_t j = 0; j < np; ++j) {
+			const uint32_t b0 = (uint32_t)(j * kXPieceBlocks);
+			const uint32_t n = (uint32_t)(nb - b0 < kXPieceBlocks ? nb - b0 : kXPieceBlocks);
+			Q.pcs[pc + j] = XPiece{p, len, F + b0, sd, b0, n, 0};
+		}
+		// phase-A waves whose share [w*pb, ...) of D begins in [F, F + nb)
+		const uint64_t pb = Q.sh[3];  // (> 0: this buffer's blocks are in the total)
+		for (uint64_t w = (F + pb - 1) / pb; w * pb < F + nb && w < Q.nwa; ++w) {
+			const uint64_t off = w * pb - F;
+			Q.astart[w] = ((pc + off / kXPieceBlocks) << 6) | (off % kXPieceBlocks);
+		}
+	}
 }
 
 // Workspace of the varlen path: the planner arrays, then (given more room)
 // the split route's flags, entries, pieces and stripe sums.
 struct XLayout {
-	uint64_t tiles, tneed, wave_first, sh, flag, ents, pcs, D, base;
+	uint64_t tiles, tneed, tcns, tpc, tnl, wave_first, astart, sh, flag, ents, big, pcs, D, base;
 	uint64_t capD, capS, capP;
 };
 static uint64_t al64(uint64_t x) { return (x + 63) & ~uint64_t(63); }
+// nwave: the row kernel's waves (phase A has at most as many, xxh3_split_waves)
 static XLayout xlayout(uint64_t count, uint64_t nwave, uint64_t ws_bytes) {
 	const uint64_t ntile = (count + 255) / 256;
 	XLayout L{};
 	L.tiles = 0;
 	L.tneed = al64(8 * (ntile + 2));
-	L.wave_first = al64(L.tneed + 8 * ntile);
-	L.sh = al64(L.wave_first + 8 * (nwave + 1) + 64);
+	L.tcns = al64(L.tneed + 8 * ntile);
+	L.tpc = al64(L.tcns + 8 * ntile);
+	L.tnl = al64(L.tpc + 8 * ntile);
+	L.wave_first = al64(L.tnl + 8 * ntile);
+	L.astart = al64(L.wave_first + 8 * (nwave + 1) + 64);
+	L.sh = al64(L.astart + 16 * nwave);  // phase A: up to twice the row kernel's waves
 	L.base = L.sh + 64;
 	// split room: flags (1 B per buffer), then per block of capacity 72 B
 	const uint64_t fl = al64(count);
@@ -1042,7 +1110,8 @@ static XLayout xlayout(uint64_t count, uint64_t nwave, uint64_t ws_bytes) {
 	L.capP = capD ? capD / kXPieceBlocks + L.capS : 0;
 	L.flag = L.base;
 	L.ents = L.flag + fl;
-	L.pcs = al64(L.ents + sizeof(XEnt) * L.capS);
+	L.big = al64(L.ents + sizeof(XEnt) * L.capS);
+	L.pcs = al64(L.big + 8 * L.capS);
 	L.D = al64(L.pcs + sizeof(XPiece) * L.capP);
 	return L;
 }
@@ -1095,23 +1164,34 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		Q.seed = P.seed;
 		Q.tiles = reinterpret_cast<uint64_t*>(w8 + L.tiles);
 		Q.tneed = reinterpret_cast<uint64_t*>(w8 + L.tneed);
+		Q.tcns = reinterpret_cast<uint64_t*>(w8 + L.tcns);
+		Q.tpc = reinterpret_cast<uint64_t*>(w8 + L.tpc);
+		Q.tnl = reinterpret_cast<uint64_t*>(w8 + L.tnl);
 		Q.sh = reinterpret_cast<uint64_t*>(w8 + L.sh);
 		Q.flag = w8 + L.flag;
 		Q.wave_first = reinterpret_cast<uint64_t*>(w8 + L.wave_first);
+		Q.astart = reinterpret_cast<uint64_t*>(w8 + L.astart);
 		Q.ntile = ntile;
 		Q.nwave = nwave;
+		Q.nwa = L.capD ? xxh3_split_waves(num_cus) : 0;
+		if (Q.nwa > 2 * nwave) Q.nwa = 2 * nwave;  // (the layout holds 2 nwave starts)
 		Q.ents = reinterpret_cast<XEnt*>(w8 + L.ents);
+		Q.big = reinterpret_cast<uint64_t*>(w8 + L.big);
 		Q.pcs = reinterpret_cast<XPiece*>(w8 + L.pcs);
 		Q.capD = L.capD;
+		Q.capS = L.capS;
+		Q.capP = L.capP;
 		Q.hneed = P.hneed;
-		if (L.capD && hipMemsetAsync(Q.sh, 0, 64, stream) != hipSuccess) return -1;
 		k_xplan<<<(unsigned)ntile, 256, 0, stream>>>(Q);
 		k_xscan<<<1, 1024, 0, stream>>>(Q);
 		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(Q);
 		if (L.capD) {
 			XSplit S{};
 			S.sh = Q.sh;
+			S.astart = Q.astart;
+			S.nwa = Q.nwa;
 			S.ents = Q.ents;
+			S.big = Q.big;
 			S.pcs = Q.pcs;
 			S.D = reinterpret_cast<uint64_t*>(w8 + L.D);
 			S.out = P.out;

@@ -14,15 +14,16 @@
 // (tests/xxh3_split_model.py restates this and checks it against the oracle.)
 //
 //   phase A  k_xsplit_a: every block of every long buffer as one flat stream
-//            of PIECES (64 consecutive blocks of one buffer), static ranges of
-//            pieces per wave; the row layout of k_xxh3_rows (a 16-lane row per
+//            (D order, PIECES of 64 consecutive blocks of one buffer carry the
+//            metadata), an equal share of blocks per wave; the row layout of k_xxh3_rows (a 16-lane row per
 //            block: four coalesced 256-byte loads, 32x32->64 products, two DPP
 //            row rotates) writes D[b] (64 B per KiB) to the workspace.
 //   phase B  k_xsplit_b: one wave per long buffer: 4 KiB of stripe sums per
 //            round by LDS-DMA (the next round in flight), eight chain lanes
 //            (one accumulator each), one scramble per block, the merge.
 // The planner (xxh3_kernels.hip: k_xplan / k_xscan / k_xassign) picks the
-// long buffers, lays out the pieces and D, and takes them off the row kernel.
+// long buffers, lays out the pieces and D in buffer order, divides D among
+// phase A's waves, and takes the long buffers off the row kernel.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -79,17 +80,38 @@ typedef __attribute__((address_space(1))) u64x2 gw_u64x2;
 typedef __attribute__((address_space(1))) const uint64_t g_u64;
 
 __device__ __forceinline__ uint64_t gld64(const uint64_t* p) { return *((g_u64*)reinterpret_cast<uintptr_t>(p)); }
+// A piece's metadata through the scalar cache (constant address space, a
+// wave-uniform address: s_load, counted by lgkmcnt): as a vector load it
+// would sit in the data loads' in-order vmcnt queue, and every piece change
+// would wait for the blocks in flight.  The planner wrote the pieces in an
+// earlier launch; nothing in this one writes them.
+typedef __attribute__((address_space(4))) const uint64_t c_u64;
+__device__ __forceinline__ XPiece ld_piece(const XPiece* pcs, uint64_t i) {
+	static_assert(sizeof(XPiece) == 48, "six words");
+	const c_u64* q = (const c_u64*)reinterpret_cast<uintptr_t>(pcs + i);
+	XPiece r;
+	r.p = q[0];
+	r.len = q[1];
+	r.d = q[2];
+	r.seed = q[3];
+	const uint64_t w = q[4];
+	r.b0 = (uint32_t)w;
+	r.nb = (uint32_t)(w >> 32);
+	r.pad = 0;
+	return r;
+}
 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Phase A: stripe sums, pieces in static ranges per wave.
+// Phase A: stripe sums, an equal share of D's blocks per wave (pieces of 64
+// blocks per wave measured 13 % of imbalance on the chunks batch: ~6 pieces
+// per wave, a third of them partial).
 // Lane (r, g, k) = (lane / 16, (lane % 16) / 4, lane % 4): row r takes block
 // b + r of a STEP (four consecutive blocks of one piece), stripes g, g+4,
 // g+8, g+12 for accumulator pair k.  The row sums close with two DPP row
 // rotates, after which every lane of a row holds its pair's sums; a step's
-// sums stay in the lanes with g == step % 4 and leave every four steps as one
-// 16-byte store per lane (1 KiB per wave).
+// sums stay in the lanes with g == step % 4 and leave in bursts (kXGroup).
 // ---------------------------------------------------------------------------
 struct AStep {
 	uint64_t v[4][2];
@@ -103,33 +125,40 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 	if (npc == 0) return;  // no long buffer this batch
 	const int lane = threadIdx.x & 63;
 	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
-	const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
 	const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	const uint64_t per = (npc + nwave - 1) / nwave;
-	const uint64_t pa = w * per < npc ? w * per : npc;
-	const uint64_t pe = pa + per < npc ? pa + per : npc;
-	if (pa >= pe) return;
+	if (w >= S.nwa) return;
+	// this wave's share of D: blocks [w*pb, min((w+1)*pb, total)), starting at
+	// block `a & 63` of piece `a >> 6` (the planner, k_xassign)
+	const uint64_t a = rdf64(gld64(S.astart + w));
+	if (a == ~0ull) return;
+	const uint64_t tb = rdf64(gld64(S.sh + 1)), pb = rdf64(gld64(S.sh + 3));
+	const uint64_t fb1 = (w + 1) * pb < tb ? (w + 1) * pb : tb;
 	const XPiece* __restrict__ pcs = S.pcs;
-	// load cursor: piece lq (metadata in Lm), step lst; the next piece's
-	// metadata (scalar loads, lgkmcnt: off the data loads' vmcnt queue)
-	uint64_t lq = pa;
-	uint32_t lst = 0;
-	XPiece Lm = pcs[rdf64(lq)];
-	XPiece Nm = pcs[rdf64(lq + 1 < pe ? lq + 1 : lq)];
-	const uint64_t idle_p = Lm.p;  // an idle step reads the range's first block again (discarded)
+	// load cursor: piece lq (metadata in Lm) at block lpos of it, rem blocks of
+	// the share left; the next piece's metadata (scalar loads, lgkmcnt: off the
+	// data loads' vmcnt queue)
+	uint64_t lq = a >> 6, rem = fb1 - w * pb;
+	uint32_t lpos = (uint32_t)(a & 63);
+	XPiece Lm = ld_piece(pcs, rdf64(lq));
+	XPiece Nm = ld_piece(pcs, rdf64(lq + 1 < npc ? lq + 1 : lq));
+	const uint64_t idle_p = Lm.p;  // an idle step reads the share's first block again (discarded)
 	auto load = [&](AStep& St) __attribute__((always_inline)) {
-		if (lq < pe) {
+		if (rem != 0) {
 			St.p = Lm.p;
 			St.len = Lm.len;
 			St.seed = Lm.seed;
-			St.b = Lm.b0 + 4 * lst;
-			St.d = Lm.d + 4 * lst;
-			St.nrows = Lm.nb - 4 * lst < 4 ? Lm.nb - 4 * lst : 4;
-			if (4 * ++lst >= Lm.nb) {
+			St.b = Lm.b0 + lpos;
+			St.d = Lm.d + lpos;
+			uint32_t n = Lm.nb - lpos < 4 ? Lm.nb - lpos : 4;
+			n = rem < n ? (uint32_t)rem : n;
+			St.nrows = n;
+			lpos += n;
+			rem -= n;
+			if (lpos >= Lm.nb && rem != 0) {
 				++lq;
-				lst = 0;
+				lpos = 0;
 				Lm = Nm;
-				Nm = pcs[rdf64(lq + 1 < pe ? lq + 1 : lq)];
+				Nm = ld_piece(pcs, rdf64(lq + 1 < npc ? lq + 1 : lq));
 			}
 		} else {
 			St.p = idle_p;
@@ -166,14 +195,29 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 		l1 = sat(16 + 2 * k, 1, sd);
 	};
 	keys(kseed);
-	// saved sums: lane (r, g, k) keeps step (g mod 4)'s sums of row r, pair k
-	uint64_t e0 = 0, e1 = 0, ei = 0;
-	bool ev = false;
+	// saved sums: lane (r, g, k) keeps the sums of row r, pair k of steps
+	// g, g + 4, g + 8, g + 12 of a group of kXGroup steps, which leave together
+	// as kXGroup / 4 16-byte stores per lane.  A store holds up the next wait on
+	// the data loads issued after it (vmcnt counts stores and loads in issue
+	// order) until it has reached memory, which under the read stream takes
+	// several us: one store per four steps cost phase A ~25 % (212 -> 162 us
+	// without the stores on the chunks batch), so they go out in bursts.
+	constexpr uint32_t kXGroup = 16;
+	uint64_t e0[kXGroup / 4], e1[kXGroup / 4], ei[kXGroup / 4];
+	bool ev[kXGroup / 4];
+#pragma unroll
+	for (uint32_t j = 0; j < kXGroup / 4; ++j) {
+		e0[j] = e1[j] = ei[j] = 0;
+		ev[j] = false;
+	}
 	uint32_t slot = 0;  // steps saved since the last store (uniform)
 	uint64_t* __restrict__ D = S.D;
 	auto flush = [&]() __attribute__((always_inline)) {
-		if (ev) *((gw_u64x2*)reinterpret_cast<uintptr_t>(D + 8 * ei + 2 * k)) = u64x2{e0, e1};
-		ev = false;
+#pragma unroll
+		for (uint32_t j = 0; j < kXGroup / 4; ++j) {
+			if (ev[j]) *((gw_u64x2*)reinterpret_cast<uintptr_t>(D + 8 * ei[j] + 2 * k)) = u64x2{e0[j], e1[j]};
+			ev[j] = false;
+		}
 	};
 	auto compute = [&](const AStep& St) __attribute__((always_inline)) {
 		if (St.nrows == 0) return;
@@ -203,13 +247,15 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 		add_dpp<0x124>(lo1, hi1);
 		add_dpp<0x128>(lo0, hi0);  // row_ror:8
 		add_dpp<0x128>(lo1, hi1);
-		if ((uint32_t)g == slot) {
-			e0 = ((uint64_t)hi0 << 32) | lo0;
-			e1 = ((uint64_t)hi1 << 32) | lo1;
-			ei = St.d + r;
-			ev = (uint32_t)r < St.nrows;
-		}
-		if (++slot == 4) {
+#pragma unroll
+		for (uint32_t j = 0; j < kXGroup / 4; ++j)
+			if ((slot >> 2) == j && (uint32_t)g == (slot & 3)) {
+				e0[j] = ((uint64_t)hi0 << 32) | lo0;
+				e1[j] = ((uint64_t)hi1 << 32) | lo1;
+				ei[j] = St.d + r;
+				ev[j] = (uint32_t)r < St.nrows;
+			}
+		if (++slot == kXGroup) {
 			flush();
 			slot = 0;
 		}
@@ -243,25 +289,28 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 }
 
 // ---------------------------------------------------------------------------
-// Phase B: the chains, one wave per long buffer (64-thread workgroups,
-// grid-stride over the buffers); lane j < 8 holds acc[j].  The stripe sums
+// Phase B: the chains, one wave per long buffer (64-thread workgroups, two
+// per SIMD: more waves per SIMD slow every chain down, and the longest one
+// sets the time); lane j < 8 holds acc[j].  The stripe sums
 // arrive 64 blocks (4 KiB) per round by LDS-DMA (global_load_lds: no VGPR
-// staging for the compiler to wait on), the next round in flight while the
-// chain runs; two 4 KiB buffers per wave keep every long buffer of a batch
-// resident at once.  The chain is the only sequential part of XXH3: one
-// scramble per 1 KiB block, so the batch's longest buffer sets this kernel's
-// time (about 30 ns per KiB).
+// staging for the compiler to wait on) into a ring of four rounds, three in
+// flight while the chain runs (with one in flight the chain waited on every
+// round: a round's 64 scrambles take less than the DMA's latency under load).
+// The chain is the only sequential part of XXH3: one scramble per 1 KiB
+// block, so the batch's longest buffer sets this kernel's time.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
-	__shared__ uint64_t sd[2 * 512];
+	constexpr uint32_t NR = 4;  // rounds of 4 KiB in the LDS ring: three in flight while one is chained
+	__shared__ uint64_t sd[NR * 512];
 	const uint64_t nsplit = rdf64(gld64(S.sh + 0));
+	const uint64_t nbig = rdf64(gld64(S.sh + 4));
 	const uint32_t lane = threadIdx.x;
 	const uint32_t j = lane & 7;
 	const uint64_t init = j == 0 ? P32_3 : j == 1 ? P64_1 : j == 2 ? P64_2 : j == 3 ? P64_3
 	                    : j == 4 ? P64_4 : j == 5 ? P32_2 : j == 6 ? P64_5 : P32_1;
 	typedef __attribute__((address_space(1))) const void* gp;
 	typedef __attribute__((address_space(3))) void* lp;
-	for (uint64_t sidx = blockIdx.x; sidx < nsplit; sidx += gridDim.x) {
+	auto chain = [&](uint64_t sidx) __attribute__((always_inline)) {
 		const XEnt E = S.ents[sidx];
 		const uint64_t len = rdf64(E.len), seed = rdf64(E.seed), idx = rdf64(E.idx);
 		const uint64_t nfull = (len - 1) >> 10, nb = nfull + 1;
@@ -276,15 +325,15 @@ __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
 		// half): shift, xor3, one 32x32->64 mad and one add per block
 		auto scr = [&](uint64_t a) __attribute__((always_inline)) -> uint64_t {
 			const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
-			const uint32_t lo2 = lo ^ (hi >> 15) ^ cklo, hi2 = hi ^ ckhi;
+			const uint32_t lo2 = __builtin_amdgcn_bitop3_b32(lo, hi >> 15, cklo, 0x96);  // xor3
 			const uint64_t m = (uint64_t)lo2 * (uint32_t)P32_1;
-			return m + ((uint64_t)(hi2 * (uint32_t)P32_1) << 32);
+			return m + ((uint64_t)((hi ^ ckhi) * (uint32_t)P32_1) << 32);
 		};
 		uint64_t acc = init;
-		// round c -> sd[(c % 2) * 512]: lane L's 16 bytes of quarter q land at
+		// round c -> sd[(c % NR) * 512]: lane L's 16 bytes of quarter q land at
 		// 1024 q + 16 L (the wave-uniform base + lane x 16 of the DMA)
 		auto issue = [&](uint64_t c) __attribute__((always_inline)) {
-			uint64_t* dst = sd + 512 * (uint32_t)(c & 1);
+			uint64_t* dst = sd + 512 * (uint32_t)(c % NR);
 #pragma unroll
 			for (int q = 0; q < 4; ++q) {
 				const uint64_t o = 4096 * c + 1024 * q + 16 * lane;
@@ -295,11 +344,12 @@ __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
 		// an ordinary load's result behind a DMA would wait for the DMA too)
 		__builtin_amdgcn_s_waitcnt(0);
 		__builtin_amdgcn_sched_barrier(0);
-		issue(0);
+#pragma unroll
+		for (uint32_t c = 0; c + 1 < NR; ++c) issue(c);
 		for (uint64_t c = 0; c < nround; ++c) {
-			issue(c + 1);  // (clamped: values past the end are never used)
-			__builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): round c has landed, c + 1 in flight
-			const uint64_t* r = sd + 512 * (uint32_t)(c & 1);
+			issue(c + NR - 1);  // into round c - 1's slot (read); clamped: values past the end are never used
+			__builtin_amdgcn_s_waitcnt(0x0F7C);  // vmcnt(12): round c has landed, c + 1 .. c + 3 in flight
+			const uint64_t* r = sd + 512 * (uint32_t)(c % NR);
 			if (lane < 8) {
 				const uint64_t b0 = 64 * c;
 				if (b0 + 64 <= nfull) {
@@ -312,7 +362,7 @@ __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
 					}
 				}
 			}
-			// the reads of round c complete before round c + 2 is issued into its buffer
+			// the reads of round c complete before round c + NR is issued into its slot
 			__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
 		}
 		__builtin_amdgcn_s_waitcnt(0);  // every DMA of this buffer landed before the next one reuses the buffers
@@ -331,23 +381,44 @@ __global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
 		h *= 0x165667919E3779F9ull;
 		h ^= h >> 32;
 		if (lane == 0) S.out[idx] = h;
+	};
+	// The batch's longest chains set this kernel's time, so they start first,
+	// each on a wave of its own (the planner's list of buffers of kXBig blocks
+	// or more); the other buffers go to the waves without one, in entry order.
+	const uint64_t W = gridDim.x, w = blockIdx.x;
+	for (uint64_t q = w; q < nbig; q += W) chain(rdf64(gld64(S.big + q)));
+	const bool apart = nbig < W && W - nbig >= W / 4;  // enough waves without a long chain
+	const uint64_t w0 = apart ? nbig : 0, nw = apart ? W - nbig : W;
+	if (w < w0) return;
+	for (uint64_t e = w - w0; e < nsplit; e += nw) {
+		const uint64_t len = rdf64(gld64(&S.ents[e].len));
+		if (((len - 1) >> 10) + 1 < kXBig) chain(e);
 	}
 }
 
-int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stream) {
+static int xsplit_a_bpc() {
 	static const int bpc = [] {
 		int a = 0, b = 0;
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xsplit_a<false>, 256, 0) != hipSuccess) a = 3;
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_xsplit_a<true>, 256, 0) != hipSuccess) b = 3;
 		a = a < b ? a : b;
+		const int c = 2 * xxh3_blocks_per_cu();  // (the workspace holds twice the row kernel's wave count of starts)
+		a = a < c ? a : c;
 		return a < 1 ? 1 : a;
 	}();
-	const unsigned ga = (unsigned)((uint64_t)num_cus * bpc);
+	return bpc;
+}
+
+uint64_t xxh3_split_waves(int num_cus) { return (uint64_t)num_cus * xsplit_a_bpc() * 4; }
+
+int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stream) {
+	const unsigned ga = (unsigned)((S.nwa + 3) / 4);
+	if (ga == 0) return 0;
 	if (seeds)
 		k_xsplit_a<true><<<ga, 256, 0, stream>>>(S);
 	else
 		k_xsplit_a<false><<<ga, 256, 0, stream>>>(S);
-	k_xsplit_b<<<(unsigned)num_cus * 20, 64, 0, stream>>>(S);  // 8 KiB of LDS each: 20 per CU
+	k_xsplit_b<<<(unsigned)num_cus * 8, 64, 0, stream>>>(S);  // two chains per SIMD: ~full speed each
 	return 0;
 }
 

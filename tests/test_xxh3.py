@@ -295,6 +295,9 @@ def test_gpu_xxh3_split_route_long_buffers(cuda):
     ws = torch.empty(X.varlen_workspace_bytes(lens.size, int(lens.sum())), dtype=torch.uint8, device=cuda)
     assert np.array_equal(host(X.batch_varlen(d, o, l, workspace=ws)), want)
     assert np.array_equal(host(X.batch_varlen(d, o, l, seeds=sd, workspace=ws)), want_s)
+    # room for a third of the long blocks: the row kernel takes every buffer
+    ws3 = torch.empty(X.varlen_workspace_bytes(lens.size, int(lens.sum()) // 3), dtype=torch.uint8, device=cuda)
+    assert np.array_equal(host(X.batch_varlen(d, o, l, seeds=sd, workspace=ws3)), want_s)
     s = torch.cuda.Stream(cuda)
     with torch.cuda.stream(s):
         for _ in range(3):

@@ -12,20 +12,24 @@ big = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
 F.fill_splitmix64(big, 0x5EED)
 out = torch.empty(n, dtype=torch.uint32, device=dev)
 out64 = torch.empty(n, dtype=torch.uint64, device=dev)
-VARLEN = ("chunks", "zipf", "v4096", "v1024")
+VARLEN = ("chunks", "zipf", "v4096", "v1024", "xchunks", "xzipf")
 if mode in VARLEN:
     import numpy as np
     import bench_workloads as W
-    lens = {"chunks": W.chunk_lengths, "zipf": W.zipf_lengths, "v4096": lambda: np.full(1 << 18, 4096),
+    lens = {"chunks": W.chunk_lengths, "zipf": W.zipf_lengths, "xchunks": W.chunk_lengths, "xzipf": W.zipf_lengths, "v4096": lambda: np.full(1 << 18, 4096),
             "v1024": lambda: np.full(1 << 20, 1024)}[mode]().astype(np.int64)
-    al = {"chunks": 4096, "zipf": 256, "v4096": 4096, "v1024": 1024}[mode]
+    al = {"chunks": 4096, "zipf": 256, "v4096": 4096, "v1024": 1024, "xchunks": 4096, "xzipf": 256}[mode]
     padded = (lens + al - 1) // al * al
     offs = torch.from_numpy(np.concatenate([[0], np.cumsum(padded)[:-1]])).to(dev)
     lt = torch.from_numpy(lens).to(dev)
     vout = torch.empty(lens.size, dtype=torch.uint32, device=dev)
+    vout64 = torch.empty(lens.size, dtype=torch.uint64, device=dev)
+    import foundationdb_amd.xxh3 as X
 torch.cuda.synchronize()
 for _ in range(5):
-    if mode in VARLEN:
+    if mode in ("xchunks", "xzipf"):
+        X.batch_varlen(big, offs, lt, out=vout64)
+    elif mode in VARLEN:
         F.batch_varlen(big, offs, lt, out=vout)
     elif mode == "xxh3":
         import foundationdb_amd.xxh3 as X
