@@ -22,40 +22,28 @@ struct XxhParams {
 
 constexpr unsigned kWavesPerBlock = 4;
 
-// Split route for long buffers (xxh3_split.hip): buffers longer than
-// kXSplitMin whose 1 KiB blocks' stripe sums are computed in parallel
-// (phase A, PIECES of up to kXPieceBlocks blocks) and chained per buffer
-// (phase B).  Planner output in the workspace:
+// Long-buffer route (xxh3_split.hip): buffers longer than kXSplitMin, each
+// computed by one CU's waves at once (k_xlong), largest first.  Planner
+// output in the workspace:
 constexpr uint64_t kXSplitMin = 16384;
-constexpr uint32_t kXPieceBlocks = 64;
-constexpr uint64_t kXBig = 256;  // phase B starts the chains of this many blocks or more first
 struct XEnt {       // one long buffer
-	uint64_t F;     // its first block in the flat stripe-sum array D
+	uint64_t p;     // its address
 	uint64_t len, seed, idx;
 };
-struct XPiece {     // kXPieceBlocks consecutive blocks of one long buffer (fewer at its end)
-	uint64_t p;     // the buffer's address
-	uint64_t len, d, seed;  // d: flat index of block b0 in D
-	uint32_t b0, nb;
-	uint64_t pad;
-};
-struct XSplit {
-	const uint64_t* sh;   // planner totals: [0] long buffers, [1] blocks, [2] pieces, [3] blocks per phase-A wave, [4] big entries
-	const uint64_t* astart;  // [nwa]: phase-A wave w's first piece << 6 | its first block in that piece (~0: none)
-	uint64_t nwa;            // phase-A waves the planner divided D among
-	const uint64_t* big;     // [sh[4]]: the entries of kXBig blocks or more (any order)
-	const XEnt* ents;
-	const XPiece* pcs;
-	uint64_t* D;          // 8 x u64 per block
+// sh[] words: [0] long buffers routed, [1] k_xlong's dequeue counter, [2] set
+// if a k_xlong wait ran out (never in a correct launch), [8 + c] the planner's
+// cursor of size class c (c = 0: the largest).
+constexpr uint32_t kXShWords = 32, kXClasses = 16;
+struct XLong {
+	uint64_t* sh;
+	const XEnt* ents;     // [sh[0]], largest size class first
 	uint64_t* out;
 	uint64_t seed;        // uniform seed (per-buffer seeds travel in the entries)
 };
-// Per block of capacity: D (64 B) + entries and pieces (<= 8 B): 72 B (plus a
-// flag byte per buffer).
-constexpr uint64_t kXSplitBytesPerBlock = 72;
-int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stream);
-// Waves of the phase-A launch (the planner's share of D per wave).
-uint64_t xxh3_split_waves(int num_cus);
+// Workspace per long block of room (the stream's need is counted in 1 KiB
+// blocks; a long buffer has more than 16): one entry per 16 blocks.
+constexpr uint64_t kXSplitBytesPerBlock = sizeof(XEnt) / 16;
+int launch_xxh3_long(const XLong& S, int num_cus, bool seeds, hipStream_t stream);
 // Resident 256-thread blocks per CU of the main kernel (occupancy query, cached).
 int xxh3_blocks_per_cu();
 inline uint64_t xxh3_nwave(int num_cus) { return (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock; }

@@ -838,15 +838,14 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 // ---------------------------------------------------------------------------
 // Varlen planning: whole buffers per wave, balanced by bytes.  Wave w takes
 // the buffers whose start lies in [w*Q, (w+1)*Q) of the concatenated stream
-// (cost = length + 64).  With room for the split route in the workspace, the
-// buffers longer than kXSplitMin take it (xxh3_split.hip) if all of their
-// stripe-sum blocks, pieces and entries fit the room (else the row kernel
-// takes the whole batch).  No counters: k_xplan writes per-tile sums, k_xscan
-// scans them (the route, the cost prefixes, the split route's totals), k_xassign
-// gives every buffer its place -- the row kernel's waves, the flag byte that
-// takes a split buffer off the row kernel (cost 64 there), the split
-// buffer's entry, its pieces in buffer order at their flat D positions, and
-// the start of every phase-A wave whose equal share of D begins inside it.
+// (cost = length + 64).  With room for the long-buffer route in the
+// workspace, the buffers longer than kXSplitMin take it (xxh3_split.hip) if
+// their entries fit the room (else the row kernel takes the whole batch).
+// No counters to reset: k_xplan writes per-tile sums, k_xscan scans them (the
+// route, the cost prefixes, the size classes' bases), k_xassign gives every
+// buffer its place -- the row kernel's waves, the flag byte that takes a long
+// buffer off the row kernel (cost 64 there) and the long buffer's entry in
+// its size class (largest class first: k_xlong takes them in that order).
 // ---------------------------------------------------------------------------
 struct XPlanP {
 	const uint64_t* lengths;  // nullptr: fixed length
@@ -854,29 +853,31 @@ struct XPlanP {
 	const uint64_t* seeds;
 	const uint8_t* base;
 	uint64_t stride, length, count, seed;
-	uint64_t* tiles;          // [ntile + 2]: cost if split (k_xplan) -> exclusive cost prefixes, total, quantum
-	uint64_t* tneed;          // [ntile]: long blocks (k_xplan) -> exclusive prefix | kTileFits (k_xscan)
-	uint64_t* tcns;           // [ntile]: cost if not split
-	uint64_t* tpc;            // [ntile]: long pieces -> exclusive prefix
-	uint64_t* tnl;            // [ntile]: long buffers -> exclusive prefix
-	uint64_t* sh;             // split totals (XSplit::sh): [0] entries, [1] blocks, [2] pieces, [3] blocks per phase-A wave
-	uint8_t* flag;            // per buffer: 1 if the split route took it
+	uint64_t* tiles;          // [ntile + 2]: cost if routed (k_xplan) -> exclusive cost prefixes, total, quantum
+	uint64_t* tcns;           // [ntile]: cost if not routed
+	uint64_t* tneed;          // [ntile]: long blocks (the stream's need) -> route flag (k_xscan)
+	uint64_t* tcls;           // [4][ntile]: long buffers per size class, 16-bit fields (class c: word c / 4)
+	uint64_t* sh;             // [kXShWords] (XLong::sh)
+	uint8_t* flag;            // per buffer: 1 if the long route took it
 	uint64_t* wave_first;
-	uint64_t* astart;         // [nwa]: phase-A wave w's first piece << 6 | block within it (~0: no work)
-	uint64_t ntile, nwave, nwa;
+	uint64_t ntile, nwave;
 	XEnt* ents;
-	uint64_t* big;            // entries of kXBig blocks or more, appended (sh[4] counts them)
-	XPiece* pcs;
-	uint64_t capD, capS, capP;
+	uint64_t capS;            // entries the room holds (0: no room)
 	uint64_t* hneed;          // host-mapped word (may be null): blocks the batch's long buffers need
 };
-constexpr uint64_t kTileFits = 1ull << 63;
+constexpr uint64_t kTileRouted = 1ull << 63;
 __device__ __forceinline__ uint64_t xp_len(const XPlanP& Q, uint64_t i) { return Q.lengths ? Q.lengths[i] : Q.length; }
 __device__ __forceinline__ uint64_t xp_off(const XPlanP& Q, uint64_t i) { return Q.offsets ? Q.offsets[i] : i * Q.stride; }
 __device__ __forceinline__ uint64_t xp_blocks(uint64_t len) { return ((len - 1) >> 10) + 1; }
-__device__ __forceinline__ uint64_t xp_cost(uint64_t len, bool split) { return split ? 64 : len + 64; }
-// a split candidate (its blocks count in the stream's need whether or not there is room)
+__device__ __forceinline__ uint64_t xp_cost(uint64_t len, bool routed) { return routed ? 64 : len + 64; }
+// a long buffer (its blocks count in the stream's need whether or not there is room)
 __device__ __forceinline__ bool xp_long(uint64_t len) { return len > kXSplitMin; }
+// Size class of a long buffer: 0 for 2^19 blocks (512 MiB) or more, then one
+// per power of two down to 15 for 16-31 blocks.
+__device__ __forceinline__ uint32_t xp_class(uint64_t nb) {
+	const uint32_t lg = 63 - __builtin_clzll(nb);
+	return lg >= 19 ? 0u : 19u - (lg < 4 ? 4u : lg);
+}
 
 // Inclusive prefix sum of a 64-bit value over the wave on DPP (row shifts,
 // then the row broadcasts of lanes 15 and 31; every lane active).
@@ -904,154 +905,151 @@ __device__ __forceinline__ uint64_t rdlane63(uint64_t v) {
 
 // One workgroup per tile of 256 buffers: the tile's sums.
 __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
-	__shared__ uint64_t part[4][5];
+	__shared__ uint64_t part[4][8];
 	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
 	const bool lg = i < Q.count && xp_long(len);
 	const uint64_t nb = lg ? xp_blocks(len) : 0;
-	uint64_t v[5] = {i < Q.count ? xp_cost(len, lg) : 0, i < Q.count ? len + 64 : 0, nb,
-	                 (nb + kXPieceBlocks - 1) / kXPieceBlocks, lg ? 1u : 0u};
+	const uint32_t cl = lg ? xp_class(nb) : 0;
+	uint64_t v[8] = {i < Q.count ? xp_cost(len, lg) : 0, i < Q.count ? len + 64 : 0, nb, 0, 0, 0, 0, 0};
+	if (lg) v[4 + (cl >> 2)] = 1ull << (16 * (cl & 3));
 #pragma unroll
-	for (int q = 0; q < 5; ++q) v[q] = rdlane63(dpp_incl64(v[q]));
+	for (int q = 0; q < 8; ++q) v[q] = rdlane63(dpp_incl64(v[q]));
 	if (lane == 0)
 #pragma unroll
-		for (int q = 0; q < 5; ++q) part[wv][q] = v[q];
+		for (int q = 0; q < 8; ++q) part[wv][q] = v[q];
 	__syncthreads();
-	if (threadIdx.x < 5) {
+	if (threadIdx.x < 8 && threadIdx.x != 3) {
 		const int q = threadIdx.x;
-		const uint64_t s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
-		uint64_t* dst = q == 0 ? Q.tiles : q == 1 ? Q.tcns : q == 2 ? Q.tneed : q == 3 ? Q.tpc : Q.tnl;
+		const uint64_t s = part[0][q] + part[1][q] + part[2][q] + part[3][q];  // (16-bit fields: <= 256 each)
+		uint64_t* dst = q == 0 ? Q.tiles : q == 1 ? Q.tcns : q == 2 ? Q.tneed : Q.tcls + (uint64_t)(q - 4) * Q.ntile;
 		dst[blockIdx.x] = s;
 	}
 }
 
-// Single workgroup.  The split route takes every split candidate or none:
-// all of them if their blocks, pieces and entries fit the room (the library
-// sizes the room from the stream's last need; the _ws form's caller sizes it
-// with xxh3_gpu_varlen_workspace_bytes_for), else the row kernel takes the
-// whole batch.  In place: the exclusive prefixes of the routed tile costs,
+// Single workgroup.  The long route takes every long buffer or none: all of
+// them if their entries fit the room (the library sizes the room from the
+// stream's last need; the _ws form's caller sizes it with
+// xxh3_gpu_varlen_workspace_bytes_for), else the row kernel takes the whole
+// batch.  In place: the exclusive prefixes of the routed tile costs,
 // tiles[ntile] = total cost, tiles[ntile + 1] = quantum Q = ceil(total /
-// nwave), and (routed) the prefixes of the blocks, pieces and entries, the
-// route flag in tneed; the split route's totals in sh[]; every phase-A
-// wave's start set to "no work" (k_xassign fills in the waves that have some).
+// nwave), the route flag in tneed; in sh[] the long buffers routed, the
+// dequeue counter (0) and the size classes' cursors (their bases, largest
+// class first).
 __global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
-	__shared__ uint64_t red[4][16];
-	__shared__ uint64_t carry_s[4];
+	__shared__ uint64_t red[kXClasses + 1][16];
+	__shared__ uint64_t tot_s[kXClasses + 1];
+	__shared__ uint64_t carry_s;
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
 	const uint64_t ntile = Q.ntile;
 	uint64_t* tiles = Q.tiles;
-	for (uint64_t w = t; w < Q.nwa; w += 1024) Q.astart[w] = ~0ull;
-	uint64_t a[3] = {0, 0, 0};
+	// totals: long blocks and the classes' counts
+	uint64_t a[kXClasses + 1] = {};
 	for (uint64_t k = t; k < ntile; k += 1024) {
-		a[0] += Q.tneed[k];
-		a[1] += Q.tpc[k];
-		a[2] += Q.tnl[k];
-	}
+		const uint64_t nb = Q.tneed[k];
+		a[kXClasses] += nb;
+		if (nb)  // (tiles without long buffers have no class counts)
 #pragma unroll
-	for (int q = 0; q < 3; ++q) {
-		const uint64_t s = rdlane63(dpp_incl64(a[q]));
-		if (lane == 0) red[q][wv] = s;
+			for (uint32_t w = 0; w < 4; ++w) {
+				const uint64_t f = Q.tcls[w * ntile + k];
+#pragma unroll
+				for (uint32_t u = 0; u < 4; ++u) a[4 * w + u] += (f >> (16 * u)) & 0xFFFFu;
+			}
 	}
-	if (t < 4) carry_s[t] = 0;
+	if (t == 0) carry_s = 0;
+	const bool anylong = __syncthreads_or(a[kXClasses] != 0);
+	if (anylong) {
+#pragma unroll
+		for (uint32_t q = 0; q <= kXClasses; ++q) {
+			const uint64_t s = rdlane63(dpp_incl64(a[q]));
+			if (lane == 0) red[q][wv] = s;
+		}
+		__syncthreads();
+		if (t <= kXClasses) {
+			uint64_t s = 0;
+			for (uint32_t u = 0; u < 16; ++u) s += red[t][u];
+			tot_s[t] = s;
+		}
+	} else if (t <= kXClasses) {
+		tot_s[t] = 0;
+	}
 	__syncthreads();
-	uint64_t tot[3] = {0, 0, 0};
-	for (uint32_t u = 0; u < 16; ++u)
-#pragma unroll
-		for (int q = 0; q < 3; ++q) tot[q] += red[q][u];
-	const bool fits = tot[0] == 0 || (Q.capD && tot[0] <= Q.capD && tot[1] <= Q.capP && tot[2] <= Q.capS);
-	const bool split = fits && tot[0] != 0;
+	uint64_t nlong = 0;
+	for (uint32_t q = 0; q < kXClasses; ++q) nlong += tot_s[q];
+	const bool routed = nlong != 0 && Q.capS && nlong <= Q.capS;
 	__syncthreads();  // (red is reused below)
 	for (uint64_t c0 = 0; c0 < ntile; c0 += 1024) {
 		const uint64_t k = c0 + t;
 		const bool in = k < ntile;
-		uint64_t x[4] = {in ? (fits ? tiles[k] : Q.tcns[k]) : 0, 0, 0, 0};
-		if (split && in) {
-			x[1] = Q.tneed[k];
-			x[2] = Q.tpc[k];
-			x[3] = Q.tnl[k];
-		}
-		uint64_t inc[4];
-		inc[0] = dpp_incl64(x[0]);
-		if (lane == 63) red[0][wv] = inc[0];
-		if (split) {
-#pragma unroll
-			for (int q = 1; q < 4; ++q) {
-				inc[q] = dpp_incl64(x[q]);
-				if (lane == 63) red[q][wv] = inc[q];
-			}
-		}
+		const uint64_t x = in ? (routed ? tiles[k] : Q.tcns[k]) : 0;
+		const uint64_t inc = dpp_incl64(x);
+		if (lane == 63) red[0][wv] = inc;
 		__syncthreads();
-		uint64_t ex[4];
-#pragma unroll
-		for (int q = 0; q < 4; ++q) {
-			uint64_t wb = carry_s[q];
-			if (q == 0 || split)
-				for (uint32_t u = 0; u < wv; ++u) wb += red[q][u];
-			ex[q] = wb + ((q == 0 || split) ? inc[q] - x[q] : 0);
-		}
+		uint64_t ex = carry_s + inc - x;
+		for (uint32_t u = 0; u < wv; ++u) ex += red[0][u];
 		if (in) {
-			tiles[k] = ex[0];
-			Q.tneed[k] = ex[1] | (split ? kTileFits : 0);
-			Q.tpc[k] = ex[2];
-			Q.tnl[k] = ex[3];
+			tiles[k] = ex;
+			Q.tneed[k] = routed ? kTileRouted : 0;
 		}
 		__syncthreads();
-		if (t == 1023)
-#pragma unroll
-			for (int q = 0; q < 4; ++q) carry_s[q] = ex[q] + x[q];
+		if (t == 1023) carry_s = ex + x;
 		__syncthreads();
 	}
 	if (t == 0) {
-		const uint64_t total = carry_s[0];
+		const uint64_t total = carry_s;
 		tiles[ntile] = total;
 		tiles[ntile + 1] = (total + Q.nwave - 1) / Q.nwave;
-		const uint64_t tb = split ? tot[0] : 0;
-		Q.sh[0] = split ? tot[2] : 0;
-		Q.sh[1] = tb;
-		Q.sh[2] = split ? tot[1] : 0;
-		Q.sh[3] = Q.nwa ? (tb + Q.nwa - 1) / Q.nwa : 0;
-		Q.sh[4] = 0;
-		if (Q.hneed) *(volatile uint64_t*)Q.hneed = tot[0];  // every split candidate's blocks, routed or not
+		Q.sh[0] = routed ? nlong : 0;
+		Q.sh[1] = 0;
+		Q.sh[2] = 0;
+		uint64_t b = 0;
+		for (uint32_t q = 0; q < kXClasses; ++q) {
+			Q.sh[8 + q] = b;
+			b += tot_s[q];
+		}
+		if (Q.hneed) *(volatile uint64_t*)Q.hneed = tot_s[kXClasses];  // every long buffer's blocks, routed or not
 	}
 }
 
 // One workgroup per tile of 256 buffers: buffer i (cost c_i, start s_i) is
 // the first buffer of every wave w with s_{i-1} < w*Q <= s_i; waves past
-// the last buffer get `count`.  A split buffer writes its entry, its pieces
-// and the starts of the phase-A waves whose share begins in its blocks.
+// the last buffer get `count`.  A routed long buffer writes its entry in its
+// size class (any order within the class).
 __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
-	__shared__ uint64_t wsum[4][4];
+	__shared__ uint64_t wsum[4];
+	__shared__ uint32_t ccount[kXClasses];
+	__shared__ uint64_t cbase[kXClasses];
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
 	const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
-	const bool fit = (Q.tneed[blockIdx.x] & kTileFits) != 0;
+	const bool routed = (Q.tneed[blockIdx.x] & kTileRouted) != 0;
 	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
-	const bool split = i < Q.count && fit && xp_long(len);
-	if (Q.capD && i < Q.count) Q.flag[i] = split ? 1 : 0;
-	const uint64_t cost = i < Q.count ? xp_cost(len, split) : 0;
-	const uint64_t nb = split ? xp_blocks(len) : 0;
-	const uint64_t np = (nb + kXPieceBlocks - 1) / kXPieceBlocks;
-	uint64_t x[4] = {cost, nb, np, split ? 1u : 0u}, ex[4];
-#pragma unroll
-	for (int q = 0; q < 4; ++q) {
-		const uint64_t inc = dpp_incl64(x[q]);
-		if (lane == 63) wsum[q][wv] = inc;
-		ex[q] = inc - x[q];
-	}
+	const bool lg = i < Q.count && routed && xp_long(len);
+	if (Q.capS && i < Q.count) Q.flag[i] = lg ? 1 : 0;
+	const uint64_t cost = i < Q.count ? xp_cost(len, lg) : 0;
+	const uint64_t inc = dpp_incl64(cost);
+	if (lane == 63) wsum[wv] = inc;
+	if (t < kXClasses) ccount[t] = 0;
 	__syncthreads();
-#pragma unroll
-	for (int q = 0; q < 4; ++q)
-		for (uint32_t u = 0; u < wv; ++u) ex[q] += wsum[q][u];
+	// a long buffer's rank in its class within the tile (LDS), then one global
+	// add per class and tile (the classes' cursors are a handful of words: one
+	// add per buffer measured 16 us of contention on the chunks batch)
+	const uint32_t cl = lg ? xp_class(xp_blocks(len)) : 0;
+	const uint32_t rank = lg ? atomicAdd(&ccount[cl], 1u) : 0;
+	__syncthreads();
+	if (t < kXClasses && ccount[t]) cbase[t] = atomicAdd((unsigned long long*)&Q.sh[8 + t], (unsigned long long)ccount[t]);
+	__syncthreads();
+	uint64_t ex = inc - cost;
+	for (uint32_t u = 0; u < wv; ++u) ex += wsum[u];
 	const uint64_t q = Q.tiles[Q.ntile + 1];
-	const uint64_t start = Q.tiles[blockIdx.x] + ex[0];
+	const uint64_t start = Q.tiles[blockIdx.x] + ex;
 	if (i < Q.count) {
 		// waves w with s_{i-1} < w*q <= s_i, i.e. [floor(s_{i-1}/q) + 1, floor(s_i/q)];
 		// buffer 0 takes w = 0
 		uint64_t prev = 0;
 		if (i != 0) {
 			const uint64_t lp = xp_len(Q, i - 1);
-			const bool fp = (Q.tneed[(i - 1) >> 8] & kTileFits) != 0;
-			prev = start - xp_cost(lp, fp && xp_long(lp));
+			prev = start - xp_cost(lp, routed && xp_long(lp));  // (the route is batch-wide)
 		}
 		const uint64_t w_lo = i == 0 ? 0 : prev / q + 1;
 		const uint64_t w_hi = start / q;
@@ -1059,68 +1057,44 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 		if (i + 1 == Q.count)  // waves whose first byte lies past the last buffer's start: none
 			for (uint64_t w = start / q + 1; w <= Q.nwave; ++w) Q.wave_first[w] = Q.count;
 	}
-	if (split) {
-		const uint64_t F = (Q.tneed[blockIdx.x] & ~kTileFits) + ex[1];
-		const uint64_t pc = Q.tpc[blockIdx.x] + ex[2];
-		const uint64_t sidx = Q.tnl[blockIdx.x] + ex[3];
+	if (lg) {
+		const uint64_t pos = cbase[cl] + rank;
 		const uint64_t sd = Q.seeds ? Q.seeds[i] : Q.seed;
-		Q.ents[sidx] = XEnt{F, len, sd, i};
-		if (nb >= kXBig) Q.big[atomicAdd((unsigned long long*)&Q.sh[4], 1ull)] = sidx;
-		const uint64_t p = reinterpret_cast<uint64_t>(Q.base) + xp_off(Q, i);
-		for (uint64_t j = 0; j < np; ++j) {
-			const uint32_t b0 = (uint32_t)(j * kXPieceBlocks);
-			const uint32_t n = (uint32_t)(nb - b0 < kXPieceBlocks ? nb - b0 : kXPieceBlocks);
-			Q.pcs[pc + j] = XPiece{p, len, F + b0, sd, b0, n, 0};
-		}
-		// phase-A waves whose share [w*pb, ...) of D begins in [F, F + nb)
-		const uint64_t pb = Q.sh[3];  // (> 0: this buffer's blocks are in the total)
-		for (uint64_t w = (F + pb - 1) / pb; w * pb < F + nb && w < Q.nwa; ++w) {
-			const uint64_t off = w * pb - F;
-			Q.astart[w] = ((pc + off / kXPieceBlocks) << 6) | (off % kXPieceBlocks);
-		}
+		Q.ents[pos] = XEnt{reinterpret_cast<uint64_t>(Q.base) + xp_off(Q, i), len, sd, i};
 	}
 }
 
 // Workspace of the varlen path: the planner arrays, then (given more room)
-// the split route's flags, entries, pieces and stripe sums.
+// the long route's flags and entries.
 struct XLayout {
-	uint64_t tiles, tneed, tcns, tpc, tnl, wave_first, astart, sh, flag, ents, big, pcs, D, base;
-	uint64_t capD, capS, capP;
+	uint64_t tiles, tcns, tneed, tcls, wave_first, sh, flag, ents, base;
+	uint64_t capS;
 };
 static uint64_t al64(uint64_t x) { return (x + 63) & ~uint64_t(63); }
-// nwave: the row kernel's waves (phase A has at most as many, xxh3_split_waves)
 static XLayout xlayout(uint64_t count, uint64_t nwave, uint64_t ws_bytes) {
 	const uint64_t ntile = (count + 255) / 256;
 	XLayout L{};
 	L.tiles = 0;
-	L.tneed = al64(8 * (ntile + 2));
-	L.tcns = al64(L.tneed + 8 * ntile);
-	L.tpc = al64(L.tcns + 8 * ntile);
-	L.tnl = al64(L.tpc + 8 * ntile);
-	L.wave_first = al64(L.tnl + 8 * ntile);
-	L.astart = al64(L.wave_first + 8 * (nwave + 1) + 64);
-	L.sh = al64(L.astart + 16 * nwave);  // phase A: up to twice the row kernel's waves
-	L.base = L.sh + 64;
-	// split room: flags (1 B per buffer), then per block of capacity 72 B
+	L.tcns = al64(8 * (ntile + 2));
+	L.tneed = al64(L.tcns + 8 * ntile);
+	L.tcls = al64(L.tneed + 8 * ntile);
+	L.wave_first = al64(L.tcls + 32 * ntile);
+	L.sh = al64(L.wave_first + 8 * (nwave + 1) + 64);
+	L.base = L.sh + 8 * kXShWords;
+	// room: flags (1 B per buffer), then the entries
 	const uint64_t fl = al64(count);
-	uint64_t capD = ws_bytes > L.base + fl ? (ws_bytes - L.base - fl) / kXSplitBytesPerBlock : 0;
-	if (capD < 256) capD = 0;
-	L.capD = capD;
-	L.capS = capD ? capD / 16 + 1 : 0;               // long buffers have > 16 blocks
-	L.capP = capD ? capD / kXPieceBlocks + L.capS : 0;
+	uint64_t capS = ws_bytes > L.base + fl ? (ws_bytes - L.base - fl) / sizeof(XEnt) : 0;
+	L.capS = capS;
 	L.flag = L.base;
 	L.ents = L.flag + fl;
-	L.big = al64(L.ents + sizeof(XEnt) * L.capS);
-	L.pcs = al64(L.big + 8 * L.capS);
-	L.D = al64(L.pcs + sizeof(XPiece) * L.capP);
 	return L;
 }
 
 uint64_t xxh3_workspace_bytes(uint64_t count, uint64_t nwave) { return xlayout(count, nwave, 0).base; }
 uint64_t xxh3_workspace_bytes_for(uint64_t count, uint64_t nwave, uint64_t long_blocks) {
 	if (long_blocks == 0) return xxh3_workspace_bytes(count, nwave);
-	const uint64_t capD = long_blocks < 256 ? 256 : long_blocks;
-	return xlayout(count, nwave, 0).base + al64(count) + kXSplitBytesPerBlock * capD + 256;
+	// (a long buffer has more than 16 blocks)
+	return xlayout(count, nwave, 0).base + al64(count) + sizeof(XEnt) * (long_blocks / 16 + 1);
 }
 
 int xxh3_blocks_per_cu() {
@@ -1146,12 +1120,11 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 	const uint64_t nwave = grid * wpb;
 	const uint64_t mis = (reinterpret_cast<uint64_t>(P.base) | (P.offsets ? 1 : P.stride));
 	const bool aligned = (mis & 15) == 0;
-	// the planner: varlen batches, and fixed-length long buffers given room for the split route
+	// the planner: varlen batches, and fixed-length long buffers given room for the long route
 	const bool fixed_split = !P.offsets && ws && P.length > kXSplitMin;
 	if (P.offsets || fixed_split) {
 		const uint64_t ntile = (P.count + 255) / 256;
 		const XLayout L = xlayout(P.count, nwave, P.ws_bytes);
-		if (fixed_split && L.capD == 0) return -1;
 		uint8_t* w8 = static_cast<uint8_t*>(ws);
 		XPlanP Q{};
 		Q.lengths = P.lengths;
@@ -1163,44 +1136,32 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		Q.count = P.count;
 		Q.seed = P.seed;
 		Q.tiles = reinterpret_cast<uint64_t*>(w8 + L.tiles);
-		Q.tneed = reinterpret_cast<uint64_t*>(w8 + L.tneed);
 		Q.tcns = reinterpret_cast<uint64_t*>(w8 + L.tcns);
-		Q.tpc = reinterpret_cast<uint64_t*>(w8 + L.tpc);
-		Q.tnl = reinterpret_cast<uint64_t*>(w8 + L.tnl);
+		Q.tneed = reinterpret_cast<uint64_t*>(w8 + L.tneed);
+		Q.tcls = reinterpret_cast<uint64_t*>(w8 + L.tcls);
 		Q.sh = reinterpret_cast<uint64_t*>(w8 + L.sh);
 		Q.flag = w8 + L.flag;
 		Q.wave_first = reinterpret_cast<uint64_t*>(w8 + L.wave_first);
-		Q.astart = reinterpret_cast<uint64_t*>(w8 + L.astart);
 		Q.ntile = ntile;
 		Q.nwave = nwave;
-		Q.nwa = L.capD ? xxh3_split_waves(num_cus) : 0;
-		if (Q.nwa > 2 * nwave) Q.nwa = 2 * nwave;  // (the layout holds 2 nwave starts)
 		Q.ents = reinterpret_cast<XEnt*>(w8 + L.ents);
-		Q.big = reinterpret_cast<uint64_t*>(w8 + L.big);
-		Q.pcs = reinterpret_cast<XPiece*>(w8 + L.pcs);
-		Q.capD = L.capD;
 		Q.capS = L.capS;
-		Q.capP = L.capP;
 		Q.hneed = P.hneed;
 		k_xplan<<<(unsigned)ntile, 256, 0, stream>>>(Q);
 		k_xscan<<<1, 1024, 0, stream>>>(Q);
 		k_xassign<<<(unsigned)ntile, 256, 0, stream>>>(Q);
-		if (L.capD) {
-			XSplit S{};
+		if (L.capS) {
+			XLong S{};
 			S.sh = Q.sh;
-			S.astart = Q.astart;
-			S.nwa = Q.nwa;
 			S.ents = Q.ents;
-			S.big = Q.big;
-			S.pcs = Q.pcs;
-			S.D = reinterpret_cast<uint64_t*>(w8 + L.D);
 			S.out = P.out;
 			S.seed = P.seed;
-			launch_xxh3_split(S, num_cus, P.seeds != nullptr, stream);
+			launch_xxh3_long(S, num_cus, P.seeds != nullptr, stream);
 		}
-		if (fixed_split) return 0;  // every buffer is long: the split route did them all
+		// fixed-length long buffers whose entries all fit: the long route did them all
+		if (fixed_split && L.capS >= P.count) return 0;
 		P.wave_first = Q.wave_first;
-		P.lflag = L.capD ? Q.flag : nullptr;
+		P.lflag = L.capS ? Q.flag : nullptr;
 		if (P.seeds)
 			k_xxh3_vrows<true><<<(unsigned)grid, 256, 0, stream>>>(P);
 		else

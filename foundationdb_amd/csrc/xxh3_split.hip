@@ -1,7 +1,7 @@
-// Split XXH3-64 route for LONG buffers (gfx950): xxHash v0.8.0
-// XXH3_64bits[_withSeed] (flow/include/flow/xxhash.h:3641-3718, 3800-3837)
-// of buffers longer than kXSplitMin, bit-identical, with the work of one
-// buffer spread over the whole GPU.
+// Long-buffer XXH3-64 route (gfx950): xxHash v0.8.0 XXH3_64bits[_withSeed]
+// (flow/include/flow/xxhash.h:3641-3718, 3800-3837) of buffers longer than
+// kXSplitMin, bit-identical, with the blocks of one buffer computed by many
+// waves at once.
 //
 // A long input accumulates 64-byte stripes into eight 64-bit lanes and
 // scrambles them after every 1 KiB block.  The accumulation of one block is a
@@ -13,17 +13,19 @@
 //     hash = mergeAccs(acc, secret + 11, len * PRIME64_1)
 // (tests/xxh3_split_model.py restates this and checks it against the oracle.)
 //
-//   phase A  k_xsplit_a: every block of every long buffer as one flat stream
-//            (D order, PIECES of 64 consecutive blocks of one buffer carry the
-//            metadata), an equal share of blocks per wave; the row layout of k_xxh3_rows (a 16-lane row per
-//            block: four coalesced 256-byte loads, 32x32->64 products, two DPP
-//            row rotates) writes D[b] (64 B per KiB) to the workspace.
-//   phase B  k_xsplit_b: one wave per long buffer: 4 KiB of stripe sums per
-//            round by LDS-DMA (the next round in flight), eight chain lanes
-//            (one accumulator each), one scramble per block, the merge.
-// The planner (xxh3_kernels.hip: k_xplan / k_xscan / k_xassign) picks the
-// long buffers, lays out the pieces and D in buffer order, divides D among
-// phase A's waves, and takes the long buffers off the row kernel.
+// k_xlong: one persistent 1024-thread workgroup per CU, D never leaves it.
+// Four CHAIN waves each own a SLOT: a buffer taken from the batch's long
+// buffers, largest first (the planner's size classes), and a ring of 64
+// STEPS (4 blocks each) of stripe sums in LDS.  Twelve PRODUCER waves claim
+// steps of the slots' buffers (LDS compare-and-swap, never past the ring's
+// free room), stream the step's four blocks exactly like k_xxh3_rows (a
+// 16-lane row per block: four coalesced 256-byte loads, 32x32->64 products,
+// two DPP row rotates) and write D into the ring with the step's tag; the
+// chain wave scrambles the steps in order as their tags appear and merges.
+// A first version wrote D to HBM (64 B per KiB) for a second kernel of
+// chains: the stores alone cost phase A a fifth of its time (they hold up the
+// in-order vmcnt waits on the loads behind them) and the chains ran after
+// the stream.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -66,6 +68,7 @@ __device__ __forceinline__ void add_dpp(uint32_t& lo, uint32_t& hi) {
 	hi = (uint32_t)(s >> 32);
 }
 
+__device__ __forceinline__ uint32_t rdf32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint64_t rdf64(uint64_t v) {
 	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
 	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
@@ -75,101 +78,185 @@ __device__ __forceinline__ uint64_t rdf64(uint64_t v) {
 typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
 typedef __attribute__((address_space(1))) const u64x2u g_u64x2u;
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) const u64x2 g_u64x2;
-typedef __attribute__((address_space(1))) u64x2 gw_u64x2;
 typedef __attribute__((address_space(1))) const uint64_t g_u64;
 
 __device__ __forceinline__ uint64_t gld64(const uint64_t* p) { return *((g_u64*)reinterpret_cast<uintptr_t>(p)); }
-// A piece's metadata through the scalar cache (constant address space, a
-// wave-uniform address: s_load, counted by lgkmcnt): as a vector load it
-// would sit in the data loads' in-order vmcnt queue, and every piece change
-// would wait for the blocks in flight.  The planner wrote the pieces in an
-// earlier launch; nothing in this one writes them.
-typedef __attribute__((address_space(4))) const uint64_t c_u64;
-__device__ __forceinline__ XPiece ld_piece(const XPiece* pcs, uint64_t i) {
-	static_assert(sizeof(XPiece) == 48, "six words");
-	const c_u64* q = (const c_u64*)reinterpret_cast<uintptr_t>(pcs + i);
-	XPiece r;
-	r.p = q[0];
-	r.len = q[1];
-	r.d = q[2];
-	r.seed = q[3];
-	const uint64_t w = q[4];
-	r.b0 = (uint32_t)w;
-	r.nb = (uint32_t)(w >> 32);
-	r.pad = 0;
-	return r;
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Phase A: stripe sums, an equal share of D's blocks per wave (pieces of 64
-// blocks per wave measured 13 % of imbalance on the chunks batch: ~6 pieces
-// per wave, a third of them partial).
-// Lane (r, g, k) = (lane / 16, (lane % 16) / 4, lane % 4): row r takes block
-// b + r of a STEP (four consecutive blocks of one piece), stripes g, g+4,
-// g+8, g+12 for accumulator pair k.  The row sums close with two DPP row
-// rotates, after which every lane of a row holds its pair's sums; a step's
-// sums stay in the lanes with g == step % 4 and leave in bursts (kXGroup).
+// k_xlong
 // ---------------------------------------------------------------------------
-struct AStep {
-	uint64_t v[4][2];
-	uint64_t p, len, seed, d;  // the piece's buffer; d: flat index of row 0's block
-	uint32_t b, nrows;         // row 0's block in the buffer; rows in use (0: idle step)
+// Four chain slots: with two (fourteen producers) the chains bound the
+// launch (264 us against 193 us on the chunks batch), three ~ four.
+constexpr uint32_t kLWaves = 16, kLChains = 4, kLProd = kLWaves - kLChains;
+constexpr uint32_t kLRingSteps = 64;  // per slot: 64 steps x 4 blocks x 64 B = 16 KiB
+constexpr uint32_t kLSpinMax = 1u << 24;  // bounded waits (a correct launch never reaches them)
+
+struct LSlot {
+	uint32_t claimed;         // steps claimed by producers (CAS; ~0 while the slot changes buffers)
+	uint32_t lim;             // steps that may be claimed: min(nsteps, consumed + kLRingSteps)
+	uint32_t gbase, nsteps;   // the slot's step number of the buffer's step 0; the buffer's steps
+	uint64_t p, len, seed;
+	uint32_t closed, pad;     // the slot takes no more buffers
+};
+struct LShared {
+	uint64_t ring[kLChains][kLRingSteps * 4][8];  // D of block row (gstep % 64) * 4 + r
+	uint32_t tag[kLChains][kLRingSteps];          // gstep + 1 once the step's D is in the ring
+	LSlot slot[kLChains];
 };
 
 template <bool SEEDS>
-__global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
-	const uint64_t npc = rdf64(gld64(S.sh + 2));
-	if (npc == 0) return;  // no long buffer this batch
-	const int lane = threadIdx.x & 63;
-	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
-	const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	if (w >= S.nwa) return;
-	// this wave's share of D: blocks [w*pb, min((w+1)*pb, total)), starting at
-	// block `a & 63` of piece `a >> 6` (the planner, k_xassign)
-	const uint64_t a = rdf64(gld64(S.astart + w));
-	if (a == ~0ull) return;
-	const uint64_t tb = rdf64(gld64(S.sh + 1)), pb = rdf64(gld64(S.sh + 3));
-	const uint64_t fb1 = (w + 1) * pb < tb ? (w + 1) * pb : tb;
-	const XPiece* __restrict__ pcs = S.pcs;
-	// load cursor: piece lq (metadata in Lm) at block lpos of it, rem blocks of
-	// the share left; the next piece's metadata (scalar loads, lgkmcnt: off the
-	// data loads' vmcnt queue)
-	uint64_t lq = a >> 6, rem = fb1 - w * pb;
-	uint32_t lpos = (uint32_t)(a & 63);
-	XPiece Lm = ld_piece(pcs, rdf64(lq));
-	XPiece Nm = ld_piece(pcs, rdf64(lq + 1 < npc ? lq + 1 : lq));
-	const uint64_t idle_p = Lm.p;  // an idle step reads the share's first block again (discarded)
-	auto load = [&](AStep& St) __attribute__((always_inline)) {
-		if (rem != 0) {
-			St.p = Lm.p;
-			St.len = Lm.len;
-			St.seed = Lm.seed;
-			St.b = Lm.b0 + lpos;
-			St.d = Lm.d + lpos;
-			uint32_t n = Lm.nb - lpos < 4 ? Lm.nb - lpos : 4;
-			n = rem < n ? (uint32_t)rem : n;
-			St.nrows = n;
-			lpos += n;
-			rem -= n;
-			if (lpos >= Lm.nb && rem != 0) {
-				++lq;
-				lpos = 0;
-				Lm = Nm;
-				Nm = ld_piece(pcs, rdf64(lq + 1 < npc ? lq + 1 : lq));
+__global__ __launch_bounds__(1024) void k_xlong(XLong S) {
+	__shared__ LShared L;
+	const uint64_t nlong = rdf64(gld64(S.sh + 0));
+	if (nlong == 0) return;  // no long buffer this batch (uniform over the grid)
+	const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	for (uint32_t q = threadIdx.x; q < kLChains * kLRingSteps; q += blockDim.x) (&L.tag[0][0])[q] = 0;
+	if (threadIdx.x < kLChains) {
+		LSlot& s = L.slot[threadIdx.x];
+		s.nsteps = s.gbase = s.lim = 0;
+		s.claimed = ~0u;
+		s.closed = 0;
+	}
+	__syncthreads();
+	volatile LSlot* VS = L.slot;
+	volatile uint32_t* VT = &L.tag[0][0];
+
+	if (wv >= kLProd) {
+		// ---------------- chain wave: slot c ----------------
+		// Its scrambles are a dependent chain of a few instructions per block,
+		// issued between the producers' streams on the same SIMD: at the default
+		// priority the arbitration starved it (the rings filled and the producers
+		// idled), so it takes the highest.
+		__builtin_amdgcn_s_setprio(3);
+		const uint32_t c = wv - kLProd;
+		const uint32_t j = lane & 7;
+		const uint64_t init = j == 0 ? P32_3 : j == 1 ? P64_1 : j == 2 ? P64_2 : j == 3 ? P64_3
+		                    : j == 4 ? P64_4 : j == 5 ? P32_2 : j == 6 ? P64_5 : P32_1;
+		uint32_t gseq = 0;
+		for (;;) {
+			uint64_t q = 0;
+			if (lane == 0) q = atomicAdd((unsigned long long*)S.sh + 1, 1ull);
+			q = rdf64(__shfl(q, 0));
+			if (q >= nlong) break;
+			const XEnt E = S.ents[q];
+			const uint64_t p = rdf64(E.p), len = rdf64(E.len), seed = rdf64(E.seed), idx = rdf64(E.idx);
+			const uint64_t nfull = (len - 1) >> 10, nb = nfull + 1;
+			const uint32_t nsteps = (uint32_t)((nb + 3) >> 2);
+			// publish: claimed is the gate (~0 while the fields change: a producer
+			// that reads it claims nothing; 0 opens the buffer's steps)
+			if (lane == 0) {
+				VS[c].p = p;
+				VS[c].len = len;
+				VS[c].seed = seed;
+				VS[c].nsteps = nsteps;
+				VS[c].gbase = gseq;
+				VS[c].lim = nsteps < kLRingSteps ? nsteps : kLRingSteps;
+				__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+				VS[c].claimed = 0;
 			}
-		} else {
-			St.p = idle_p;
-			St.len = 1025;
-			St.seed = 0;
-			St.b = 0;
-			St.d = 0;
-			St.nrows = 0;
+			const uint64_t ck = swd(16 + (int)j, seed);  // scramble key: secret + 128 + 8j
+			const uint64_t gk = sat(1 + (int)j, 3, seed);  // merge key: secret + 11 + 8j
+			const uint32_t cklo = (uint32_t)ck, ckhi = (uint32_t)(ck >> 32);
+			// scrambleAcc (xxhash.h:3702-3718) in 32-bit halves: the high half's
+			// product is off the low half's dependent path
+			auto scr = [&](uint64_t a) __attribute__((always_inline)) -> uint64_t {
+				const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+				const uint32_t lo2 = __builtin_amdgcn_bitop3_b32(lo, hi >> 15, cklo, 0x96);  // xor3
+				const uint64_t m = (uint64_t)lo2 * (uint32_t)P32_1;
+				return m + ((uint64_t)((hi ^ ckhi) * (uint32_t)P32_1) << 32);
+			};
+			uint64_t acc = init;
+			for (uint32_t t = 0; t < nsteps; ++t) {
+				const uint32_t gs = gseq + t, ri = gs % kLRingSteps;
+				for (uint32_t spin = 0; VT[c * kLRingSteps + ri] != gs + 1; ++spin) {
+					if (spin >= kLSpinMax) {
+						if (lane == 0) *(volatile uint64_t*)(S.sh + 2) = 1;  // (never: a stalled ring)
+						return;
+					}
+					__builtin_amdgcn_s_sleep(1);
+				}
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+				const uint64_t b0 = 4ull * t;
+				uint64_t x[4];
+#pragma unroll
+				for (uint32_t r = 0; r < 4; ++r) x[r] = L.ring[c][ri * 4 + r][j];
+#pragma unroll
+				for (uint32_t r = 0; r < 4; ++r)
+					if (b0 + r < nb) acc = b0 + r < nfull ? scr(acc + x[r]) : acc + x[r];
+				// the ring rows are read (in registers) before the step's room is handed back
+				__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+				if (lane == 0) VS[c].lim = t + 1 + kLRingSteps < nsteps ? t + 1 + kLRingSteps : nsteps;
+			}
+			if (lane == 0) {
+				VS[c].claimed = ~0u;  // (every step was claimed: claimed == nsteps, no CAS in flight succeeds)
+			}
+			gseq += nsteps;
+			// mergeAccs (xxhash.h:3678-3700): lanes 2k, 2k+1 -> mulfold, summed over k
+			const uint64_t a = acc ^ gk;
+			const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)a, 1), phi = (uint32_t)__shfl_xor((int)(uint32_t)(a >> 32), 1);
+			const uint64_t bq = ((uint64_t)phi << 32) | plo;
+			uint64_t m = (lane < 8 && !(j & 1)) ? (a * bq ^ __umul64hi(a, bq)) : 0;
+#pragma unroll
+			for (int o = 2; o < 8; o <<= 1) {
+				const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), o);
+				m += ((uint64_t)hi << 32) | lo;
+			}
+			uint64_t h = len * P64_1 + m;
+			h ^= h >> 37;
+			h *= 0x165667919E3779F9ull;
+			h ^= h >> 32;
+			if (lane == 0) S.out[idx] = h;
 		}
-		const uint32_t rr = (uint32_t)r < St.nrows ? (uint32_t)r : 0u;  // rows past the piece: row 0's block
-		const uint64_t blk = St.b + rr;
+		if (lane == 0) VS[c].closed = 1;
+		return;
+	}
+
+	// ---------------- producer wave ----------------
+	// Lane (r, g, k) = (lane / 16, (lane % 16) / 4, lane % 4): row r takes block
+	// 4t + r of a step, stripes g, g+4, g+8, g+12 for accumulator pair k.
+	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
+	struct PStep {
+		uint64_t v[4][2];
+		uint64_t p, len, seed;
+		uint32_t c, t, gs, nrows;  // slot, step, its tag - 1, rows in use (0: idle)
+	};
+	uint32_t pref = wv % kLChains;  // the slot tried first (rotates)
+	// Claim a step (wave-uniform): one LDS read of the slot's {claimed, lim},
+	// lane 0's compare-and-swap, then the buffer's fields (the buffer cannot
+	// change while one of its steps is unwritten).
+	auto claim = [&](PStep& St) __attribute__((always_inline)) {
+		St.nrows = 0;
+		// (a lost race moves on to the next slot: the winner's neighbours are
+		// likely racing for this one too; two rounds over the slots)
+		for (uint32_t u = 0; u < 2 * kLChains; ++u) {
+			const uint32_t c = (pref + u) % kLChains;
+			{
+				const uint64_t cw = *(volatile uint64_t*)&L.slot[c].claimed;
+				const uint32_t cl = (uint32_t)cw, lim = (uint32_t)(cw >> 32);
+				if (cl >= lim) continue;  // (~0: between buffers)
+				uint32_t old = 0;
+				if (lane == 0) old = atomicCAS((uint32_t*)&L.slot[c].claimed, cl, cl + 1);
+				if ((uint32_t)__builtin_amdgcn_readlane((int)old, 0) != cl) {
+					continue;
+				}
+				St.c = c;
+				St.t = cl;
+				St.gs = rdf32(VS[c].gbase) + cl;
+				St.p = rdf64(VS[c].p);
+				St.len = rdf64(VS[c].len);
+				St.seed = rdf64(VS[c].seed);
+				const uint64_t nb = ((St.len - 1) >> 10) + 1;
+				St.nrows = 4ull * cl + 4 <= nb ? 4u : (uint32_t)(nb - 4ull * cl);
+				pref = (c + 1) % kLChains;
+				return;
+			}
+		}
+	};
+	auto load = [&](PStep& St) __attribute__((always_inline)) {
+		if (St.nrows == 0) return;
+		const uint32_t rr = (uint32_t)r < St.nrows ? (uint32_t)r : 0u;  // rows past the buffer: row 0's block
+		const uint64_t blk = 4ull * St.t + rr;
 		const uint64_t nfull = (St.len - 1) >> 10;
 		const uint32_t ns = (uint32_t)(((St.len - 1) - (nfull << 10)) >> 6);
 		const bool fin = blk == nfull;
@@ -195,37 +282,14 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 		l1 = sat(16 + 2 * k, 1, sd);
 	};
 	keys(kseed);
-	// saved sums: lane (r, g, k) keeps the sums of row r, pair k of steps
-	// g, g + 4, g + 8, g + 12 of a group of kXGroup steps, which leave together
-	// as kXGroup / 4 16-byte stores per lane.  A store holds up the next wait on
-	// the data loads issued after it (vmcnt counts stores and loads in issue
-	// order) until it has reached memory, which under the read stream takes
-	// several us: one store per four steps cost phase A ~25 % (212 -> 162 us
-	// without the stores on the chunks batch), so they go out in bursts.
-	constexpr uint32_t kXGroup = 16;
-	uint64_t e0[kXGroup / 4], e1[kXGroup / 4], ei[kXGroup / 4];
-	bool ev[kXGroup / 4];
-#pragma unroll
-	for (uint32_t j = 0; j < kXGroup / 4; ++j) {
-		e0[j] = e1[j] = ei[j] = 0;
-		ev[j] = false;
-	}
-	uint32_t slot = 0;  // steps saved since the last store (uniform)
-	uint64_t* __restrict__ D = S.D;
-	auto flush = [&]() __attribute__((always_inline)) {
-#pragma unroll
-		for (uint32_t j = 0; j < kXGroup / 4; ++j) {
-			if (ev[j]) *((gw_u64x2*)reinterpret_cast<uintptr_t>(D + 8 * ei[j] + 2 * k)) = u64x2{e0[j], e1[j]};
-			ev[j] = false;
-		}
-	};
-	auto compute = [&](const AStep& St) __attribute__((always_inline)) {
+	uint32_t tag_at = 0, tag_v = 0;  // the last computed step's tag, not yet published
+	auto compute = [&](const PStep& St) __attribute__((always_inline)) {
 		if (St.nrows == 0) return;
 		if (SEEDS && St.seed != kseed) {
 			kseed = St.seed;
 			keys(kseed);
 		}
-		const uint64_t blk = St.b + r;
+		const uint64_t blk = 4ull * St.t + r;
 		const uint64_t nfull = (St.len - 1) >> 10;
 		const uint32_t ns = (uint32_t)(((St.len - 1) - (nfull << 10)) >> 6);
 		const bool fin = blk == nfull;
@@ -247,178 +311,59 @@ __global__ __launch_bounds__(256) void k_xsplit_a(XSplit S) {
 		add_dpp<0x124>(lo1, hi1);
 		add_dpp<0x128>(lo0, hi0);  // row_ror:8
 		add_dpp<0x128>(lo1, hi1);
-#pragma unroll
-		for (uint32_t j = 0; j < kXGroup / 4; ++j)
-			if ((slot >> 2) == j && (uint32_t)g == (slot & 3)) {
-				e0[j] = ((uint64_t)hi0 << 32) | lo0;
-				e1[j] = ((uint64_t)hi1 << 32) | lo1;
-				ei[j] = St.d + r;
-				ev[j] = (uint32_t)r < St.nrows;
-			}
-		if (++slot == kXGroup) {
-			flush();
-			slot = 0;
-		}
+		const uint32_t ri = St.gs % kLRingSteps;
+		if (g == 0 && (uint32_t)r < St.nrows)
+			*reinterpret_cast<u64x2*>(&L.ring[St.c][ri * 4 + r][2 * k]) =
+			    u64x2{((uint64_t)hi0 << 32) | lo0, ((uint64_t)hi1 << 32) | lo1};
+		tag_at = St.c * kLRingSteps + ri;
+		tag_v = St.gs + 1;
 	};
-	AStep s0, s1, t0, t1;
+	// The step's tag, once its D is in LDS: issued after the next claim, whose
+	// LDS round trips (in order with the D writes) already waited for them.
+	auto publish = [&]() __attribute__((always_inline)) {
+		if (tag_v == 0) return;
+		__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (normally complete already)
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+		if (lane == 0) VT[tag_at] = tag_v;
+		tag_v = 0;
+	};
+	auto all_closed = [&]() -> bool {
+		bool cl = true;
 #pragma unroll
-	for (int i = 0; i < 4; ++i) s0.v[i][0] = s0.v[i][1] = s1.v[i][0] = s1.v[i][1] = 0;
-	s0.p = s1.p = idle_p;
-	s0.len = s1.len = 1025;
-	s0.seed = s1.seed = 0;
-	s0.b = s1.b = 0;
-	s0.d = s1.d = 0;
-	s0.nrows = s1.nrows = 0;
+		for (uint32_t c = 0; c < kLChains; ++c) cl = cl && VS[c].closed;
+		return cl;
+	};
+	PStep A, B;
+	claim(A);
+	load(A);
+	claim(B);
+	load(B);
+	uint32_t idle = 0;
 	for (;;) {
-		load(t0);
-		load(t1);
-		__builtin_amdgcn_sched_barrier(0);
-		compute(s0);
-		compute(s1);
-		__builtin_amdgcn_sched_barrier(0);
-		if (t0.nrows == 0) break;  // (t1 is idle too: steps are loaded in order)
-		load(s0);
-		load(s1);
-		__builtin_amdgcn_sched_barrier(0);
-		compute(t0);
-		compute(t1);
-		__builtin_amdgcn_sched_barrier(0);
-		if (s0.nrows == 0) break;
-	}
-	flush();
-}
-
-// ---------------------------------------------------------------------------
-// Phase B: the chains, one wave per long buffer (64-thread workgroups, two
-// per SIMD: more waves per SIMD slow every chain down, and the longest one
-// sets the time); lane j < 8 holds acc[j].  The stripe sums
-// arrive 64 blocks (4 KiB) per round by LDS-DMA (global_load_lds: no VGPR
-// staging for the compiler to wait on) into a ring of four rounds, three in
-// flight while the chain runs (with one in flight the chain waited on every
-// round: a round's 64 scrambles take less than the DMA's latency under load).
-// The chain is the only sequential part of XXH3: one scramble per 1 KiB
-// block, so the batch's longest buffer sets this kernel's time.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_xsplit_b(XSplit S) {
-	constexpr uint32_t NR = 4;  // rounds of 4 KiB in the LDS ring: three in flight while one is chained
-	__shared__ uint64_t sd[NR * 512];
-	const uint64_t nsplit = rdf64(gld64(S.sh + 0));
-	const uint64_t nbig = rdf64(gld64(S.sh + 4));
-	const uint32_t lane = threadIdx.x;
-	const uint32_t j = lane & 7;
-	const uint64_t init = j == 0 ? P32_3 : j == 1 ? P64_1 : j == 2 ? P64_2 : j == 3 ? P64_3
-	                    : j == 4 ? P64_4 : j == 5 ? P32_2 : j == 6 ? P64_5 : P32_1;
-	typedef __attribute__((address_space(1))) const void* gp;
-	typedef __attribute__((address_space(3))) void* lp;
-	auto chain = [&](uint64_t sidx) __attribute__((always_inline)) {
-		const XEnt E = S.ents[sidx];
-		const uint64_t len = rdf64(E.len), seed = rdf64(E.seed), idx = rdf64(E.idx);
-		const uint64_t nfull = (len - 1) >> 10, nb = nfull + 1;
-		const uint8_t* base = reinterpret_cast<const uint8_t*>(S.D + 8 * rdf64(E.F));
-		const uint64_t last16 = 64 * nb - 16;  // the last 16 bytes of this buffer's stripe sums
-		const uint64_t nround = (nb + 63) >> 6;
-		const uint64_t ck = swd(16 + (int)j, seed);  // scramble key: secret + 128 + 8j
-		const uint64_t gk = sat(1 + (int)j, 3, seed);  // merge key: secret + 11 + 8j
-		const uint32_t cklo = (uint32_t)ck, ckhi = (uint32_t)(ck >> 32);
-		// scrambleAcc (xxhash.h:3702-3718) in 32-bit halves: the high half's
-		// product is off the dependent path (a ^= a >> 47 changes only the low
-		// half): shift, xor3, one 32x32->64 mad and one add per block
-		auto scr = [&](uint64_t a) __attribute__((always_inline)) -> uint64_t {
-			const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
-			const uint32_t lo2 = __builtin_amdgcn_bitop3_b32(lo, hi >> 15, cklo, 0x96);  // xor3
-			const uint64_t m = (uint64_t)lo2 * (uint32_t)P32_1;
-			return m + ((uint64_t)((hi ^ ckhi) * (uint32_t)P32_1) << 32);
-		};
-		uint64_t acc = init;
-		// round c -> sd[(c % NR) * 512]: lane L's 16 bytes of quarter q land at
-		// 1024 q + 16 L (the wave-uniform base + lane x 16 of the DMA)
-		auto issue = [&](uint64_t c) __attribute__((always_inline)) {
-			uint64_t* dst = sd + 512 * (uint32_t)(c % NR);
-#pragma unroll
-			for (int q = 0; q < 4; ++q) {
-				const uint64_t o = 4096 * c + 1024 * q + 16 * lane;
-				__builtin_amdgcn_global_load_lds((gp)(base + (o < last16 ? o : last16)), (lp)(dst + 128 * q), 16, 0, 0);
-			}
-		};
-		// the entry's loads complete here, before any DMA is in flight (a use of
-		// an ordinary load's result behind a DMA would wait for the DMA too)
-		__builtin_amdgcn_s_waitcnt(0);
-		__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-		for (uint32_t c = 0; c + 1 < NR; ++c) issue(c);
-		for (uint64_t c = 0; c < nround; ++c) {
-			issue(c + NR - 1);  // into round c - 1's slot (read); clamped: values past the end are never used
-			__builtin_amdgcn_s_waitcnt(0x0F7C);  // vmcnt(12): round c has landed, c + 1 .. c + 3 in flight
-			const uint64_t* r = sd + 512 * (uint32_t)(c % NR);
-			if (lane < 8) {
-				const uint64_t b0 = 64 * c;
-				if (b0 + 64 <= nfull) {
-#pragma unroll 16
-					for (int t = 0; t < 64; ++t) acc = scr(acc + r[8 * t + j]);
-				} else {
-					for (uint64_t t = 0; b0 + t < nb; ++t) {
-						const uint64_t x = r[8 * t + j];
-						acc = b0 + t < nfull ? scr(acc + x) : acc + x;
-					}
-				}
-			}
-			// the reads of round c complete before round c + NR is issued into its slot
-			__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+		compute(A);
+		claim(A);
+		publish();
+		load(A);
+		compute(B);
+		claim(B);
+		publish();
+		load(B);
+		if (A.nrows == 0 && B.nrows == 0) {
+			if (all_closed()) break;
+			if (++idle >= kLSpinMax) break;  // (never: see the chain's bound)
+			__builtin_amdgcn_s_sleep(2);
+		} else {
+			idle = 0;
 		}
-		__builtin_amdgcn_s_waitcnt(0);  // every DMA of this buffer landed before the next one reuses the buffers
-		// mergeAccs (xxhash.h:3678-3700): lanes 2k, 2k+1 -> mulfold, summed over k
-		const uint64_t a = acc ^ gk;
-		const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)a, 1), phi = (uint32_t)__shfl_xor((int)(uint32_t)(a >> 32), 1);
-		const uint64_t bq = ((uint64_t)phi << 32) | plo;
-		uint64_t m = (lane < 8 && !(j & 1)) ? (a * bq ^ __umul64hi(a, bq)) : 0;
-#pragma unroll
-		for (int o = 2; o < 8; o <<= 1) {
-			const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), o);
-			m += ((uint64_t)hi << 32) | lo;
-		}
-		uint64_t h = len * P64_1 + m;
-		h ^= h >> 37;
-		h *= 0x165667919E3779F9ull;
-		h ^= h >> 32;
-		if (lane == 0) S.out[idx] = h;
-	};
-	// The batch's longest chains set this kernel's time, so they start first,
-	// each on a wave of its own (the planner's list of buffers of kXBig blocks
-	// or more); the other buffers go to the waves without one, in entry order.
-	const uint64_t W = gridDim.x, w = blockIdx.x;
-	for (uint64_t q = w; q < nbig; q += W) chain(rdf64(gld64(S.big + q)));
-	const bool apart = nbig < W && W - nbig >= W / 4;  // enough waves without a long chain
-	const uint64_t w0 = apart ? nbig : 0, nw = apart ? W - nbig : W;
-	if (w < w0) return;
-	for (uint64_t e = w - w0; e < nsplit; e += nw) {
-		const uint64_t len = rdf64(gld64(&S.ents[e].len));
-		if (((len - 1) >> 10) + 1 < kXBig) chain(e);
 	}
 }
 
-static int xsplit_a_bpc() {
-	static const int bpc = [] {
-		int a = 0, b = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xsplit_a<false>, 256, 0) != hipSuccess) a = 3;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_xsplit_a<true>, 256, 0) != hipSuccess) b = 3;
-		a = a < b ? a : b;
-		const int c = 2 * xxh3_blocks_per_cu();  // (the workspace holds twice the row kernel's wave count of starts)
-		a = a < c ? a : c;
-		return a < 1 ? 1 : a;
-	}();
-	return bpc;
-}
 
-uint64_t xxh3_split_waves(int num_cus) { return (uint64_t)num_cus * xsplit_a_bpc() * 4; }
-
-int launch_xxh3_split(const XSplit& S, int num_cus, bool seeds, hipStream_t stream) {
-	const unsigned ga = (unsigned)((S.nwa + 3) / 4);
-	if (ga == 0) return 0;
+int launch_xxh3_long(const XLong& S, int num_cus, bool seeds, hipStream_t stream) {
 	if (seeds)
-		k_xsplit_a<true><<<ga, 256, 0, stream>>>(S);
+		k_xlong<true><<<(unsigned)num_cus, 1024, 0, stream>>>(S);
 	else
-		k_xsplit_a<false><<<ga, 256, 0, stream>>>(S);
-	k_xsplit_b<<<(unsigned)num_cus * 8, 64, 0, stream>>>(S);  // two chains per SIMD: ~full speed each
+		k_xlong<false><<<(unsigned)num_cus, 1024, 0, stream>>>(S);
 	return 0;
 }
 

@@ -51,69 +51,33 @@ def test_planner_covers_every_wave():
         assert (np.diff(wf) >= 0).all() and wf[-1] == n
 
 
-# ---- split route layout (k_xplan / k_xscan / k_xassign, then k_xsplit_a's shares)
-SPLIT_MIN, PIECE = 16384, 64
+# ---- long-buffer route (k_xplan / k_xscan / k_xassign, then k_xlong's order)
+SPLIT_MIN, NCLASS = 16384, 16
 
 
-def split_plan(lengths, capD, nwa):
-    """Restates the planner's split layout: the buffers over 16 KiB go to the
-    split route if all their blocks / pieces / entries fit the room (else
-    none does), pieces in buffer order at their flat D
-    positions, and phase-A wave w's start (piece << 6 | block) for its share
-    [w*pb, (w+1)*pb) of D."""
-    capS = capD // 16 + 1 if capD else 0
-    capP = capD // PIECE + capS if capD else 0
-    n = lengths.size
+def size_class(nb):
+    """xp_class: 0 for 2^19 blocks or more, then one per power of two down to 15."""
+    lg = int(nb).bit_length() - 1
+    return 0 if lg >= 19 else 19 - max(lg, 4)
+
+
+def long_plan(lengths, capS):
+    """Restates the planner's long route: every buffer over 16 KiB or none
+    (the entries must fit the room), entries grouped by size class, largest
+    class first, and the row kernel's costs with the routed buffers at 64."""
     lg = lengths > SPLIT_MIN
-    nb = np.where(lg, (lengths - 1) // 1024 + 1, 0).astype(np.int64)
-    npc = (nb + PIECE - 1) // PIECE
-    # every split candidate or none (k_xscan)
-    tb_all, tp_all, ts_all = int(nb.sum()), int(npc.sum()), int(lg.sum())
-    fits = tb_all == 0 or (capD > 0 and tb_all <= capD and tp_all <= capP and ts_all <= capS)
-    split = lg & fits
-    nbs = np.where(split, nb, 0)
-    F = np.concatenate([[0], np.cumsum(nbs)[:-1]])
-    pcs = []  # (buffer, first block, blocks, d)
-    for i in np.nonzero(split)[0]:
-        for j in range(int(npc[i])):
-            b0 = PIECE * j
-            pcs.append((int(i), b0, min(PIECE, int(nb[i]) - b0), int(F[i]) + b0))
-    tb = int(nbs.sum())
-    pb = (tb + nwa - 1) // nwa if nwa else 0
-    astart = [None] * nwa
-    pstart = 0
-    for i in np.nonzero(split)[0]:
-        w = (int(F[i]) + pb - 1) // pb
-        while w * pb < int(F[i]) + int(nb[i]) and w < nwa:
-            off = w * pb - int(F[i])
-            astart[w] = (pstart + off // PIECE, off % PIECE)
-            w += 1
-        pstart += int(npc[i])
-    return split, F, pcs, tb, pb, astart
+    nlong = int(lg.sum())
+    routed = nlong != 0 and capS > 0 and nlong <= capS
+    cls = [size_class((int(x) - 1) // 1024 + 1) if l else -1 for x, l in zip(lengths, lg)]
+    order = sorted((i for i in range(lengths.size) if routed and lg[i]), key=lambda i: cls[i])
+    cost = np.where(lg & routed, 64, lengths + 64)
+    return routed, order, cost, cls
 
 
-def phase_a_rows(pcs, tb, pb, astart, w):
-    """The (buffer, block, D index) rows wave w computes (k_xsplit_a's load cursor)."""
-    if astart[w] is None:
-        return []
-    lq, lpos = astart[w]
-    rem = min((w + 1) * pb, tb) - w * pb
-    rows = []
-    while rem:
-        buf, b0, nbk, d = pcs[lq]
-        n = min(nbk - lpos, 4, rem)
-        rows += [(buf, b0 + lpos + r, d + lpos + r) for r in range(n)]
-        lpos += n
-        rem -= n
-        if lpos >= nbk and rem:
-            lq, lpos = lq + 1, 0
-    return rows
-
-
-def test_split_layout_phase_a_shares_cover_d_once():
+def test_long_route_entries_by_size_class():
     rng = np.random.default_rng(17)
     for trial in range(40):
-        n = int(rng.integers(1, 2000))
+        n = int(rng.integers(1, 3000))
         kind = trial % 4
         if kind == 0:
             lens = np.exp(rng.uniform(np.log(4096), np.log(1 << 20), n)).astype(np.int64)
@@ -123,16 +87,18 @@ def test_split_layout_phase_a_shares_cover_d_once():
             lens = np.where(rng.random(n) < 0.02, rng.integers(1 << 20, 8 << 20, n), rng.integers(0, 20000, n))
         else:
             lens = np.full(n, 16385 + int(rng.integers(0, 3000)))
-        need = int(np.where(lens > SPLIT_MIN, (lens - 1) // 1024 + 1, 0).sum())
-        capD = int(rng.choice([0, max(256, need), max(256, need // 2), 10 ** 9]))
-        nwa = int(rng.choice([4, 768, 3072]))
-        split, F, pcs, tb, pb, astart = split_plan(lens, capD, nwa)
-        assert tb <= max(capD, 0)
-        seen = np.zeros(tb, dtype=np.int64)
-        for w in range(nwa):
-            for buf, blk, d in phase_a_rows(pcs, tb, pb, astart, w):
-                assert split[buf] and d == F[buf] + blk and blk <= (lens[buf] - 1) // 1024
-                seen[d] += 1
-        assert (seen == 1).all(), "a stripe-sum block computed twice or never"
-        if capD >= need:
-            assert split.sum() == (lens > SPLIT_MIN).sum() or capD == 0
+        nlong = int((lens > SPLIT_MIN).sum())
+        capS = int(rng.choice([0, nlong, max(1, nlong // 2), 10 ** 9]))
+        routed, order, cost, cls = long_plan(lens, capS)
+        if routed:
+            assert sorted(order) == list(np.nonzero(lens > SPLIT_MIN)[0])
+            assert [cls[i] for i in order] == sorted(cls[i] for i in order)
+            # a class's buffers are within a factor of two of each other (largest first)
+            blocks = [(int(lens[i]) - 1) // 1024 + 1 for i in order]
+            for a, b in zip(blocks, blocks[1:]):
+                assert b < 2 * a or cls[order[0]] == 0
+        else:
+            assert order == [] and (cost == lens + 64).all()
+        # the row kernel's waves still cover every buffer (the cost model above)
+        wf, start, q = plan(cost - 64, 64)
+        assert (wf >= 0).all() and wf[-1] == n
