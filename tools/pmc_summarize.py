@@ -81,13 +81,14 @@ def main(mode="pages4k", workload="pages4k", kernel=("k_pages4k",), algorithmic=
                                           "per_unit")}))
 
 
-def _varlen(fn):
-    """Algorithmic bytes of a bench_workloads varlen batch: data + 20 B per buffer."""
+def _varlen(fn, per_buffer=20):
+    """Algorithmic bytes of a bench_workloads varlen batch: data + 20 B per
+    buffer (CRC: offset, length, 4-byte checksum; XXH3: 24 B, an 8-byte digest)."""
     def f():
         sys.path.insert(0, ROOT)
         import bench_workloads as W
         lens = getattr(W, fn)()
-        return int(lens.sum()) + 20 * lens.size, lens.size
+        return int(lens.sum()) + per_buffer * lens.size, lens.size
     return f
 
 
@@ -98,6 +99,8 @@ PRESETS = {
     "xxh3": ("xxh3", "xxh3-pages4k", ("k_xxh3_rows",), (1 << 20) * (4088 + 8), 1 << 20),
     "zipf": ("zipf", "zipf", VARLEN_KERNELS, _varlen("zipf_lengths"), None),
     "chunks": ("chunks", "chunks", VARLEN_KERNELS, _varlen("chunk_lengths"), None),
+    "xchunks": ("xchunks", "xxh3-chunks", ("k_xplan", "k_xscan", "k_xassign", "k_xlong", "k_xxh3_vrows"),
+                _varlen("chunk_lengths", 24), None),
 }
 
 if __name__ == "__main__":
