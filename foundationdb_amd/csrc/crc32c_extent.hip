@@ -40,6 +40,7 @@
 //               a batch that failed the checks: every buffer directly, one
 //               lane each (x_fallback)
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "crc32c_common.h"
@@ -384,13 +385,16 @@ __device__ __forceinline__ uint32_t xmul_blocks(const DevTables* T, uint32_t v, 
 // then the point registers and remainder bytes) instead of one per multiply.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kFinThreads = 1024;
-constexpr uint32_t kFinXinv = 0;                        // xinv64[65]
-constexpr uint32_t kFinPow1 = kFinXinv + 65 * 128;      // pow1[64]
-constexpr uint32_t kFinPow64 = kFinPow1 + 64 * 128;     // pow64[64]
-constexpr uint32_t kFinBp0 = kFinPow64 + 64 * 128;      // bpow[0][0..63]
+constexpr uint32_t kFinXinv = 0;                        // xinv64[65]  } in DevTables' order: one
+constexpr uint32_t kFinPow64 = kFinXinv + 65 * 128;     // pow64[64]   } contiguous copy
+constexpr uint32_t kFinPow1 = kFinPow64 + 64 * 128;     // pow1[64]    }
+constexpr uint32_t kFinBp0 = kFinPow1 + 64 * 128;       // bpow[0][0..63]
 constexpr uint32_t kFinS4 = kFinBp0 + 64 * 128;         // slice4[4][256]
 constexpr uint32_t kFinC = kFinS4 + 4 * 256;            // M^per (built per launch)
 constexpr uint32_t kFinWords = kFinC + 128;             // 34048 words = 133 KiB
+static_assert(offsetof(DevTables, pow64) == offsetof(DevTables, xinv64) + sizeof(uint32_t) * 65 * 128 &&
+                  offsetof(DevTables, pow1) == offsetof(DevTables, pow64) + sizeof(uint32_t) * 64 * 128,
+              "xinv64, pow64, pow1 are contiguous");
 
 __device__ __forceinline__ uint32_t lmul(const uint32_t* lds, uint32_t tab, uint32_t v) {
 	uint32_t r = 0;
@@ -399,19 +403,34 @@ __device__ __forceinline__ uint32_t lmul(const uint32_t* lds, uint32_t tab, uint
 	return r;
 }
 
+// The finishing kernel's LDS tables: every 16-byte load of the three copies
+// issued before any LDS write (clamped addresses, so no load sits behind a
+// branch), one L2 round trip instead of one per copy-loop iteration.
 __device__ __forceinline__ void fin_fill(uint32_t* lds, const DevTables* T) {
 	typedef __attribute__((address_space(1))) const u32x4 gq;
-	auto cp = [&](uint32_t dst, const uint32_t* src, uint32_t words) {
-		u32x4* d = reinterpret_cast<u32x4*>(lds + dst);
-		const gq* sq = (const gq*)reinterpret_cast<uintptr_t>(src);
-		for (uint32_t q = threadIdx.x; q < words / 4; q += blockDim.x) d[q] = sq[q];
-	};
-	cp(kFinXinv, &T->xinv64[0][0][0], 65 * 128);
-	cp(kFinPow1, &T->pow1[0][0][0], 64 * 128);
-	cp(kFinPow64, &T->pow64[0][0][0], 64 * 128);
-	cp(kFinBp0, &T->bpow[0][0][0][0], 64 * 128);
-	cp(kFinS4, &T->slice4[0][0], 4 * 256);
-	__syncthreads();
+	constexpr uint32_t NA = 193 * 32, NB = 64 * 32, NC = 256;  // quads: xinv64..pow1, bpow[0][0..63], slice4
+	constexpr uint32_t IA = (NA + kFinThreads - 1) / kFinThreads, IB = NB / kFinThreads;
+	static_assert(NB % kFinThreads == 0 && NC <= kFinThreads, "copy shapes");
+	const gq* sa = (const gq*)reinterpret_cast<uintptr_t>(&T->xinv64[0][0][0]);
+	const gq* sb = (const gq*)reinterpret_cast<uintptr_t>(&T->bpow[0][0][0][0]);
+	const gq* sc = (const gq*)reinterpret_cast<uintptr_t>(&T->slice4[0][0]);
+	const uint32_t t = threadIdx.x;
+	u32x4 a[IA], b[IB], c;
+#pragma unroll
+	for (uint32_t i = 0; i < IA; ++i) {
+		const uint32_t q = t + kFinThreads * i;
+		a[i] = sa[q < NA ? q : NA - 1];
+	}
+#pragma unroll
+	for (uint32_t i = 0; i < IB; ++i) b[i] = sb[t + kFinThreads * i];
+	c = sc[t < NC ? t : NC - 1];
+	u32x4* d = reinterpret_cast<u32x4*>(lds);
+#pragma unroll
+	for (uint32_t i = 0; i < IA; ++i)
+		if (t + kFinThreads * i < NA) d[kFinXinv / 4 + t + kFinThreads * i] = a[i];
+#pragma unroll
+	for (uint32_t i = 0; i < IB; ++i) d[kFinBp0 / 4 + t + kFinThreads * i] = b[i];
+	if (t < NC) d[kFinS4 / 4 + t] = c;
 }
 
 // The batch failed the packing or capacity check (k_v7count): every lane
@@ -459,6 +478,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	const XGeo G = x_geo(P);
 	const uint64_t per = x_per(G.nblk, P.nwave);
 	const uint32_t* s4 = lds + kFinS4;
+	fin_fill(lds, T);
 	// nibble tables of C = M^per (the range stride), for the straddling
 	// buffers' aggregate chains: entry [n][v] = (v x^4n) * C, bit by bit
 	if (threadIdx.x < 128) {
@@ -471,7 +491,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		}
 		lds[kFinC + threadIdx.x] = r;
 	}
-	fin_fill(lds, T);
+	__syncthreads();
 	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t i = i0 + threadIdx.x;
 		const bool ok = i < P.count;

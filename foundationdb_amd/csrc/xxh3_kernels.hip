@@ -768,16 +768,19 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 		add_dpp<0x128>(lo1, hi1);
 		a0 += ((uint64_t)hi0 << 32) | lo0;
 		a1 += ((uint64_t)hi1 << 32) | lo1;
-		const uint64_t m = mulfold(a0 ^ K.g0, a1 ^ K.g1);
-		uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
-		add_dpp<0xB1>(lo, hi);
-		add_dpp<0x4E>(lo, hi);
-		const uint64_t h = xxh3_aval(S.len * P64_1 + (((uint64_t)hi << 32) | lo));
+		uint64_t done = __ballot(l == 0 && fin && S.act);
+		uint64_t h = 0;
+		if (done != 0) {  // some row's buffer ends at this block: the merge (uniform branch, most steps skip it)
+			const uint64_t m = mulfold(a0 ^ K.g0, a1 ^ K.g1);
+			uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+			add_dpp<0xB1>(lo, hi);
+			add_dpp<0x4E>(lo, hi);
+			h = xxh3_aval(S.len * P64_1 + (((uint64_t)hi << 32) | lo));
+		}
 		if (!fin) {
 			a0 = ((a0 ^ (a0 >> 47)) ^ K.c0) * P32_1;
 			a1 = ((a1 ^ (a1 >> 47)) ^ K.c1) * P32_1;
 		}
-		uint64_t done = __ballot(l == 0 && fin && S.act);
 		while (done != 0) {
 			const int src = __builtin_ctzll(done);
 			done &= done - 1;
