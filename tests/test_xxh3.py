@@ -339,3 +339,29 @@ def test_gpu_xxh3_split_route_fixed_and_chained(cuda):
     ref = O.ref_xxh3_64 if O.xxh3_reference_available() else (lambda b: O.xxh3_64(np.frombuffer(b, np.uint8)))
     for c in range(3):
         assert int(got[c]) == ref(cat(c)), c
+
+
+@pytest.mark.gpu
+def test_gpu_xxh3_long_route_reuses_slots(cuda):
+    """More long buffers than k_xlong has chain slots (4 per CU): every slot
+    takes several buffers in turn (its LDS ring's step numbers run on across
+    buffers), largest first, over packed, overlapping and unaligned offsets;
+    per-buffer seeds and a uniform one; twice on one stream (the dequeue
+    counter and class cursors are re-planned per launch)."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    rng = np.random.default_rng(2068)
+    h = O.splitmix64((96 << 20) // 8, 0x5107).view(np.uint8)
+    d = torch.from_numpy(h).to(cuda)
+    n = 3000
+    lens = np.exp(rng.uniform(np.log(16385), np.log(96 << 10), n)).astype(np.int64)
+    lens[:40] = 16385 + rng.integers(0, 4096, 40)  # the smallest class, many per slot
+    offs = np.array([int(rng.integers(0, h.size - L + 1)) for L in lens], dtype=np.int64)
+    seeds = rng.integers(0, 2 ** 63, n, dtype=np.int64)
+    want = O.xxh3_batch_varlen(h, offs, lens, seed=0xFDBEEFDB)
+    want_s = O.xxh3_batch_varlen(h, offs, lens, seeds=seeds.view(np.uint64))
+    o, l, sd = i64(offs, cuda), i64(lens, cuda), torch.from_numpy(seeds).to(cuda)
+    ws = torch.empty(X.varlen_workspace_bytes(n, int(lens.sum())), dtype=torch.uint8, device=cuda)
+    for _ in range(2):
+        assert np.array_equal(host(X.batch_varlen(d, o, l, seed=0xFDBEEFDB, workspace=ws)), want)
+        assert np.array_equal(host(X.batch_varlen(d, o, l, seeds=sd, workspace=ws)), want_s)
