@@ -365,3 +365,30 @@ def test_gpu_xxh3_long_route_reuses_slots(cuda):
     for _ in range(2):
         assert np.array_equal(host(X.batch_varlen(d, o, l, seed=0xFDBEEFDB, workspace=ws)), want)
         assert np.array_equal(host(X.batch_varlen(d, o, l, seeds=sd, workspace=ws)), want_s)
+
+
+@pytest.mark.gpu
+def test_gpu_xxh3_long_route_planner_forms(cuda):
+    """Long buffers among tens of thousands of short ones: at 256 tiles of
+    256 buffers (65536) the planner's assign pass reduces the tiles itself
+    (no k_xscan, class bases from the earlier tiles' counts), past that it
+    takes the separate scan; both against the oracle, uniform and per-buffer
+    seeds."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    rng = np.random.default_rng(1087)
+    h = O.splitmix64((48 << 20) // 8, 0x1087).view(np.uint8)
+    d = torch.from_numpy(h).to(cuda)
+    for count in (65536, 70001):
+        lens = rng.integers(0, 600, count).astype(np.int64)
+        where = rng.choice(count, 60, replace=False)
+        lens[where] = rng.integers(16385, 400000, where.size)
+        lens[where[:3]] = [16385, 1 << 20, 17409]
+        offs = rng.integers(0, h.size - lens.max() - 1, count).astype(np.int64)
+        seeds = rng.integers(0, 2 ** 63, count, dtype=np.int64)
+        o, l, sd = i64(offs, cuda), i64(lens, cuda), torch.from_numpy(seeds).to(cuda)
+        ws = torch.empty(X.varlen_workspace_bytes(count, int(lens.sum())), dtype=torch.uint8, device=cuda)
+        want = O.xxh3_batch_varlen(h, offs, lens)
+        assert np.array_equal(host(X.batch_varlen(d, o, l, workspace=ws)), want), count
+        want_s = O.xxh3_batch_varlen(h, offs, lens, seeds=seeds.view(np.uint64))
+        assert np.array_equal(host(X.batch_varlen(d, o, l, seeds=sd, workspace=ws)), want_s), count
