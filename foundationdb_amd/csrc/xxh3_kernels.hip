@@ -1096,7 +1096,10 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 			uint64_t b = 0;
 #pragma unroll
 			for (uint32_t c = 0; c < kXClasses; ++c) b += c < t ? cnt[c] : 0;
-			cbase[t] = b + ((tot[8 + (t >> 1)] >> (32 * (t & 1))) & 0xFFFFFFFFull);
+			uint64_t e = 0;  // (selects, not a register index: that would go to scratch)
+#pragma unroll
+			for (uint32_t w = 0; w < 8; ++w) e = (t >> 1) == w ? tot[8 + w] : e;
+			cbase[t] = b + ((e >> (32 * (t & 1))) & 0xFFFFFFFFull);
 		}
 		if (blockIdx.x == 0 && t == 0) {
 			Q.sh[0] = routed ? nlong : 0;
