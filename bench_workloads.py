@@ -166,7 +166,8 @@ def _spot_check(buf, offsets, lengths, seed, got, n=512):
 
 
 class VarLen:
-    kernel_name = "varlen engine: fdbcrc::k_v7count + k_v7prep + the batch's route (k_bigblocks 4 KiB blocks and/or k_varlen7 1 KiB windows)"
+    kernel_name = ("varlen engine, the batch's route: extent (k_v7count + k_xstream + k_xz + k_xfin), "
+                   "blocks (k_v7prep_b + k_bigblocks) or windows (k_v7prep_w + k_varlen7)")
 
     def __init__(self, dev, rank, lengths, align, desc, seed=0, metric=None, shape=None):
         self.dev, self.seed = dev, seed
@@ -555,7 +556,7 @@ class Xxh3Zipf(VarLen):
     """XXH3-64 of every packet of the configs[2] Zipf batch (FlowTransport packet
     checksum, fdbrpc/FlowTransport.cpp:2025-2068), device-resident."""
     metric = "device-resident XXH3-64 GiB/s on Zipf 64 B-16 KiB packet batches; % of HBM-read peak"
-    kernel_name = "fdbxxh::k_xxh3 (+ planner)"
+    kernel_name = "fdbxxh planner (k_xplan + k_xscan + k_xassign) + k_xxh3_vrows"
 
     def __init__(self, dev, rank):
         import foundationdb_amd.xxh3 as X
@@ -594,7 +595,7 @@ class Xxh3Chunks(Xxh3Zipf):
     log-uniform), device-resident: the split route for every chunk over 16 KiB
     (xxh3_split.hip), the row kernel for the rest."""
     metric = "device-resident XXH3-64 GiB/s on 4 KiB-1 MiB chunk batches; % of HBM-read peak"
-    kernel_name = "fdbxxh planner + k_xsplit_a (stripe sums) + k_xsplit_b (chains) + k_xxh3_vrows"
+    kernel_name = "fdbxxh planner (k_xplan + k_xassign) + k_xlong (buffers over 16 KiB) + k_xxh3_vrows"
 
     def __init__(self, dev, rank):
         import foundationdb_amd.xxh3 as X
