@@ -38,7 +38,7 @@ struct StreamState {
 	uint64_t* hst_d = nullptr;  // ... its device address
 	// extent route state (crc32c_extent.hip): grown to the batches seen
 	void* xmem = nullptr;
-	uint64_t xcount = 0, xblk = 0;  // buffers and extent blocks it holds
+	uint64_t xcount = 0;            // buffers it holds
 	uint32_t xepoch = 0;            // launches on the extent route (epoch tags, never 0)
 };
 
@@ -181,33 +181,23 @@ int stream_route(DeviceState* st, hipStream_t s, uint64_t** hstat) {
 }
 
 // The stream's extent-route state for a batch of `count` buffers (caller
-// holds the stream's lock).  Sized for the extent the stream's last checked
-// batch needed (hstat, written by the device) with headroom; a batch whose
-// extent is larger than what is held is routed to the window engine on the
-// device (the capacity flag) and the next call grows the state.  false: no
-// state (allocation failed): the caller routes to the window engine.
+// holds the stream's lock): per-buffer point values and per-wave aggregates,
+// grown to the largest batch seen.  false: no state (allocation failed): the
+// caller routes to the window engine.
 bool stream_extent(DeviceState* st, hipStream_t s, uint64_t count, XState* xs) {
 	StreamState* ss = stream_state(st, s);
-	constexpr uint64_t kMaxBlk = 1ull << 26;  // 256 GiB extents
-	uint64_t need = ss->hst_h ? ss->hst_h[kHstatNblk] : 0;
-	need = need > kMaxBlk ? kMaxBlk : need;
-	if (!ss->xmem || count > ss->xcount || need > ss->xblk) {
+	if (!ss->xmem || count > ss->xcount) {
 		if (ss->xmem) {
 			if (hipStreamSynchronize(s) != hipSuccess) return false;
 			(void)hipFree(ss->xmem);
 			ss->xmem = nullptr;
 		}
-		uint64_t nc = count > ss->xcount ? count + count / 4 : ss->xcount;
-		uint64_t nb = need + need / 4;
-		const uint64_t guess = count * 16 > 65536 ? count * 16 : 65536;  // first batch: 64 KiB per buffer
-		nb = nb > guess ? nb : guess;
-		nb = nb > ss->xblk ? nb : ss->xblk;
-		nb = nb > kMaxBlk ? kMaxBlk : nb;
+		const uint64_t nc = count + count / 4;
 		void* m = nullptr;
-		const uint64_t bytes = extent_state_bytes(nc, nb, st->num_cus);
+		const uint64_t bytes = extent_state_bytes(nc, st->num_cus);
 		if (hipMalloc(&m, bytes) != hipSuccess) {
 			(void)hipGetLastError();
-			ss->xcount = ss->xblk = 0;
+			ss->xcount = 0;
 			return false;
 		}
 		if (hipMemsetAsync(m, 0, 256, s) != hipSuccess) {  // the epoch-tagged flags
@@ -216,9 +206,8 @@ bool stream_extent(DeviceState* st, hipStream_t s, uint64_t count, XState* xs) {
 		}
 		ss->xmem = m;
 		ss->xcount = nc;
-		ss->xblk = nb;
 	}
-	extent_state_carve(ss->xmem, ss->xcount, ss->xblk, st->num_cus, xs);
+	extent_state_carve(ss->xmem, ss->xcount, st->num_cus, xs);
 	if (++ss->xepoch == 0) ++ss->xepoch;
 	xs->epoch = ss->xepoch;
 	return true;
@@ -288,7 +277,7 @@ uint64_t stream_bytes(hipStream_t stream) {
 	auto it = st->streams.find(stream);
 	if (it == st->streams.end()) return 0;
 	return it->second->ws_bytes + it->second->ctr_bytes +
-	       (it->second->xmem ? extent_state_bytes(it->second->xcount, it->second->xblk, st->num_cus) : 0);
+	       (it->second->xmem ? extent_state_bytes(it->second->xcount, st->num_cus) : 0);
 }
 
 // used by the host pipeline (crc32c_pipeline.cpp)
@@ -572,7 +561,7 @@ uint64_t xxh3_gpu_varlen_workspace_bytes_for(uint64_t count, uint64_t total_byte
 
 static int xxh3_varlen_impl(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                             uint64_t seed, const uint64_t* d_seeds, uint64_t* d_out, void* d_workspace,
-                            uint64_t workspace_bytes, void* stream, uint64_t* hneed) {
+                            uint64_t workspace_bytes, void* stream, uint64_t* hneed, uint32_t* err = nullptr) {
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths || !d_base)
 		return fail(FDB_CRC32C_EINVAL, "xxh3_gpu_batch_varlen: null pointer");
@@ -591,6 +580,7 @@ static int xxh3_varlen_impl(const void* d_base, const uint64_t* d_offsets, const
 	P.out = d_out;
 	P.ws_bytes = workspace_bytes;
 	P.hneed = hneed;
+	P.err = err;
 	if (fdbxxh::launch_xxh3(P, st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream)))
 		return fail(FDB_CRC32C_EHIP, "xxh3_gpu_batch_varlen: launch setup failed");
 	return check_launch("xxh3_gpu_batch_varlen launch");
@@ -630,7 +620,8 @@ int xxh3_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const u
 	if (int rc = stream_workspace(st, s, want, &ws, &have, &hold)) return rc;
 	// (the room asked for, not the whole workspace: no long buffers last time, no split launches now)
 	return xxh3_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, want < have ? want : have,
-	                        stream, mapped ? ss->hst_d + kHstatXxhNeed : nullptr);
+	                        stream, mapped ? ss->hst_d + kHstatXxhNeed : nullptr,
+	                        mapped ? reinterpret_cast<uint32_t*>(ss->hst_d + kHstatErr) : nullptr);
 }
 
 uint64_t xxh3_gpu_chained_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes) {
@@ -770,8 +761,12 @@ int crc32c_gpu_stream_status(void* stream) {
 	std::lock_guard<std::mutex> lock(g_mu);
 	if (!ss->hst_h) return 0;
 	volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(ss->hst_h + kHstatErr);
-	if (!*w) return 0;
+	const uint32_t v = *w;
+	if (!v) return 0;
 	*w = 0;
+	if (v == fdbxxh::kErrXxhStall)
+		return fail(FDB_CRC32C_EHIP, "an XXH3 batch on this stream stalled on the device (a long-route wait ran out); "
+		                             "some of its digests were not written");
 	return fail(FDB_CRC32C_EINVAL, "a variable-length batch on this stream was refused: it covered 2^32 - 1 or more "
 	                               "1 KiB windows (or 4 KiB blocks); its checksums are undefined");
 }

@@ -88,22 +88,20 @@ inline int route_for_stats(const volatile uint64_t* s) {
 }
 // Extent route state of one stream (device memory owned by the library):
 // xhdr[0] the epoch of the last launch whose batch was found not packed,
-// xhdr[1] the epoch of the last launch whose extent exceeded the capacity;
-// per buffer the start / end point registers; per 4 KiB block of the extent
-// the range-local prefix Z; per wave of the streaming kernel its range's
-// aggregate register.
+// xhdr[1] the epoch of the last launch whose extent exceeded kXMaxExtent;
+// per buffer its start and end points' captured values {G, Y}; per wave of
+// the streaming kernel its range's aggregate register.
+constexpr uint64_t kXMaxExtent = 1ull << 40;  // 32-bit block numbers with room
 struct XState {
 	uint32_t* xhdr;
-	uint32_t* vs;
-	uint32_t* ve;
+	uint32_t* ps;         // per buffer, 2 words: its start point's G and Y (k_xstream)
+	uint32_t* pe;         // ... its end point's
 	uint32_t* dummy;      // 128 words per wave of the stream kernel
-	uint32_t* zb;         // per block: X_k * x^(8*4096), X_k the range-local prefix at the block's start
 	uint32_t* ragg;       // per stream wave: the range-local prefix at its range's end
-	uint64_t cap_blk;     // blocks the arrays hold
 	uint32_t epoch;       // this launch (never 0)
 };
-uint64_t extent_state_bytes(uint64_t count, uint64_t cap_blk, int num_cus);
-void extent_state_carve(void* mem, uint64_t count, uint64_t cap_blk, int num_cus, XState* x);
+uint64_t extent_state_bytes(uint64_t count, int num_cus);
+void extent_state_carve(void* mem, uint64_t count, int num_cus, XState* x);
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 // err (device-visible, may be null): set to 1 (never cleared here) when the
 // planner refuses the batch -- 2^32 - 1 or more 1 KiB windows or 4 KiB route

@@ -191,8 +191,10 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 		}
 		q = qa + __builtin_popcountll(__ballot(le));
 	}
-	uint32_t wbs, wbe, wcs, wce, wlast;  // per lane: start / end blocks and spans; uniform: last end block
-	uint32_t Vs = 0, Ve = 0;
+	// per lane: start / end blocks, whole lane spans before each point and the
+	// 16-byte chunk of its span it lies in; uniform: the window's last end block
+	uint32_t wbs, wbe, wcs, wce, wqs, wqe, wlast;
+	uint32_t Vs = 0, Ve = 0, Ys = 0, Ye = 0;  // captured: G(p) and the span's register at p's chunk
 	uint64_t pf0 = 0, pf1 = 0;  // the next window's buffer (prefetched one window ahead)
 	auto prefetch = [&](uint64_t q0) {
 		const uint64_t j = q0 + lane < P.count ? q0 + lane : P.count - 1;
@@ -205,9 +207,10 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 		wbe = ok ? x_blk(e) : 0xFFFFFFFEu;
 		wcs = x_cnt(s, wbs);
 		wce = x_cnt(e, wbe);
+		wqs = ((uint32_t)s >> 4) & 3u;  // (p - 4096k - 64 cnt) >> 4: S is 16-byte aligned
+		wqe = ((uint32_t)e >> 4) & 3u;
 		wlast = q0 + 64 <= P.count ? rdlane(wbe, 63) : 0xFFFFFFFFu;  // the batch's last window never retires
-		Vs = 0;
-		Ve = 0;
+		Vs = Ve = Ys = Ye = 0;
 	};
 	uint32_t* const dmy = P.x.dummy + 128 * w;
 	// the window's points that lie in this wave's blocks leave (the others
@@ -215,8 +218,9 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 	auto flush = [&](uint64_t q0) {
 		const bool ok = q0 + lane < P.count;
 		const bool os = ok && wbs >= k0 && wbs < k1, oe = ok && wbe >= k0 && wbe < k1;
-		*(os ? P.x.vs + q0 + lane : dmy + lane) = Vs;
-		*(oe ? P.x.ve + q0 + lane : dmy + 64 + lane) = Ve;
+		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+		*reinterpret_cast<u32x2*>(os ? P.x.ps + 2 * (q0 + lane) : dmy + 2 * lane) = u32x2{Vs, Ys};
+		*reinterpret_cast<u32x2*>(oe ? P.x.pe + 2 * (q0 + lane) : dmy + 2 * lane) = u32x2{Ve, Ye};
 	};
 	prefetch(q);
 	make_window(q);
@@ -226,13 +230,28 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 	if (k0 >= k1) return;
 
 	// ---- blocks -------------------------------------------------------------
-	uint32_t mine = 0;       // lane k - gs: register of block k of the current group
-	uint64_t gs = k0;        // first block of the group
-	auto store_group = [&](uint64_t n) {  // the block registers B (k_xz turns them into Z in place)
-		*((uint64_t)lane < n ? P.x.zb + gs + lane : dmy + lane) = mine;
+	// X: the range-local prefix register at the start of the next block (0 at
+	// k0).  Per block: Z = X * M (M = x^(8*4096)), X = Z ^ B.  The uniform
+	// multiply by M chains two of the lane tables already in LDS -- lane 0's
+	// x^(8*64*63) and lane 62's x^(8*64) -- eight lanes per table (lane n:
+	// nibble n; all 64 lanes run it, lanes n and n + 8k read the same word).
+	uint32_t X = 0;
+	auto mulM = [&](uint32_t v) -> uint32_t {
+		const uint32_t n = lane & 7;
+		uint32_t t = lds_rd(lds, kS4LaneOff + ((n * 16 + ((v >> (4 * n)) & 15u)) << 7));
+		t ^= __builtin_amdgcn_update_dpp(0u, t, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+		t ^= __builtin_amdgcn_update_dpp(0u, t, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+		t ^= __builtin_amdgcn_update_dpp(0u, t, 0x124, 0xF, 0xF, false);  // row_ror:4 (n ^ 4)
+		t = rdfirst(t);
+		uint32_t u = lds_rd(lds, kS4LaneOff + 4 * (4096 + (n * 16 + ((t >> (4 * n)) & 15u)) * 32 + 30));
+		u ^= __builtin_amdgcn_update_dpp(0u, u, 0xB1, 0xF, 0xF, false);
+		u ^= __builtin_amdgcn_update_dpp(0u, u, 0x4E, 0xF, 0xF, false);
+		u ^= __builtin_amdgcn_update_dpp(0u, u, 0x124, 0xF, 0xF, false);
+		return rdfirst(u);
 	};
-	// chains, lane weights and the prefix XOR over the lanes of one unit
-	auto unit_h = [&](Block (&u)[kXU], uint32_t (&H)[kXU]) {
+	// chains, lane weights and the prefix XOR over the lanes of one unit; Y:
+	// each lane's register after 16, 32 and 48 bytes of its span
+	auto unit_h = [&](Block (&u)[kXU], uint32_t (&H)[kXU], uint32_t (&Y)[kXU][3]) {
 		uint32_t x[kXU];
 #pragma unroll
 		for (uint32_t j = 0; j < kXU; ++j) {
@@ -242,28 +261,57 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 #pragma unroll
 		for (int wd = 0; wd < 16; ++wd)
 #pragma unroll
-			for (uint32_t j = 0; j < kXU; ++j)
-				x[j] = word_step4_next(lds, x[j], wd < 15 ? u[j].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u, c4);
+			for (uint32_t j = 0; j < kXU; ++j) {
+				const uint32_t nx = wd < 15 ? u[j].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u;
+				x[j] = word_step4_next(lds, x[j], nx, c4);
+				// after step wd, x = y_(wd+1) ^ word (wd+1): y_4, y_8, y_12
+				if (wd == 3 || wd == 7 || wd == 11) Y[j][(wd >> 2)] = x[j] ^ nx;
+			}
 #pragma unroll
 		for (uint32_t j = 0; j < kXU; ++j) H[j] = wave_scanx(mul_nibbles(lds, x[j], c_lane));
 	};
-	// the window's points in block kb (branch-free: two permutes per block)
-	auto capture = [&](uint32_t H, uint32_t kb, bool valid) {
+	// the window's points in block kb (two permutes per block for G; the span
+	// registers only for points past a span's first chunk -- uniform skip)
+	auto capture = [&](uint32_t H, const uint32_t (&Yb)[3], uint32_t Zb, uint32_t kb, bool valid) {
 		const bool hs = valid && wbs == kb, he = valid && wbe == kb;
 		const uint32_t ts = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((wcs ? wcs - 1 : 0) << 2), (int)H);
 		const uint32_t te = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((wce ? wce - 1 : 0) << 2), (int)H);
-		Vs = hs ? (wcs ? ts : 0u) : Vs;
-		Ve = he ? (wce ? te : 0u) : Ve;
+		Vs = hs ? Zb ^ (wcs ? ts : 0u) : Vs;
+		Ve = he ? Zb ^ (wce ? te : 0u) : Ve;
+		auto pull = [&](uint32_t cnt, uint32_t qd) -> uint32_t {
+			const int a = (int)((cnt & 63u) << 2);
+			const uint32_t y1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)Yb[0]);
+			const uint32_t y2 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)Yb[1]);
+			const uint32_t y3 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)Yb[2]);
+			return qd == 1 ? y1 : qd == 2 ? y2 : qd == 3 ? y3 : 0u;
+		};
+		if (__ballot(hs && wqs)) {
+			const uint32_t y = pull(wcs, wqs);
+			Ys = hs ? y : Ys;
+		}
+#ifdef FDBX_NOPULL
+		if (false) {
+#else
+		if (__ballot(he && wqe)) {
+#endif
+			const uint32_t y = pull(wce, wqe);
+			Ye = he ? y : Ye;
+		}
 	};
 	// the registers and points of blocks k .. k + 2U - 1 (those before kend)
-	auto finish = [&](const uint32_t (&H)[2 * kXU], uint64_t k, uint64_t kend) {
+	auto finish = [&](const uint32_t (&H)[2 * kXU], const uint32_t (&Y)[2 * kXU][3], uint64_t k, uint64_t kend) {
+		uint32_t Z[2 * kXU];
 #pragma unroll
 		for (uint32_t j = 0; j < 2 * kXU; ++j) {
-			const uint32_t B = rdlane(H[j], 63);
-			mine = lane == (uint32_t)(k + j - gs) ? B : mine;
+#ifdef FDBX_NOMUL
+			Z[j] = X;
+#else
+			Z[j] = mulM(X);
+#endif
+			if (k + j < kend) X = Z[j] ^ rdlane(H[j], 63);
 		}
 #pragma unroll
-		for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], (uint32_t)(k + j), k + j < kend);
+		for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], Y[j], Z[j], (uint32_t)(k + j), k + j < kend);
 		const uint64_t kn = k + 2 * kXU < kend ? k + 2 * kXU : kend;
 		// every buffer of the window ends in the blocks done so far: the next 64
 		// (rare for packets of KiBs; these blocks' prefixes are still in
@@ -274,28 +322,24 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 			make_window(q);
 			prefetch(q + 64);
 #pragma unroll
-			for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], (uint32_t)(k + j), k + j < kend);
-		}
-		if (kn - gs >= 64 || kn == kend) {  // a full group, or the range's end
-			store_group(kn - gs);
-			gs = kn;
+			for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], Y[j], Z[j], (uint32_t)(k + j), k + j < kend);
 		}
 	};
 	// two units in ping-pong: one computes while the other's loads are in
 	// flight (a register copy of a block in flight would wait for its loads)
 	for (uint64_t k = k0; k < km; k += 2 * kXU) {
-		uint32_t H[2 * kXU];
+		uint32_t H[2 * kXU], Y[2 * kXU][3];
 #pragma unroll
 		for (uint32_t j = 0; j < kXU; ++j) load_blk(u1[j], k + kXU + j);
 		__builtin_amdgcn_sched_barrier(0);
-		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]));
+		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[0]));
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (uint32_t j = 0; j < kXU; ++j) load_blk(u0[j], k + 2 * kXU + j);
 		__builtin_amdgcn_sched_barrier(0);
-		unit_h(u1, reinterpret_cast<uint32_t(&)[kXU]>(H[kXU]));
+		unit_h(u1, reinterpret_cast<uint32_t(&)[kXU]>(H[kXU]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[kXU]));
 		__builtin_amdgcn_sched_barrier(0);
-		finish(H, k, km);
+		finish(H, Y, k, km);
 	}
 	if (km < k1) {  // the extent's last block: chunks past its end re-read its last chunk (never used)
 		const uint64_t last_chunk = G.Eend - 16;
@@ -306,64 +350,15 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 			u0[0].r[q2] = ld16(reinterpret_cast<const uint8_t*>(o <= last_chunk ? o : last_chunk));
 		}
 		u0[1] = u0[0];
-		uint32_t H[2 * kXU];
-		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]));
+		uint32_t H[2 * kXU], Y[2 * kXU][3];
+		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[0]));
 		H[2] = H[3] = 0;
-		finish(H, km, k1);
+#pragma unroll
+		for (uint32_t j = 0; j < 3; ++j) Y[2][j] = Y[3][j] = 0;
+		finish(H, Y, km, k1);
 	}
 	flush(q);
-}
-
-// ---------------------------------------------------------------------------
-// k_xz: the range-local prefixes, one wave per stream wave's range (the same
-// numbering), lane-parallel per group of 64 blocks from LDS copies of the
-// M^j tables (j <= 32; every lane of a step reads the same table: broadcast,
-// no bank conflicts).  The carry X_gs enters lane 0 as carry * M; a 6-step
-// weighted scan I_j = XOR_{m<=j} v_m * M^(j-m) gives X_{gs+j+1}, so
-//     Z[gs+j] = X_{gs+j+1} ^ B[gs+j]      (in place of B),   A[w] = X_{k1}.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kZTabs = 33;  // bpow[0][0..32]: M^j
-
-__device__ __forceinline__ uint32_t lmulz(const uint32_t* lds, uint32_t j, uint32_t v) {
-	uint32_t r = 0;
-#pragma unroll
-	for (int n = 0; n < 8; ++n) r ^= lds[128 * j + 16 * n + ((v >> (4 * n)) & 15u)];
-	return r;
-}
-
-__global__ __launch_bounds__(1024) void k_xz(XParams P) {
-	__shared__ uint32_t lds[kZTabs * 128];
-	if (!x_packed(P)) return;
-	const XGeo G = x_geo(P);
-	if (G.nblk == 0) return;
-	{
-		typedef __attribute__((address_space(1))) const u32x4 gq;
-		const gq* src = (const gq*)reinterpret_cast<uintptr_t>(&P.tabs->bpow[0][0][0][0]);
-		u32x4* dst = reinterpret_cast<u32x4*>(lds);
-		for (uint32_t q = threadIdx.x; q < kZTabs * 32; q += blockDim.x) dst[q] = src[q];
-	}
-	__syncthreads();
-	const uint32_t lane = threadIdx.x & 63;
-	const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + rdfirst(threadIdx.x >> 6);
-	const uint64_t per = x_per(G.nblk, P.nwave);
-	const uint64_t k0 = w * per < G.nblk ? w * per : G.nblk;
-	const uint64_t k1 = k0 + per < G.nblk ? k0 + per : G.nblk;
-	uint32_t carry = 0;
-	for (uint64_t gs = k0; gs < k1; gs += 64) {
-		const uint64_t n = k1 - gs < 64 ? k1 - gs : 64;
-		const bool in = lane < n;
-		const uint32_t B = xld32(P.x.zb + (in ? gs + lane : gs));
-		uint32_t I = lane == 0 ? B ^ lmulz(lds, 1, carry) : B;
-#pragma unroll
-		for (uint32_t d = 1; d < 64; d <<= 1) {
-			const uint32_t y = (uint32_t)__shfl_up((int)I, d);
-			const uint32_t ym = lmulz(lds, d, y);
-			I ^= lane >= d ? ym : 0u;
-		}
-		if (in) P.x.zb[gs + lane] = I ^ B;
-		carry = rdlane(I, (int)n - 1);
-	}
-	if (lane == 0) P.x.ragg[w] = carry;  // A[w]: the range-local prefix at the range's end
+	if (lane == 0) P.x.ragg[w] = X;  // A[w]: the range-local prefix at the range's end
 }
 
 // ---------------------------------------------------------------------------
@@ -476,9 +471,17 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		return;
 	}
 	const XGeo G = x_geo(P);
+	if (G.nblk == 0) {  // every buffer empty at one 16-byte-aligned address: crc32c_append(seed, p, 0) == seed
+		for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.count;
+		     i += (uint64_t)gridDim.x * blockDim.x)
+			P.out[i] = P.seeds ? xld32(P.seeds + i) : P.seed;
+		return;
+	}
 	const uint64_t per = x_per(G.nblk, P.nwave);
 	const uint32_t* s4 = lds + kFinS4;
+#ifndef FDBX_NOFILL
 	fin_fill(lds, T);
+#endif
 	// nibble tables of C = M^per (the range stride), for the straddling
 	// buffers' aggregate chains: entry [n][v] = (v x^4n) * C, bit by bit
 	if (threadIdx.x < 128) {
@@ -492,19 +495,23 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		lds[kFinC + threadIdx.x] = r;
 	}
 	__syncthreads();
+	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+	typedef __attribute__((address_space(1))) const u32x2 xg_u2;
 	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t i = i0 + threadIdx.x;
 		const bool ok = i < P.count;
 		const uint64_t ic = ok ? i : P.count - 1;
+		// the captured point values do not depend on the metadata: one round trip
+		const u32x2 cs = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.ps + 2 * ic));
+		const u32x2 ce = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.pe + 2 * ic));
 		uint64_t P0, P1;
 		x_buffer(P, ic, P0, P1);
 		const uint32_t sd = P.seeds ? xld32(P.seeds + ic) : P.seed;
 		const uint64_t sp = P0 - G.S, ep = P1 - G.S;
-		const uint32_t vs = xld32(P.x.vs + ic), ve = xld32(P.x.ve + ic);
 		const uint32_t ks = x_blk(sp), ke = x_blk(ep);
 		// G(p): the range-local prefix at p64, positioned at its block's end
-		uint32_t gs = sp ? xld32(P.x.zb + ks) ^ vs : 0u;
-		uint32_t ge = ep ? xld32(P.x.zb + ke) ^ ve : 0u;
+		const uint32_t gs = cs[0];
+		uint32_t ge = ce[0];
 		// A buffer spanning ranges ws < we: the end point takes the aggregates of
 		// the ranges from ws to we - 1 (the start point's range start is the origin)
 		const uint64_t ws = ks / per, we = ke / per;
@@ -514,36 +521,39 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 			const uint32_t j = (uint32_t)(ke - we * per + 1);
 			ge ^= j < 64 ? lmul(lds, kFinBp0 + 128 * j, D) : xmul_blocks(T, D, j);
 		}
-		// R(p): the prefix register at point p (0 at p = 0)
-		auto R = [&](uint64_t p, uint32_t g) -> uint32_t {
+		// R(p): the prefix register at point p (0 at p = 0).  p = 4096k + 64 cnt
+		// + 16 cq + r: G(p) back to p64, on by 16 cq bytes plus Y (the span's
+		// register after its first cq chunks), then the r < 16 bytes of the
+		// chunk at p - r (one 16-byte load).
+		auto R = [&](uint64_t p, uint32_t g, uint32_t y) -> uint32_t {
 			const uint32_t k = x_blk(p);
 			const uint32_t cnt = x_cnt(p, k);
-			const uint64_t p64 = p ? 4096ull * k + 64ull * cnt : 0;
+			const uint32_t rem = (uint32_t)(p - 4096ull * k) & 63u;  // (cnt = 64: rem 0)
+			const uint32_t cq = rem >> 4, r16 = rem & 15u;
 			uint32_t r = lmul(lds, kFinXinv + 128 * (64 - cnt), g);
+			r = cq ? lmul(lds, kFinPow1 + 128 * (16 * cq), r) ^ y : r;
 			r = p ? r : 0u;
-			const uint32_t rem = (uint32_t)(p - p64);  // < 64 bytes after the lane span
-			const uint8_t* src = reinterpret_cast<const uint8_t*>(G.S + p64);
-			u32x4 ch[4];
+#ifdef FDBX_NOREM
+			if (false) {
+#else
+			if (r16) {
+#endif
+				const u32x4 ch = ld16(reinterpret_cast<const uint8_t*>(G.S + p - r16));
 #pragma unroll
-			for (uint32_t q = 0; q < 4; ++q) ch[q] = 16 * q < rem ? ld16(src + 16 * q) : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-			for (uint32_t q = 0; q < 16; ++q) {
-				if (4 * q + 4 <= rem) {
-					r ^= ch[q >> 2][q & 3];
-					r = s4[r & 255u] ^ s4[256 + ((r >> 8) & 255u)] ^ s4[512 + ((r >> 16) & 255u)] ^ s4[768 + (r >> 24)];
+				for (uint32_t t = 0; t < 3; ++t) {
+					if (4 * t + 4 <= r16) {
+						r ^= ch[t];
+						r = s4[r & 255u] ^ s4[256 + ((r >> 8) & 255u)] ^ s4[512 + ((r >> 16) & 255u)] ^ s4[768 + (r >> 24)];
+					}
 				}
-			}
-			const uint32_t wd = rem >> 2, nb = rem & 3u;
-			if (nb) {
-				uint32_t word = 0;
-#pragma unroll
-				for (uint32_t q = 0; q < 16; ++q) word = q == wd ? ch[q >> 2][q & 3] : word;
+				const uint32_t wd = r16 >> 2, nb = r16 & 3u;
+				const uint32_t word = wd == 0 ? ch[0] : wd == 1 ? ch[1] : wd == 2 ? ch[2] : ch[3];
 				for (uint32_t b = 0; b < nb; ++b) r = (r >> 8) ^ s4[768 + ((r ^ (word >> (8 * b))) & 255u)];
 			}
 			return r;
 		};
-		const uint32_t re = R(ep, ge);
-		uint32_t rs = R(sp, gs) ^ ~sd;
+		const uint32_t re = R(ep, ge, ce[1]);
+		uint32_t rs = R(sp, gs, cs[1]) ^ ~sd;
 		// rs * x^(8 len), len = 4096a + 64c + d
 		const uint64_t len = P1 - P0;
 		rs = lmul(lds, kFinPow1 + 128 * (uint32_t)(len & 63u), rs);
@@ -562,26 +572,23 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 // ---------------------------------------------------------------------------
 static uint64_t xal(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
-uint64_t extent_state_bytes(uint64_t count, uint64_t cap_blk, int num_cus) {
+uint64_t extent_state_bytes(uint64_t count, int num_cus) {
 	const uint64_t nwave = (uint64_t)num_cus * 16;
-	return 256 + 2 * xal(4 * count) + xal(512 * nwave) + xal(4 * cap_blk) + xal(4 * nwave);
+	return 256 + 2 * xal(8 * count) + xal(512 * nwave) + xal(4 * nwave);
 }
 
-void extent_state_carve(void* mem, uint64_t count, uint64_t cap_blk, int num_cus, XState* x) {
+void extent_state_carve(void* mem, uint64_t count, int num_cus, XState* x) {
 	uint8_t* p = static_cast<uint8_t*>(mem);
 	const uint64_t nwave = (uint64_t)num_cus * 16;
 	x->xhdr = reinterpret_cast<uint32_t*>(p);
 	p += 256;
-	x->vs = reinterpret_cast<uint32_t*>(p);
-	p += xal(4 * count);
-	x->ve = reinterpret_cast<uint32_t*>(p);
-	p += xal(4 * count);
+	x->ps = reinterpret_cast<uint32_t*>(p);
+	p += xal(8 * count);
+	x->pe = reinterpret_cast<uint32_t*>(p);
+	p += xal(8 * count);
 	x->dummy = reinterpret_cast<uint32_t*>(p);
 	p += xal(512 * nwave);
-	x->zb = reinterpret_cast<uint32_t*>(p);
-	p += xal(4 * cap_blk);
 	x->ragg = reinterpret_cast<uint32_t*>(p);
-	x->cap_blk = cap_blk;
 }
 
 // phase 0: the streaming kernel; phase 1: the finishing kernel.  Both return
@@ -598,7 +605,6 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 	if (phase == 0)
 		k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
 	else {
-		k_xz<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
 		// persistent, but no more workgroups than the buffers fill (each fills 133 KiB of LDS)
 		const uint64_t g = (count + kFinThreads - 1) / kFinThreads;
 		k_xfin<<<(unsigned)(g < (uint64_t)num_cus ? g : (uint64_t)num_cus), kFinThreads, 0, stream>>>(P);

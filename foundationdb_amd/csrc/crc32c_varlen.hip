@@ -383,9 +383,8 @@ struct V7Params {
 	// extent route (kRouteExtent, crc32c_extent.hip): the count kernel checks
 	// the packing (the extent kernels follow it; prep and the window kernel
 	// are not launched)
-	uint32_t* xhdr;            // [0] / [1]: epoch of the last launch found not packed / over capacity
+	uint32_t* xhdr;            // [0] / [1]: epoch of the last launch found not packed / over kXMaxExtent
 	uint32_t epoch;
-	uint64_t xcap;             // extent blocks the route's arrays hold
 };
 // hdr[6]: 1 if the planner refused the batch (2^32 - 1 or more windows or
 // blocks: 32-bit slot indices); the streaming kernels then do nothing.
@@ -453,7 +452,7 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 			const uint64_t E = (reinterpret_cast<uint64_t>(P.base) + o1 + l1 + 15) & ~uint64_t(15);
 			// (an unordered batch may give E < S: the packing check refuses it anyway)
 			const uint64_t nblk = E > S ? (E - S + 4095) >> 12 : 0;
-			if (nblk > P.xcap || E - S >= (1ull << 40)) P.xhdr[1] = P.epoch;
+			if (E - S >= kXMaxExtent) P.xhdr[1] = P.epoch;
 			if (P.hstat) P.hstat[kHstatNblk] = nblk;
 		}
 		if (blockIdx.x == 0 && P.hstat) v7_route_stats(P, i, off, len, s_stat);
@@ -1157,7 +1156,6 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	if (extent) {
 		P.xhdr = xs->xhdr;
 		P.epoch = xs->epoch;
-		P.xcap = xs->cap_blk;
 	}
 	P.hdr = reinterpret_cast<uint64_t*>(wp);      // [0..3] totals and quantum, [kHdrRefused] refusal flag
 	P.tsum = reinterpret_cast<uint64_t*>(wp + 64);

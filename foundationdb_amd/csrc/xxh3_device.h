@@ -18,7 +18,10 @@ struct XxhParams {
 	uint64_t ws_bytes;           // varlen: workspace size (room past the planner's arrays: the split route)
 	uint64_t* hneed;             // varlen: host-mapped word for the blocks the long buffers needed (may be null)
 	const uint8_t* lflag;        // (set by launch_xxh3) per buffer: the split route took it (not the row kernel's)
+	uint32_t* err;               // stream's host-mapped status word (may be null): kErrXxhStall if a long-route wait ran out
 };
+// Status word values shared with the CRC engine's refusal flag (crc32c_gpu_stream_status).
+constexpr uint32_t kErrRefused = 1, kErrXxhStall = 2;
 
 constexpr unsigned kWavesPerBlock = 4;
 
@@ -39,6 +42,7 @@ struct XLong {
 	const XEnt* ents;     // [sh[0]], largest size class first
 	uint64_t* out;
 	uint64_t seed;        // uniform seed (per-buffer seeds travel in the entries)
+	uint32_t* err;        // XxhParams::err
 };
 // Workspace per long block of room (the stream's need is counted in 1 KiB
 // blocks; a long buffer has more than 16): one entry per 16 blocks.

@@ -1248,6 +1248,7 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 			S.ents = Q.ents;
 			S.out = P.out;
 			S.seed = P.seed;
+			S.err = P.err;
 			launch_xxh3_long(S, num_cus, P.seeds != nullptr, stream);
 		}
 		// fixed-length long buffers whose entries all fit: the long route did them all

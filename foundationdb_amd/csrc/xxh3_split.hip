@@ -68,7 +68,6 @@ __device__ __forceinline__ void add_dpp(uint32_t& lo, uint32_t& hi) {
 	hi = (uint32_t)(s >> 32);
 }
 
-__device__ __forceinline__ uint32_t rdf32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint64_t rdf64(uint64_t v) {
 	const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
 	const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
@@ -93,9 +92,14 @@ constexpr uint32_t kLRingSteps = 64;  // per slot: 64 steps x 4 blocks x 64 B = 
 constexpr uint32_t kLSpinMax = 1u << 24;  // bounded waits (a correct launch never reaches them)
 
 struct LSlot {
-	uint32_t claimed;         // steps claimed by producers (CAS; ~0 while the slot changes buffers)
+	// {claimed, gbase} is the producers' 64-bit compare-and-swap word: gbase (the
+	// slot's step number of its buffer's step 0) grows with every buffer the
+	// slot takes, so a claim read before the slot changed buffers can never
+	// succeed after it (no ABA on `claimed` alone)
+	uint32_t claimed;         // steps claimed by producers (~0 while the slot changes buffers)
+	uint32_t gbase;
 	uint32_t lim;             // steps that may be claimed: min(nsteps, consumed + kLRingSteps)
-	uint32_t gbase, nsteps;   // the slot's step number of the buffer's step 0; the buffer's steps
+	uint32_t nsteps;          // the buffer's steps
 	uint64_t p, len, seed;
 	uint32_t closed, pad;     // the slot takes no more buffers
 };
@@ -171,7 +175,13 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 				const uint32_t gs = gseq + t, ri = gs % kLRingSteps;
 				for (uint32_t spin = 0; VT[c * kLRingSteps + ri] != gs + 1; ++spin) {
 					if (spin >= kLSpinMax) {
-						if (lane == 0) *(volatile uint64_t*)(S.sh + 2) = 1;  // (never: a stalled ring)
+						// (never in a correct launch: a stalled ring).  The buffer's digest
+						// is not written: the stall is reported through the workspace word
+						// and the stream's status word (crc32c_gpu_stream_status).
+						if (lane == 0) {
+							*(volatile uint64_t*)(S.sh + 2) = 1;
+							if (S.err) *(volatile uint32_t*)S.err = kErrXxhStall;
+						}
 						return;
 					}
 					__builtin_amdgcn_s_sleep(1);
@@ -233,16 +243,19 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 			const uint32_t c = (pref + u) % kLChains;
 			{
 				const uint64_t cw = *(volatile uint64_t*)&L.slot[c].claimed;
-				const uint32_t cl = (uint32_t)cw, lim = (uint32_t)(cw >> 32);
+				const uint32_t cl = (uint32_t)cw, gb = (uint32_t)(cw >> 32);
+				// lim is read after {claimed, gbase}: if the slot changed buffers in
+				// between, gbase differs and the swap below fails
+				const uint32_t lim = VS[c].lim;
 				if (cl >= lim) continue;  // (~0: between buffers)
-				uint32_t old = 0;
-				if (lane == 0) old = atomicCAS((uint32_t*)&L.slot[c].claimed, cl, cl + 1);
-				if ((uint32_t)__builtin_amdgcn_readlane((int)old, 0) != cl) {
-					continue;
-				}
+				unsigned long long old = 0;
+				if (lane == 0)
+					old = atomicCAS((unsigned long long*)&L.slot[c].claimed, (unsigned long long)cw,
+					                (unsigned long long)cw + 1ull);
+				if (rdf64((uint64_t)__shfl((long long)old, 0)) != cw) continue;
 				St.c = c;
 				St.t = cl;
-				St.gs = rdf32(VS[c].gbase) + cl;
+				St.gs = gb + cl;
 				St.p = rdf64(VS[c].p);
 				St.len = rdf64(VS[c].len);
 				St.seed = rdf64(VS[c].seed);

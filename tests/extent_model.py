@@ -145,20 +145,22 @@ def ranges_per(nblk, nwave, unit=4):
 
 
 def extent_crcs_ranges(mem, offsets, lengths, seed, nwave):
-    """The same CRCs the way the kernels compute them since round 3, without a
+    """The same CRCs the way the kernels compute them since round 4, without a
     scan over all blocks: wave w streams the blocks [k0, k1) = [w*per, ...) of
-    its RANGE and keeps the range-local prefix X (0 at k0):
-        Z[k] = X_k * M  (stored per block),  X_{k+1} = Z[k] ^ B[k],  A[w] = X_{k1}
-    computed by k_xz once per group of 64 blocks, lane-parallel (the carry
-    enters lane 0 as carry * M, then a 6-step weighted scan over the lanes;
-    modelled here group by group).  The ranges' global start registers are
-    X0[w+1] = X0[w] * M^per ^ A[w].  A point
-    p in block k of range w, with cnt lane spans before it, has
-        G(p) = Z[k] ^ H_k[cnt-1]    (its range-local prefix at p64, positioned
-                                     at block k's end)
-    and, positioned the same way, the global prefix G(p) ^ X0[w] * M^(k-k0+1).
-    A buffer whose two points lie in one range needs only the local values
-    (X0[w] cancels); others take the global ones."""
+    its RANGE and keeps the range-local prefix X (0 at k0) itself, block by
+    block:  Z[k] = X_k * M,  X_{k+1} = Z[k] ^ B[k],  A[w] = X_{k1}.  A point
+    p = 4096k + 64 cnt + 16 cq + r (r < 16) of block k is CAPTURED by the wave
+    streaming block k as two words:
+        G(p) = Z[k] ^ H_k[cnt-1]   (its range-local prefix at p64, positioned
+                                    at block k's end)
+        Y(p) = y_cq of lane span cnt: the raw register of that span's first
+               16 cq bytes (0 for cq = 0)
+    and the finishing pass forms
+        R(p16) = G(p) * x^(-8*64*(64-cnt)) * x^(8*16 cq) ^ Y(p),
+        R(p)   = R(p16) fed the r bytes of the 16-byte chunk at p16.
+    The ranges' global start registers are X0[w+1] = X0[w] * M^per ^ A[w]; a
+    buffer whose two points lie in one range needs only the local values (X0[w]
+    cancels), others add X0 * M^(k-k0+1) to both."""
     P0 = [int(o) for o in offsets]
     P1 = [int(o) + int(l) for o, l in zip(offsets, lengths)]
     assert eligible(P0, P1)
@@ -180,17 +182,9 @@ def extent_crcs_ranges(mem, offsets, lengths, seed, nwave):
     for w in range(nwave):
         k0, k1 = min(w * per, nblk), min(w * per + per, nblk)
         X = 0
-        for g0 in range(k0, k1, 64):  # groups of 64 blocks, as k_xz does them
-            n = min(64, k1 - g0)
-            B = [H[g0 + j][63] for j in range(n)]
-            I = [B[0] ^ gf2_mul(X, M)] + B[1:]
-            d = 1
-            while d < 64:  # weighted scan: I_j ^= I_(j-d) * M^d
-                I = [I[j] ^ (gf2_mul(I[j - d], xpow8(4096 * d)) if j >= d else 0) for j in range(n)]
-                d *= 2
-            for j in range(n):
-                Z[g0 + j] = I[j] ^ B[j]  # X_{g0+j+1} ^ B = X_{g0+j} * M
-            X = I[n - 1]
+        for k in range(k0, k1):  # block by block, as k_xstream does
+            Z[k] = gf2_mul(X, M)
+            X = Z[k] ^ H[k][63]
         A.append(X)
     X0 = [0]
     for w in range(nwave - 1):
@@ -201,15 +195,31 @@ def extent_crcs_ranges(mem, offsets, lengths, seed, nwave):
         cnt = (p - 4096 * k) >> 6 if p else 0
         return k, cnt, k // per
 
+    def capture(p):
+        """the two words k_xstream stores for point p"""
+        if p == 0:
+            return 0, 0
+        k, cnt, _ = point(p)
+        cq = ((p - 4096 * k) & 63) >> 4
+        G = Z[k] ^ (H[k][cnt - 1] if cnt else 0)
+        span = 4096 * k + 64 * cnt
+        Y = feed(0, ext[span:span + 16 * cq]) if cq else 0
+        return G, Y
+
     def R(p, glob):
         if p == 0:
             return 0
         k, cnt, w = point(p)
-        G = Z[k] ^ (H[k][cnt - 1] if cnt else 0)
+        G, Y = capture(p)
         if glob:
             G ^= gf2_mul(X0[w], xpow8(4096 * (k - w * per + 1)))
-        p64 = 4096 * k + 64 * cnt
-        return feed(gf2_mul(G, xpow8_inv(64 * (64 - cnt))), ext[p64:p])
+        rem = (p - 4096 * k) & 63
+        cq, r = rem >> 4, rem & 15
+        reg = gf2_mul(G, xpow8_inv(64 * (64 - cnt)))
+        if cq:
+            reg = gf2_mul(reg, xpow8(16 * cq)) ^ Y
+        p16 = p - r
+        return feed(reg, ext[p16:p])
 
     out = []
     for a, b in zip(P0, P1):

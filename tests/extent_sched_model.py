@@ -1,6 +1,6 @@
 """CPU model of k_xstream's SCHEDULE (crc32c_extent.hip), symbolic: which
 wave captures which point, from which block and lane span, and which blocks
-each wave's group stores cover.  Lane prefixes are represented by their
+each wave folds into its range prefix.  Lane prefixes are represented by their
 (block, lane) coordinates, so the model checks the control flow -- static
 ranges of whole units, the window search, window retirement inside a unit,
 the extent's last block, the ownership of points at range boundaries --
@@ -21,7 +21,7 @@ def schedule(P0, P1, nwave):
     """P0/P1: absolute starts/ends of a packed batch.  Returns (vs, ve, blk):
     vs[i] / ve[i] = list of (wave, value) writes, value = None (0) or the
     (block, lane) whose prefix was captured; blk[k] = list of waves that
-    stored block k's register."""
+    folded block k's register into its range's prefix X."""
     n = len(P0)
     S = P0[0] & ~15
     Eend = (P1[-1] + 15) & ~15
@@ -69,9 +69,10 @@ def schedule(P0, P1, nwave):
                     c = win["ce"][j]
                     win["Ve"][j] = (kb, c - 1) if c else 0
 
-        gs = [k0]
-
         def finish(k, kend):
+            for j in range(2 * U):
+                if k + j < kend:  # X = X * M ^ B[k + j]
+                    blk[k + j].append(w)
             for j in range(2 * U):
                 capture(k + j, k + j < kend)
             kn = min(k + 2 * U, kend)
@@ -80,10 +81,6 @@ def schedule(P0, P1, nwave):
                 make_window(win["q"] + 64)
                 for j in range(2 * U):
                     capture(k + j, k + j < kend)
-            if kn - gs[0] >= 64 or kn == kend:
-                for b in range(gs[0], kn):
-                    blk[b].append(w)
-                gs[0] = kn
 
         make_window(q)
         if k0 >= k1:

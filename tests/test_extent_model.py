@@ -56,7 +56,7 @@ def test_eligibility_rule():
 def _check_schedule(P0, P1, nwave):
     from tests import extent_sched_model as M
     vs, ve, blk, S, nblk = M.schedule(P0, P1, nwave)
-    assert all(len(b) == 1 for b in blk), "every block register stored exactly once"
+    assert all(len(b) == 1 for b in blk), "every block folded into its range prefix exactly once"
     for i, (a, b) in enumerate(zip(P0, P1)):
         for p, rec in ((a - S, vs[i]), (b - S, ve[i])):
             k = M.x_blk(p)
@@ -74,7 +74,7 @@ def test_stream_schedule_captures_every_point_once(nwave):
     """k_xstream's control flow (static unit ranges, window search and
     retirement, the extent's last block): every point is captured exactly
     once, by the wave whose range holds its block, from the right block and
-    lane span; every block register is stored exactly once."""
+    lane span; every block is folded into its range prefix exactly once."""
     rng = np.random.default_rng(nwave)
     for trial in range(12):
         P0, P1, pos = [], [], int(rng.integers(0, 4096))
