@@ -11,9 +11,11 @@
 #include <string>
 
 #include "../../include/fdb_crc32c.h"
+#include "../../include/fdb_packets.h"
 #include "../../include/fdb_pagecheck.h"
 #include "../../include/fdb_xxh3.h"
 #include "crc32c_device.h"
+#include "packets.h"
 #include "pagecheck.h"
 #include "xxh3_device.h"
 
@@ -747,6 +749,63 @@ int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok
 	                              &hold))
 		return rc;
 	return fdb_diskqueue_check_pages_ws(d_pages, count, d_ok, d_bad, ws, have, stream);
+}
+
+// ---- FlowTransport receive verification (include/fdb_packets.h) ------------
+
+uint64_t fdb_packets_workspace_bytes(uint64_t nbuf, uint64_t max_frames, uint64_t total_bytes) {
+	DeviceState* st = nullptr;
+	if (device_state(&st)) return 0;
+	return fdbpkt::workspace_bytes(nbuf, max_frames, total_bytes, st->num_cus);
+}
+
+int fdb_packets_verify_ws(const void* d_base, const uint64_t* d_buf_offsets, const uint64_t* d_buf_lengths,
+                          uint64_t nbuf, uint64_t total_bytes, int checksum_enabled, uint32_t packet_limit,
+                          uint64_t max_frames, fdb_packet_result* d_results, void* d_workspace,
+                          uint64_t workspace_bytes, void* stream) {
+	if (nbuf == 0) return 0;
+	if (!d_base || !d_buf_offsets || !d_buf_lengths || !d_results)
+		return fail(FDB_CRC32C_EINVAL, "fdb_packets_verify: null pointer");
+	if (nbuf >= 0xFFFFFFFFull || max_frames >= 0xFFFFFFFFull)
+		return fail(FDB_CRC32C_EINVAL, "fdb_packets_verify: nbuf and max_frames must be below 2^32");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	const uint64_t need = fdbpkt::workspace_bytes(nbuf, max_frames, total_bytes, st->num_cus);
+	if (!d_workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_packets_verify: workspace too small or misaligned");
+	if (fdbpkt::launch_verify(static_cast<const uint8_t*>(d_base), d_buf_offsets, d_buf_lengths, nbuf,
+	                          checksum_enabled ? 1 : 0, packet_limit, max_frames, d_results, d_workspace,
+	                          workspace_bytes, st->num_cus, reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "fdb_packets_verify: launch setup failed");
+	return check_launch("fdb_packets_verify launch");
+}
+
+int fdb_packets_verify(const void* d_base, const uint64_t* d_buf_offsets, const uint64_t* d_buf_lengths,
+                       uint64_t nbuf, uint64_t total_bytes, int checksum_enabled, uint32_t packet_limit,
+                       uint64_t max_frames, fdb_packet_result* d_results, void* stream) {
+	if (nbuf == 0) return 0;
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
+	                              fdbpkt::workspace_bytes(nbuf, max_frames, total_bytes, st->num_cus), &ws, &have,
+	                              &hold))
+		return rc;
+	return fdb_packets_verify_ws(d_base, d_buf_offsets, d_buf_lengths, nbuf, total_bytes, checksum_enabled,
+	                             packet_limit, max_frames, d_results, ws, have, stream);
+}
+
+int fdb_packets_frames(const void* d_workspace, uint64_t nbuf, uint64_t max_frames, fdb_packet_frame* d_frames,
+                       uint64_t capacity, uint64_t* d_nframes, void* stream) {
+	if (!d_workspace || (capacity && !d_frames)) return fail(FDB_CRC32C_EINVAL, "fdb_packets_frames: null pointer");
+	void* xws = nullptr;
+	uint64_t xb = 0;
+	const fdbpkt::Ws w = fdbpkt::carve(const_cast<void*>(d_workspace), nbuf, max_frames, ~0ull >> 1, &xws, &xb);
+	if (fdbpkt::launch_frames(w, d_frames, capacity, d_nframes, reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "fdb_packets_frames: launch setup failed");
+	return check_launch("fdb_packets_frames launch");
 }
 
 int crc32c_gpu_release_stream(void* stream) { return release_stream(reinterpret_cast<hipStream_t>(stream)); }

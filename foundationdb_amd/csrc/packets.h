@@ -1,0 +1,42 @@
+// Device-side interface of the packet-verify kernels (packets.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fdb_packets.h"
+
+namespace fdbpkt {
+
+// Workspace: [0] the frame counter, then per buffer the walk's results and the
+// first failing frame, per frame slot the list the walk appends to.
+struct Ws {
+	uint64_t* hdr;       // [0]: frames appended (may exceed cap: then some were not recorded)
+	uint32_t* walked;    // per buffer: frames walked
+	int32_t* wstat;      // ... why the walk stopped
+	uint32_t* bad_ord;   // ... first frame whose checksum failed (~0: none)
+	uint64_t* wend;      // ... bytes walked
+	uint64_t* bad_pos;   // ... header position of that frame
+	uint64_t* foff;      // per frame: payload offset from base
+	uint64_t* flen;      // ... payload bytes
+	uint64_t* fexp;      // ... the header's checksum
+	uint64_t* fh;        // ... XXH3 of the payload
+	uint32_t* fbuf;      // ... buffer
+	uint32_t* ford;      // ... ordinal in its buffer
+	uint64_t cap;
+};
+struct CheckP {
+	const uint8_t* base;
+	const uint64_t* boff;
+	uint64_t nbuf;
+	uint32_t hdr;
+	Ws w;
+	fdb_packet_result* out;
+};
+uint64_t workspace_bytes(uint64_t nbuf, uint64_t max_frames, uint64_t total_bytes, int num_cus);
+Ws carve(void* ws, uint64_t nbuf, uint64_t max_frames, uint64_t ws_bytes, void** xws, uint64_t* xws_bytes);
+int launch_verify(const uint8_t* base, const uint64_t* boff, const uint64_t* blen, uint64_t nbuf, int checksum,
+                  uint32_t limit, uint64_t max_frames, fdb_packet_result* out, void* ws, uint64_t ws_bytes,
+                  int num_cus, hipStream_t s);
+int launch_frames(const Ws& w, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n, hipStream_t s);
+
+}  // namespace fdbpkt

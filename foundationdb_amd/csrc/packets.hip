@@ -1,0 +1,298 @@
+// Batched FlowTransport receive verification (gfx950): the checksum half of
+// scanPackets (fdbrpc/FlowTransport.cpp:1260-1366) over many connections'
+// receive buffers at once.  A receive buffer holds frames
+//     [u32 len][u64 XXH3_64bits(payload)][payload: len bytes]
+// back to back ([u32 len][payload] for TLS peers, whose checksum is off,
+// :1275).  The reference walks one buffer's frames in order on the network
+// thread and, per complete frame, rejects len > PACKET_LIMIT (:1299-1304,
+// checked before the frame's bytes have all arrived), stops at an incomplete
+// frame (:1306-1307), rejects len < sizeof(UID) (:1309-1319), recomputes the
+// payload's XXH3 and throws checksum_failed on a mismatch (:1346-1358); every
+// frame before the one that stops or throws is delivered, and
+// unprocessed_begin moves past it.
+//
+// Here the length walk and the hashing are separated, so the hashing is
+// balanced over the whole GPU instead of one buffer per thread:
+//   k_pkt_walk    one wave per receive buffer walks its frame headers -- a
+//                 serial chain, each header's length locating the next --
+//                 from windows of the buffer staged in LDS by coalesced loads
+//                 (one restage per window, not one HBM round trip per frame),
+//                 and appends every complete, well-sized frame to a frame list
+//                 (64 at a time: one atomic per group of frames)
+//   XXH3 varlen   the frame payloads through the XXH3 engine
+//                 (xxh3_kernels.hip / xxh3_split.hip), batch size read on the
+//                 device from the walk's frame counter
+//   k_pkt_check   per frame: a mismatch lowers its buffer's first failing
+//                 ordinal (and header position) with atomicMin
+//   k_pkt_final   per buffer: the reference's outcome -- the frames it
+//                 delivers, the bytes it consumes, and why it stopped
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/fdb_packets.h"
+#include "packets.h"
+#include "xxh3_device.h"
+
+namespace fdbpkt {
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) const uint64_t g_u64;
+
+__device__ __forceinline__ uint32_t rdfirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rdfirst64(uint64_t v) {
+	return ((uint64_t)rdfirst((uint32_t)(v >> 32)) << 32) | (uint64_t)rdfirst((uint32_t)v);
+}
+
+constexpr uint32_t kWalkWaves = 4;                 // buffers per 256-thread workgroup
+constexpr uint32_t kWin = 8192;                    // bytes of a buffer staged per window
+constexpr uint32_t kWinWords = kWin / 4 + 4;       // + slack: an unaligned word read past the window's last byte
+
+}  // namespace
+
+struct WalkP {
+	const uint8_t* base;
+	const uint64_t* boff;
+	const uint64_t* blen;
+	uint64_t nbuf;
+	uint32_t hdr;     // 12 (checksums on) or 4
+	uint32_t limit;   // FLOW_KNOBS->PACKET_LIMIT
+	Ws w;
+};
+
+// One wave per receive buffer.  Every lane runs the same walk (the header
+// words are LDS broadcasts), so control flow is uniform; a group of up to 64
+// frames collects in the lanes (lane j: frame j of the group) and leaves with
+// one atomic reservation.
+__global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
+	__shared__ uint32_t win[kWalkWaves][kWinWords];
+	const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const uint64_t b = (uint64_t)blockIdx.x * kWalkWaves + wv;
+	if (b >= P.nbuf) return;  // (uniform per wave; no workgroup barrier below)
+	uint32_t* const L = win[wv];
+	const uint64_t B0 = rdfirst64(reinterpret_cast<uint64_t>(P.base) + *((g_u64*)reinterpret_cast<uintptr_t>(P.boff + b)));
+	const uint64_t len = rdfirst64(*((g_u64*)reinterpret_cast<uintptr_t>(P.blen + b)));
+	const uint64_t E = B0 + len;
+	const uint64_t last_chunk = (E - 1) & ~uint64_t(15);  // (len > 0 wherever a window is staged)
+	uint64_t wbeg = ~uint64_t(0);  // window: bytes [wbeg, wbeg + kWin), wbeg 16-byte aligned
+	auto restage = [&](uint64_t a) {
+		wbeg = a & ~uint64_t(15);
+#pragma unroll
+		for (uint32_t i = 0; i < kWin / 1024; ++i) {
+			const uint64_t c = wbeg + 16ull * (lane + 64 * i);
+			// chunks past the buffer re-read its last one (never used: the walk
+			// checks every length against the buffer's end)
+			const u32x4 v = *((g_u32x4*)reinterpret_cast<uintptr_t>(c <= last_chunk ? c : last_chunk));
+			*reinterpret_cast<u32x4*>(L + 4 * (lane + 64 * i)) = v;
+		}
+		__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's LDS writes are done before its reads
+		__builtin_amdgcn_wave_barrier();
+	};
+	// little-endian u32 at absolute address a inside the window
+	auto rd32 = [&](uint64_t a) -> uint32_t {
+		const uint32_t o = (uint32_t)(a - wbeg);
+		const uint32_t w0 = L[o >> 2], w1 = L[(o >> 2) + 1];
+		return __builtin_amdgcn_alignbyte(w1, w0, o & 3u);
+	};
+	uint64_t p = 0;     // bytes of the buffer walked
+	uint32_t ord = 0;   // frames walked
+	int32_t status = FDB_PACKET_OK;
+	// the group of frames not yet written out
+	uint32_t pend = 0;
+	uint64_t g_off = 0, g_len = 0, g_exp = 0;
+	uint32_t g_ord = 0;
+	uint64_t* const fcount = P.w.hdr;
+	bool overflow = false;
+	auto flush = [&]() {
+		if (pend == 0) return;
+		uint64_t at = 0;
+		if (lane == 0) at = atomicAdd((unsigned long long*)fcount, (unsigned long long)pend);
+		at = rdfirst64(at);  // (every lane is active: lane 0's reservation)
+		const uint64_t f = at + lane;
+		if (lane < pend && f < P.w.cap) {
+			P.w.foff[f] = g_off;
+			P.w.flen[f] = g_len;
+			P.w.fexp[f] = g_exp;
+			P.w.fbuf[f] = (uint32_t)b;
+			P.w.ford[f] = g_ord;
+		}
+		if (at + pend > P.w.cap) overflow = true;
+		pend = 0;
+	};
+	for (;;) {
+		if (len - p < 4) break;                              // FlowTransport.cpp:1285-1286
+		if (P.hdr == 12 && len - p - 4 < 8) break;           // :1293-1294
+		const uint64_t a = B0 + p;
+		if (a < wbeg || a + P.hdr > wbeg + kWin) restage(a);
+		const uint32_t fl = rdfirst(rd32(a));
+		if (fl > P.limit) {                                  // :1299-1304 (before the frame is complete)
+			status = FDB_PACKET_LIMIT_EXCEEDED;
+			break;
+		}
+		if (len - p - P.hdr < fl) break;                     // :1306-1307
+		if (fl < 16) {                                       // :1309-1319 (sizeof(UID))
+			status = FDB_PACKET_TOO_SMALL;
+			break;
+		}
+		uint64_t ck = 0;
+		if (P.hdr == 12) ck = ((uint64_t)rdfirst(rd32(a + 8)) << 32) | rdfirst(rd32(a + 4));
+		if (lane == pend) {
+			g_off = a + P.hdr - reinterpret_cast<uint64_t>(P.base);
+			g_len = fl;
+			g_exp = ck;
+			g_ord = ord;
+		}
+		if (++pend == 64) flush();
+		p += P.hdr + fl;
+		++ord;
+	}
+	flush();
+	if (lane == 0) {
+		P.w.walked[b] = ord;
+		P.w.wstat[b] = overflow ? FDB_PACKET_ECAPACITY : status;
+		P.w.wend[b] = p;
+		P.w.bad_ord[b] = ~0u;
+		P.w.bad_pos[b] = ~0ull;
+	}
+}
+
+// Per frame: the digest against the header's checksum.
+__global__ __launch_bounds__(256) void k_pkt_check(CheckP P) {
+	const uint64_t n = *P.w.hdr < P.w.cap ? *P.w.hdr : P.w.cap;
+	for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n; f += (uint64_t)gridDim.x * blockDim.x) {
+		if (P.w.fh[f] != P.w.fexp[f]) {
+			const uint32_t b = P.w.fbuf[f];
+			atomicMin(P.w.bad_ord + b, P.w.ford[f]);
+			// the frame's header position in its buffer: the bytes consumed before it
+			const uint64_t pos = reinterpret_cast<uint64_t>(P.base) + P.w.foff[f] - P.hdr -
+			                     (reinterpret_cast<uint64_t>(P.base) + P.boff[b]);
+			atomicMin((unsigned long long*)(P.w.bad_pos + b), (unsigned long long)pos);
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void k_pkt_final(CheckP P) {
+	const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (b >= P.nbuf) return;
+	const uint32_t n = P.w.walked[b], bo = P.w.bad_ord[b];
+	fdb_packet_result r;
+	if (bo < n) {  // the first frame that fails its checksum comes before the walk's stop
+		r.consumed = P.w.bad_pos[b];
+		r.frames = bo;
+		r.status = FDB_PACKET_CHECKSUM_FAILED;
+	} else {
+		r.consumed = P.w.wend[b];
+		r.frames = n;
+		r.status = P.w.wstat[b];
+	}
+	P.out[b] = r;
+}
+
+__global__ __launch_bounds__(256) void k_pkt_frames(Ws w, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n) {
+	const uint64_t n0 = *w.hdr < w.cap ? *w.hdr : w.cap;
+	const uint64_t n = n0 < capacity ? n0 : capacity;
+	if (blockIdx.x == 0 && threadIdx.x == 0 && d_n) *d_n = n0;
+	for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n; f += (uint64_t)gridDim.x * blockDim.x) {
+		fdb_packet_frame r;
+		r.offset = w.foff[f];
+		r.length = w.flen[f];
+		r.checksum = w.fexp[f];
+		r.buffer = w.fbuf[f];
+		r.ordinal = w.ford[f];
+		out[f] = r;
+	}
+}
+
+int launch_frames(const Ws& w, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n, hipStream_t s) {
+	const uint64_t g = (w.cap < capacity ? w.cap : capacity) / 256 + 1;
+	k_pkt_frames<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, s>>>(w, out, capacity, d_n);
+	return 0;
+}
+
+static uint64_t a256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+uint64_t workspace_bytes(uint64_t nbuf, uint64_t max_frames, uint64_t total_bytes, int num_cus) {
+	const uint64_t own = 256 + a256(4 * nbuf) * 3 + a256(8 * nbuf) * 2 + a256(8 * max_frames) * 4 +
+	                     a256(4 * max_frames) * 2;
+	const uint64_t xw = fdbxxh::xxh3_workspace_bytes_for(max_frames, fdbxxh::xxh3_nwave(num_cus),
+	                                                     fdbxxh::xxh3_long_blocks_bound(total_bytes));
+	return own + a256(xw);
+}
+
+Ws carve(void* ws, uint64_t nbuf, uint64_t max_frames, uint64_t ws_bytes, void** xws, uint64_t* xws_bytes) {
+	uint8_t* p = static_cast<uint8_t*>(ws);
+	Ws w{};
+	w.hdr = reinterpret_cast<uint64_t*>(p);
+	p += 256;
+	w.walked = reinterpret_cast<uint32_t*>(p);
+	p += a256(4 * nbuf);
+	w.wstat = reinterpret_cast<int32_t*>(p);
+	p += a256(4 * nbuf);
+	w.bad_ord = reinterpret_cast<uint32_t*>(p);
+	p += a256(4 * nbuf);
+	w.wend = reinterpret_cast<uint64_t*>(p);
+	p += a256(8 * nbuf);
+	w.bad_pos = reinterpret_cast<uint64_t*>(p);
+	p += a256(8 * nbuf);
+	w.foff = reinterpret_cast<uint64_t*>(p);
+	p += a256(8 * max_frames);
+	w.flen = reinterpret_cast<uint64_t*>(p);
+	p += a256(8 * max_frames);
+	w.fexp = reinterpret_cast<uint64_t*>(p);
+	p += a256(8 * max_frames);
+	w.fh = reinterpret_cast<uint64_t*>(p);
+	p += a256(8 * max_frames);
+	w.fbuf = reinterpret_cast<uint32_t*>(p);
+	p += a256(4 * max_frames);
+	w.ford = reinterpret_cast<uint32_t*>(p);
+	p += a256(4 * max_frames);
+	w.cap = max_frames;
+	*xws = p;
+	*xws_bytes = ws_bytes - (uint64_t)(p - static_cast<uint8_t*>(ws));
+	return w;
+}
+
+int launch_verify(const uint8_t* base, const uint64_t* boff, const uint64_t* blen, uint64_t nbuf, int checksum,
+                  uint32_t limit, uint64_t max_frames, fdb_packet_result* out, void* ws, uint64_t ws_bytes,
+                  int num_cus, hipStream_t s) {
+	void* xws = nullptr;
+	uint64_t xws_bytes = 0;
+	const Ws w = carve(ws, nbuf, max_frames, ws_bytes, &xws, &xws_bytes);
+	if (hipMemsetAsync(w.hdr, 0, 8, s) != hipSuccess) return -1;
+	WalkP W{};
+	W.base = base;
+	W.boff = boff;
+	W.blen = blen;
+	W.nbuf = nbuf;
+	W.hdr = checksum ? 12u : 4u;
+	W.limit = limit;
+	W.w = w;
+	k_pkt_walk<<<(unsigned)((nbuf + kWalkWaves - 1) / kWalkWaves), 64 * kWalkWaves, 0, s>>>(W);
+	CheckP C{};
+	C.base = base;
+	C.boff = boff;
+	C.nbuf = nbuf;
+	C.hdr = W.hdr;
+	C.w = w;
+	C.out = out;
+	if (checksum && max_frames) {
+		fdbxxh::XxhParams X{};
+		X.base = base;
+		X.offsets = w.foff;
+		X.lengths = w.flen;
+		X.count = max_frames;
+		X.d_count = w.hdr;
+		X.out = w.fh;
+		X.ws_bytes = xws_bytes;
+		if (fdbxxh::launch_xxh3(X, num_cus, xws, s)) return -1;
+		const uint64_t g = (max_frames + 255) / 256;
+		k_pkt_check<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, s>>>(C);
+	}
+	k_pkt_final<<<(unsigned)((nbuf + 255) / 256), 256, 0, s>>>(C);
+	return 0;
+}
+
+}  // namespace fdbpkt

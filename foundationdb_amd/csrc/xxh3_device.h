@@ -14,7 +14,7 @@ struct XxhParams {
 	uint64_t* out;
 	const uint64_t* wave_first;  // varlen: first buffer of every wave [nwave + 1] (planner output)
 	const uint32_t* idx;         // fixed list mode: buffer i = base + idx[i]*stride, count = *d_count
-	const uint64_t* d_count;
+	const uint64_t* d_count;     // ... varlen: may be null, else the batch is min(count, *d_count) buffers
 	uint64_t ws_bytes;           // varlen: workspace size (room past the planner's arrays: the split route)
 	uint64_t* hneed;             // varlen: host-mapped word for the blocks the long buffers needed (may be null)
 	const uint8_t* lflag;        // (set by launch_xxh3) per buffer: the split route took it (not the row kernel's)

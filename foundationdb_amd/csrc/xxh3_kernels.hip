@@ -610,6 +610,7 @@ struct VStep {
 
 template <bool SEEDS>
 __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
+	if (P.d_count) P.count = min(P.count, (uint64_t)*P.d_count);  // device-sized batch (the planner's too)
 	const int lane = threadIdx.x & 63;
 	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
 	const uint64_t wpb = blockDim.x >> 6;
@@ -869,6 +870,7 @@ struct XPlanP {
 	XEnt* ents;
 	uint64_t capS;            // entries the room holds (0: no room)
 	uint64_t* hneed;          // host-mapped word (may be null): blocks the batch's long buffers need
+	const uint64_t* dcount;   // may be null: the batch size is min(count, *dcount) (count bounds the grid)
 };
 constexpr uint64_t kTileRouted = 1ull << 63;
 __device__ __forceinline__ uint64_t xp_len(const XPlanP& Q, uint64_t i) { return Q.lengths ? Q.lengths[i] : Q.length; }
@@ -911,6 +913,7 @@ __device__ __forceinline__ uint64_t rdlane63(uint64_t v) {
 // One workgroup per tile of 256 buffers: the tile's sums.
 __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
 	__shared__ uint64_t part[4][8];
+	if (Q.dcount) Q.count = min(Q.count, (uint64_t)*Q.dcount);
 	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
@@ -1033,6 +1036,7 @@ constexpr uint64_t kXFuseTiles = FDBXXH_FUSE_TILES;
 template <bool FUSED>
 __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 	__shared__ uint64_t wsum[4];
+	if (Q.dcount) Q.count = min(Q.count, (uint64_t)*Q.dcount);
 	__shared__ uint32_t ccount[kXClasses];
 	__shared__ uint64_t cbase[kXClasses];
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1235,6 +1239,7 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		Q.ents = reinterpret_cast<XEnt*>(w8 + L.ents);
 		Q.capS = L.capS;
 		Q.hneed = P.hneed;
+		Q.dcount = P.d_count;
 		k_xplan<<<(unsigned)ntile, 256, 0, stream>>>(Q);
 		if (ntile <= kXFuseTiles) {
 			k_xassign<true><<<(unsigned)ntile, 256, 0, stream>>>(Q);

@@ -423,3 +423,47 @@ def diskqueue_check_page(page):
     if ver == 2:
         return int(int.from_bytes(page[:8], "little") == xxh3_64(page[8:]))
     return 0
+
+
+# ---- FlowTransport receive checks (packets_oracle.c) --------------------------
+PACKETS_SO = os.path.join(_HERE, "liboracle_packets.so")
+PACKETS_REF_SO = os.path.join(_HERE, "_ref", "libpackets_ref.so")
+_pk = {}
+
+
+def _packets_lib(ref):
+    path = PACKETS_REF_SO if ref else PACKETS_SO
+    if path not in _pk:
+        if not os.path.exists(path):
+            if ref:
+                raise FileNotFoundError(path + " (run `make -C oracle` where /root/reference exists)")
+            build()
+        L = ctypes.CDLL(path)
+        vp = ctypes.c_void_p
+        L.oracle_packets_verify.restype = None
+        L.oracle_packets_verify.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, vp, vp, vp]
+        _pk[path] = L
+    return _pk[path]
+
+
+def packets_reference_available():
+    return os.path.exists(PACKETS_REF_SO)
+
+
+def packets_verify(buf, buf_offsets, buf_lengths, checksum=True, packet_limit=100 << 20, ref=False):
+    """scanPackets' outcome per receive buffer (FlowTransport.cpp:1260-1366):
+    (consumed u64, frames u32, status i32) arrays.  ref=True hashes with the
+    reference's own flow/xxhash.c instead of our XXH3 restatement."""
+    buf = np.ascontiguousarray(buf).view(np.uint8)
+    bo = np.ascontiguousarray(buf_offsets, dtype=np.uint64)
+    bl = np.ascontiguousarray(buf_lengths, dtype=np.uint64)
+    n = bo.size
+    if n:
+        assert int((bo + bl).max()) <= buf.nbytes
+    consumed = np.zeros(n, np.uint64)
+    frames = np.zeros(n, np.uint32)
+    status = np.zeros(n, np.int32)
+    _packets_lib(ref).oracle_packets_verify(buf.ctypes.data, bo.ctypes.data, bl.ctypes.data, n, 1 if checksum else 0,
+                                            packet_limit, consumed.ctypes.data, frames.ctypes.data,
+                                            status.ctypes.data)
+    return consumed, frames, status
