@@ -37,7 +37,7 @@ $(TU_LIB): $(TU_SRCS) foundationdb_amd/testutil/fdb_crc32c_testutil.h
 # the page kernels' grab requests must stay single-lane atomics whose return is
 # awaited only where it is used (the atomic optimizer's wave reduction reads it
 # back at once, which stalls on every data load in flight)
-$(OBJ)/crc32c_kernels.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+$(OBJ)/crc32c_kernels.hip.o $(OBJ)/crc32c_extent.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 
 $(OBJ)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
@@ -57,7 +57,7 @@ oracle:
 # bounds-checked build for kernel debugging (foundationdb_amd/lib/libfdb_crc32c_debug.so)
 # (built by default: the GPU suite replays route batches against it)
 DBG_OBJS := $(patsubst $(CSRC)/%.hip,build/dbg/%.hip.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,build/dbg/%.cpp.o,$(CPP_SRCS))
-build/dbg/crc32c_kernels.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+build/dbg/crc32c_kernels.hip.o build/dbg/crc32c_extent.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 build/dbg/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build/dbg
 	$(HIPCC) $(HIPFLAGS) -DFDBCRC_DEBUG -c $< -o $@

@@ -196,7 +196,7 @@ bool stream_extent(DeviceState* st, hipStream_t s, uint64_t count, XState* xs) {
 		}
 		const uint64_t nc = count + count / 4;
 		void* m = nullptr;
-		const uint64_t bytes = extent_state_bytes(nc, st->num_cus);
+		const uint64_t bytes = extent_state_bytes(nc, kXGrabCap, st->num_cus);
 		if (hipMalloc(&m, bytes) != hipSuccess) {
 			(void)hipGetLastError();
 			ss->xcount = 0;
@@ -209,7 +209,12 @@ bool stream_extent(DeviceState* st, hipStream_t s, uint64_t count, XState* xs) {
 		ss->xmem = m;
 		ss->xcount = nc;
 	}
-	extent_state_carve(ss->xmem, ss->xcount, st->num_cus, xs);
+	extent_state_carve(ss->xmem, ss->xcount, kXGrabCap, st->num_cus, xs);
+	// the dynamic stream kernel's grab counters (development: FDBCRC_XSTATIC=1
+	// streams with static per-wave ranges instead)
+	static const bool stat = getenv("FDBCRC_XSTATIC") && atoi(getenv("FDBCRC_XSTATIC")) == 1;
+	xs->ctr = nullptr;
+	if (!stat && page_counters(s, st->num_cus, &xs->ctr)) xs->ctr = nullptr;
 	if (++ss->xepoch == 0) ++ss->xepoch;
 	xs->epoch = ss->xepoch;
 	return true;
@@ -279,7 +284,7 @@ uint64_t stream_bytes(hipStream_t stream) {
 	auto it = st->streams.find(stream);
 	if (it == st->streams.end()) return 0;
 	return it->second->ws_bytes + it->second->ctr_bytes +
-	       (it->second->xmem ? extent_state_bytes(it->second->xcount, st->num_cus) : 0);
+	       (it->second->xmem ? extent_state_bytes(it->second->xcount, kXGrabCap, st->num_cus) : 0);
 }
 
 // used by the host pipeline (crc32c_pipeline.cpp)

@@ -92,16 +92,30 @@ inline int route_for_stats(const volatile uint64_t* s) {
 // per buffer its start and end points' captured values {G, Y}; per wave of
 // the streaming kernel its range's aggregate register.
 constexpr uint64_t kXMaxExtent = 1ull << 40;  // 32-bit block numbers with room
+// Grabs of the dynamic stream kernel (k_xgrab): kXGrabMin blocks, more when the
+// extent has more than capg grabs of that size, so the per-grab arrays never
+// overflow whatever the extent.
+constexpr uint64_t kXGrabMin = 8;
+__host__ __device__ inline uint64_t x_gsz(uint64_t nblk, uint64_t capg) {
+	const uint64_t g = (nblk + kXGrabMin - 1) / kXGrabMin;
+	const uint64_t f = capg ? (g + capg - 1) / capg : 1;
+	return kXGrabMin * (f ? f : 1);
+}
+constexpr uint64_t kXGrabCap = 1ull << 18;  // grabs the per-stream state holds (2 MiB)
 struct XState {
 	uint32_t* xhdr;
 	uint32_t* ps;         // per buffer, 2 words: its start point's G and Y (k_xstream)
 	uint32_t* pe;         // ... its end point's
 	uint32_t* dummy;      // 128 words per wave of the stream kernel
-	uint32_t* ragg;       // per stream wave: the range-local prefix at its range's end
+	uint32_t* ragg;       // per stream wave: the range-local prefix at its range's end (k_xstream)
+	uint32_t* wq;         // per grab: the first buffer ending past its start (k_v7count; k_xgrab)
+	uint32_t* gagg;       // per grab: its grab-local prefix at its end (k_xgrab)
+	uint64_t capg;        // grabs wq / gagg hold
+	uint32_t* ctr;        // the stream's page-kernel grab counters (k_xgrab); null: static ranges
 	uint32_t epoch;       // this launch (never 0)
 };
-uint64_t extent_state_bytes(uint64_t count, int num_cus);
-void extent_state_carve(void* mem, uint64_t count, int num_cus, XState* x);
+uint64_t extent_state_bytes(uint64_t count, uint64_t capg, int num_cus);
+void extent_state_carve(void* mem, uint64_t count, uint64_t capg, int num_cus, XState* x);
 uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 // err (device-visible, may be null): set to 1 (never cleared here) when the
 // planner refuses the batch -- 2^32 - 1 or more 1 KiB windows or 4 KiB route

@@ -75,6 +75,8 @@ struct XParams {
 	const DevTables* tabs;
 	uint64_t* hstat;
 	uint64_t nwave;  // waves of k_xstream (its static ranges)
+	uint32_t* ctr;   // k_xgrab: the stream's per-workgroup grab counters (page_counters)
+	bool grabs;      // k_xgrab streamed the batch (else k_xstream's static ranges)
 };
 
 __device__ __forceinline__ void x_buffer(const XParams& P, uint64_t i, uint64_t& P0, uint64_t& P1) {
@@ -362,6 +364,262 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 }
 
 // ---------------------------------------------------------------------------
+// k_xgrab: the extent as 4 KiB blocks in GRABS of gsz blocks (x_gsz: 8 or
+// more), taken dynamically by the waves of a workgroup -- the page kernel's
+// load balance (a static share per wave finishes unevenly: the SIMD's issue
+// arbitration favours some waves).  A grab is self-contained: its prefix X
+// starts at 0 at its first block, its points are captured grab-local from a
+// window of buffers starting at wq[g] (the first buffer ending past the
+// grab's start, written by k_v7count), and its aggregate X at its end is
+// gagg[g]; k_xfin chains the grabs a buffer spans (the range form of
+// tests/extent_model.py with per = gsz).
+// The grabs [0, ngrab - 1) are full blocks and stream without clamping; the
+// last grab, which holds the extent's partial last block, goes first to
+// wave 0 of workgroup 0 with clamped chunk addresses.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
+	if (!x_packed(P)) return;  // k_xfin checksums this batch buffer by buffer
+	if (x_geo(P).nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
+	FillRegs fill;
+	fill_issue_1024(fill, P.tabs);
+	__shared__ uint32_t lds[kLdsBytesB / 4];
+	const XGeo G = x_geo(P);
+	const LaneCtx c = make_ctx();
+	const uint32_t lane = (uint32_t)c.lane;
+	const uint32_t col4 = (lane & 31) * 4;
+	const uint32_t c4 = col4 | 0x10000u;
+	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
+	const uint32_t wpb = blockDim.x >> 6;
+	const uint32_t wi = rdfirst(threadIdx.x >> 6);
+	const uint32_t w = blockIdx.x * wpb + wi;
+	// (32-bit block, grab and buffer numbers: the extent is below 2^40 bytes,
+	// the grabs at most kXGrabCap, the route takes batches of < 2^32 buffers)
+	const uint32_t nblk = (uint32_t)G.nblk;
+	const uint32_t gsz = (uint32_t)x_gsz(nblk, P.x.capg);  // blocks per grab
+	const uint32_t ngrab = (nblk + gsz - 1) / gsz;
+	const uint32_t spg = gsz / 4;                          // steps of 4 blocks per grab
+	const uint32_t nd = ngrab - 1;                         // dynamic grabs [0, nd)
+	const uint32_t gper = (nd + gridDim.x - 1) / gridDim.x;
+	const uint32_t g0 = blockIdx.x * gper < nd ? blockIdx.x * gper : nd;
+	const uint32_t g1 = g0 + gper < nd ? g0 + gper : nd;
+	const uint32_t cnt32 = (uint32_t)P.count;
+	uint32_t* const my_ctr = P.ctr + kPageCtrWords * blockIdx.x;
+	auto clampg = [&](uint32_t g) { return g < g1 ? g : nd; };  // nd: nothing left
+	auto request = [&]() -> uint32_t {
+		uint32_t r = 0;
+		if (lane == 0) r = atomicAdd(my_ctr, 1u);
+		return r;
+	};
+	auto blk_ptr = [&](uint32_t k) { return reinterpret_cast<const uint8_t*>(G.S + 4096ull * k); };
+	// a dynamic step's blocks (a step past the wave's grabs re-reads block 0: discarded)
+	auto load_step_unit = [&](Block (&u)[kXU], uint32_t g, uint32_t s, uint32_t half) {
+		const uint32_t k = g < nd ? g * gsz + 4 * s + 2 * half : 0;
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) load_block(u[j], blk_ptr(k + j), c.ld_off);
+	};
+	uint32_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
+	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
+	Block u0[kXU], u1[kXU];
+	// wave 0 of workgroup 0 streams the last grab first (below): its first
+	// dynamic unit is loaded after that
+	const bool lastg = blockIdx.x == 0 && wi == 0;
+	if (!lastg && gA < nd) load_step_unit(u0, gA, 0, 0);  // (nd > 0: block 0 is a full block)
+	uint32_t* const dmy = P.x.dummy + 128 * w;
+
+	// ---- window of 64 buffers (lane j <-> buffer q + j) ---------------------
+	uint32_t q = 0;
+	uint32_t wbs, wbe, wcs, wce, wqs, wqe, wlast;
+	uint32_t Vs = 0, Ve = 0, Ys = 0, Ye = 0;
+	uint64_t pf0 = 0, pf1 = 0;  // the next window's buffer (prefetched)
+	auto prefetch = [&](uint32_t q0) {
+		const uint32_t j = q0 + lane < cnt32 ? q0 + lane : cnt32 - 1;
+		x_buffer(P, j, pf0, pf1);
+	};
+	auto make_window = [&](uint32_t q0) {
+		const bool ok = q0 + lane < cnt32;
+		const uint64_t s = pf0 - G.S, e = pf1 - G.S;
+		wbs = ok ? x_blk(s) : 0xFFFFFFFEu;
+		wbe = ok ? x_blk(e) : 0xFFFFFFFEu;
+		wcs = x_cnt(s, wbs);
+		wce = x_cnt(e, wbe);
+		wqs = ((uint32_t)s >> 4) & 3u;
+		wqe = ((uint32_t)e >> 4) & 3u;
+		wlast = (uint64_t)q0 + 64 <= cnt32 ? rdlane(wbe, 63) : 0xFFFFFFFFu;  // the batch's last window never retires
+		Vs = Ve = Ys = Ye = 0;
+	};
+	// the window's points in blocks [kb0, kb1) leave (unconditional stores)
+	auto flush = [&](uint32_t q0, uint32_t kb0, uint32_t kb1) {
+		const bool ok = q0 + lane < cnt32;
+		const bool os = ok && wbs >= kb0 && wbs < kb1, oe = ok && wbe >= kb0 && wbe < kb1;
+		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+		*reinterpret_cast<u32x2*>(os ? P.x.ps + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Vs, Ys};
+		*reinterpret_cast<u32x2*>(oe ? P.x.pe + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Ve, Ye};
+	};
+	auto wq_of = [&](uint32_t g) -> uint32_t { return rdfirst(xld32(P.x.wq + g)); };
+	if (gA < nd) {
+		q = wq_of(gA);
+		prefetch(q);
+	}
+
+	fill_commit_1024(fill, lds);
+
+	uint32_t X = 0;  // the grab-local prefix at the next block
+	auto mulM = [&](uint32_t v) -> uint32_t {  // v * x^(8*4096), uniform (lane tables of lanes 0 and 62)
+		const uint32_t n = lane & 7;
+		uint32_t t = lds_rd(lds, kS4LaneOff + ((n * 16 + ((v >> (4 * n)) & 15u)) << 7));
+		t ^= __builtin_amdgcn_update_dpp(0u, t, 0xB1, 0xF, 0xF, false);
+		t ^= __builtin_amdgcn_update_dpp(0u, t, 0x4E, 0xF, 0xF, false);
+		t ^= __builtin_amdgcn_update_dpp(0u, t, 0x124, 0xF, 0xF, false);
+		t = rdfirst(t);
+		uint32_t u = lds_rd(lds, kS4LaneOff + 4 * (4096 + (n * 16 + ((t >> (4 * n)) & 15u)) * 32 + 30));
+		u ^= __builtin_amdgcn_update_dpp(0u, u, 0xB1, 0xF, 0xF, false);
+		u ^= __builtin_amdgcn_update_dpp(0u, u, 0x4E, 0xF, 0xF, false);
+		u ^= __builtin_amdgcn_update_dpp(0u, u, 0x124, 0xF, 0xF, false);
+		return rdfirst(u);
+	};
+	auto unit_h = [&](Block (&u)[kXU], uint32_t (&H)[kXU], uint32_t (&Y)[kXU][3]) {
+		uint32_t x[kXU];
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) {
+			unswizzle(u[j]);
+			x[j] = u[j].r[0][0];
+		}
+#pragma unroll
+		for (int wd = 0; wd < 16; ++wd)
+#pragma unroll
+			for (uint32_t j = 0; j < kXU; ++j) {
+				const uint32_t nx = wd < 15 ? u[j].r[(wd + 1) >> 2][(wd + 1) & 3] : 0u;
+				x[j] = word_step4_next(lds, x[j], nx, c4);
+				if (wd == 3 || wd == 7 || wd == 11) Y[j][(wd >> 2)] = x[j] ^ nx;
+			}
+#pragma unroll
+		for (uint32_t j = 0; j < kXU; ++j) H[j] = wave_scanx(mul_nibbles(lds, x[j], c_lane));
+	};
+	auto capture = [&](uint32_t H, const uint32_t (&Yb)[3], uint32_t Zb, uint32_t kb, bool valid) {
+		const bool hs = valid && wbs == kb, he = valid && wbe == kb;
+		const uint32_t ts = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((wcs ? wcs - 1 : 0) << 2), (int)H);
+		const uint32_t te = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((wce ? wce - 1 : 0) << 2), (int)H);
+		Vs = hs ? Zb ^ (wcs ? ts : 0u) : Vs;
+		Ve = he ? Zb ^ (wce ? te : 0u) : Ve;
+		auto pull = [&](uint32_t cnt, uint32_t qd) -> uint32_t {
+			const int a = (int)((cnt & 63u) << 2);
+			const uint32_t y1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)Yb[0]);
+			const uint32_t y2 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)Yb[1]);
+			const uint32_t y3 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)Yb[2]);
+			return qd == 1 ? y1 : qd == 2 ? y2 : qd == 3 ? y3 : 0u;
+		};
+		if (__ballot(hs && wqs)) {
+			const uint32_t y = pull(wcs, wqs);
+			Ys = hs ? y : Ys;
+		}
+		if (__ballot(he && wqe)) {
+			const uint32_t y = pull(wce, wqe);
+			Ye = he ? y : Ye;
+		}
+	};
+	// blocks k .. k + 3 of grab [gb0, gb1) (those before kend): the prefix
+	// chain, the points, windows retired inside the grab
+	auto finish = [&](const uint32_t (&H)[2 * kXU], const uint32_t (&Y)[2 * kXU][3], uint32_t k, uint32_t kend,
+	                  uint32_t gb0, uint32_t gb1) {
+		uint32_t Z[2 * kXU];
+#pragma unroll
+		for (uint32_t j = 0; j < 2 * kXU; ++j) {
+			Z[j] = mulM(X);
+			if (k + j < kend) X = Z[j] ^ rdlane(H[j], 63);
+		}
+#pragma unroll
+		for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
+		const uint32_t kn = k + 2 * kXU < kend ? k + 2 * kXU : kend;
+		while (wlast < kn) {  // every buffer of the window ends in the blocks so far: the next 64
+			flush(q, gb0, gb1);
+			q += 64;
+			make_window(q);
+			prefetch(q + 64);
+#pragma unroll
+			for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
+		}
+	};
+
+	// ---- the last grab (partial last block): clamped loads, no pipelining ----
+	if (lastg) {
+		const uint32_t gb0 = nd * gsz, gb1 = nblk;
+		const uint64_t last_chunk = G.Eend - 16;
+		const uint32_t ql = wq_of(nd);
+		prefetch(ql);
+		make_window(ql);
+		q = ql;
+		prefetch(q + 64);
+		X = 0;
+		for (uint32_t s = 0; s < spg && gb0 + 4 * s < nblk; ++s) {
+			uint32_t H[2 * kXU], Y[2 * kXU][3];
+#pragma unroll
+			for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+				for (uint32_t j = 0; j < kXU; ++j) {
+					const uint64_t a = G.S + 4096ull * (gb0 + 4 * s + 2 * h + j) + c.ld_off;
+#pragma unroll
+					for (int q2 = 0; q2 < 4; ++q2) {
+						const uint64_t o = a + 2048u * (q2 & 1) + 1024u * (q2 >> 1);
+						u1[j].r[q2] = ld16(reinterpret_cast<const uint8_t*>(o <= last_chunk ? o : last_chunk));
+					}
+				}
+				unit_h(u1, reinterpret_cast<uint32_t(&)[kXU]>(H[2 * h]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[2 * h]));
+			}
+			finish(H, Y, gb0 + 4 * s, gb1, gb0, gb1);
+		}
+		flush(q, gb0, gb1);
+		if (lane == 0) P.x.gagg[nd] = X;
+		// back to this wave's first dynamic grab
+		if (gA < nd) {
+			q = wq_of(gA);
+			prefetch(q);
+			load_step_unit(u0, gA, 0, 0);
+		}
+	}
+
+	// ---- dynamic grabs: steps of 4 blocks, two units in ping-pong ----------
+	uint32_t s = 0;
+	while (gA < nd) {
+		const uint32_t gb0 = gA * gsz, gb1 = gb0 + gsz;
+		const uint32_t k = gb0 + 4 * s;
+		uint32_t H[2 * kXU], Y[2 * kXU][3];
+		if (s == 0) {  // the grab's window (its metadata was prefetched a grab ahead)
+			make_window(q);
+			prefetch(q + 64);
+			X = 0;
+		}
+		load_step_unit(u1, gA, s, 1);
+		__builtin_amdgcn_sched_barrier(0);
+		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[0]));
+		__builtin_amdgcn_sched_barrier(0);
+		const bool last_step = s + 1 == spg;
+		uint32_t qn = 0;
+		if (last_step && gB < nd) qn = wq_of(gB);  // (scalar load, ahead of the next unit's loads)
+		load_step_unit(u0, last_step ? gB : gA, last_step ? 0u : s + 1, 0);
+		__builtin_amdgcn_sched_barrier(0);
+		unit_h(u1, reinterpret_cast<uint32_t(&)[kXU]>(H[kXU]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[kXU]));
+		__builtin_amdgcn_sched_barrier(0);
+		finish(H, Y, k, gb1, gb0, gb1);
+		if (last_step) {
+			flush(q, gb0, gb1);
+			if (lane == 0) P.x.gagg[gA] = X;
+			q = qn;
+			if (gB < nd) prefetch(q);  // the next grab's window, consumed a step later
+			gA = gB;
+			gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
+			req = request();
+			s = 0;
+		} else {
+			++s;
+		}
+	}
+	// every request of every wave has returned: the counter goes back to zero
+	__builtin_amdgcn_s_waitcnt(0);
+	__syncthreads();
+	if (threadIdx.x == 0) *my_ctr = 0;
+}
+
+// ---------------------------------------------------------------------------
 // v * M^m for 0 <= m < 2^32 blocks (bpow: x^(8*4096*j*256^i)); the levels no
 // lane needs are skipped.
 __device__ __forceinline__ uint32_t xmul_blocks(const DevTables* T, uint32_t v, uint32_t m) {
@@ -477,7 +735,9 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 			P.out[i] = P.seeds ? xld32(P.seeds + i) : P.seed;
 		return;
 	}
-	const uint64_t per = x_per(G.nblk, P.nwave);
+	// the chained units: k_xgrab's grabs or k_xstream's static ranges
+	const uint64_t per = P.grabs ? x_gsz(G.nblk, P.x.capg) : x_per(G.nblk, P.nwave);
+	const uint32_t* const agg = P.grabs ? P.x.gagg : P.x.ragg;
 	const uint32_t* s4 = lds + kFinS4;
 #ifndef FDBX_NOFILL
 	fin_fill(lds, T);
@@ -517,7 +777,14 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		const uint64_t ws = ks / per, we = ke / per;
 		if (ws != we) {
 			uint32_t D = 0;
-			for (uint64_t v = ws; v < we; ++v) D = lmul(lds, kFinC, D) ^ xld32(P.x.ragg + v);
+			for (uint64_t v = ws; v < we; v += 8) {  // eight aggregates in flight per round trip
+				uint32_t a[8];
+#pragma unroll
+				for (uint32_t t = 0; t < 8; ++t) a[t] = xld32(agg + (v + t < we ? v + t : we - 1));
+#pragma unroll
+				for (uint32_t t = 0; t < 8; ++t)
+					if (v + t < we) D = lmul(lds, kFinC, D) ^ a[t];
+			}
 			const uint32_t j = (uint32_t)(ke - we * per + 1);
 			ge ^= j < 64 ? lmul(lds, kFinBp0 + 128 * j, D) : xmul_blocks(T, D, j);
 		}
@@ -572,12 +839,12 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 // ---------------------------------------------------------------------------
 static uint64_t xal(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
-uint64_t extent_state_bytes(uint64_t count, int num_cus) {
+uint64_t extent_state_bytes(uint64_t count, uint64_t capg, int num_cus) {
 	const uint64_t nwave = (uint64_t)num_cus * 16;
-	return 256 + 2 * xal(8 * count) + xal(512 * nwave) + xal(4 * nwave);
+	return 256 + 2 * xal(8 * count) + xal(512 * nwave) + xal(4 * nwave) + 2 * xal(4 * capg);
 }
 
-void extent_state_carve(void* mem, uint64_t count, int num_cus, XState* x) {
+void extent_state_carve(void* mem, uint64_t count, uint64_t capg, int num_cus, XState* x) {
 	uint8_t* p = static_cast<uint8_t*>(mem);
 	const uint64_t nwave = (uint64_t)num_cus * 16;
 	x->xhdr = reinterpret_cast<uint32_t*>(p);
@@ -589,6 +856,11 @@ void extent_state_carve(void* mem, uint64_t count, int num_cus, XState* x) {
 	x->dummy = reinterpret_cast<uint32_t*>(p);
 	p += xal(512 * nwave);
 	x->ragg = reinterpret_cast<uint32_t*>(p);
+	p += xal(4 * nwave);
+	x->wq = reinterpret_cast<uint32_t*>(p);
+	p += xal(4 * capg);
+	x->gagg = reinterpret_cast<uint32_t*>(p);
+	x->capg = capg;
 }
 
 // phase 0: the streaming kernel; phase 1: the finishing kernel.  Both return
@@ -602,9 +874,14 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 	P.base = base; P.offsets = offsets; P.lengths = lengths; P.stride = stride; P.length = length; P.count = count;
 	P.seed = seed; P.seeds = seeds; P.out = out; P.x = xs; P.tabs = tabs; P.hstat = hstat;
 	P.nwave = (uint64_t)num_cus * 16;  // k_xstream: one 1024-thread workgroup per CU
-	if (phase == 0)
-		k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
-	else {
+	P.ctr = xs.ctr;
+	P.grabs = xs.ctr != nullptr && xs.wq != nullptr;
+	if (phase == 0) {
+		if (P.grabs)
+			k_xgrab<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+		else
+			k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+	} else {
 		// persistent, but no more workgroups than the buffers fill (each fills 133 KiB of LDS)
 		const uint64_t g = (count + kFinThreads - 1) / kFinThreads;
 		k_xfin<<<(unsigned)(g < (uint64_t)num_cus ? g : (uint64_t)num_cus), kFinThreads, 0, stream>>>(P);

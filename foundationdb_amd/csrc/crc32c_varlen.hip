@@ -385,6 +385,8 @@ struct V7Params {
 	// are not launched)
 	uint32_t* xhdr;            // [0] / [1]: epoch of the last launch found not packed / over kXMaxExtent
 	uint32_t epoch;
+	uint32_t* xwq;             // per grab of k_xgrab: the first buffer ending past its start (may be null)
+	uint64_t xcapg;            // ... grabs it holds
 };
 // hdr[6]: 1 if the planner refused the batch (2^32 - 1 or more windows or
 // blocks: 32-bit slot indices); the streaming kernels then do nothing.
@@ -456,6 +458,33 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 			if (P.hstat) P.hstat[kHstatNblk] = nblk;
 		}
 		if (blockIdx.x == 0 && P.hstat) v7_route_stats(P, i, off, len, s_stat);
+		// k_xgrab's grab map: buffer i is the first to end past the start T(g)
+		// of grabs g with end(i-1) <= T(g) < end(i); the last buffer also
+		// covers the grabs after its end.  Only ordered pairs write (a batch
+		// that is not packed is never streamed), at most the grabs that exist.
+		if (P.xwq && i < P.count) {
+			uint64_t o0, l0, o1, l1;
+			v7_buffer(P, 0, o0, l0);
+			v7_buffer(P, P.count - 1, o1, l1);
+			const uint64_t S = (reinterpret_cast<uint64_t>(P.base) + o0) & ~uint64_t(15);
+			const uint64_t E = (reinterpret_cast<uint64_t>(P.base) + o1 + l1 + 15) & ~uint64_t(15);
+			const uint64_t nblk = E > S ? (E - S + 4095) >> 12 : 0;
+			const uint64_t gsz = x_gsz(nblk, P.xcapg), ngrab = (nblk + gsz - 1) / gsz, tg = 4096 * gsz;
+			const uint64_t Pe = reinterpret_cast<uint64_t>(P.base) + off + len;
+			uint64_t pe = 0;
+			if (i) {
+				uint64_t op, lp;
+				v7_buffer(P, i - 1, op, lp);
+				pe = reinterpret_cast<uint64_t>(P.base) + op + lp;
+			}
+			if (nblk && E - S < kXMaxExtent && Pe >= S && (i == 0 || (pe >= S && pe <= Pe))) {
+				const uint64_t ep = i ? pe - S : 0, ei = Pe - S;
+				const uint64_t glo = (ep + tg - 1) / tg;
+				uint64_t ghi = (ei + tg - 1) / tg;
+				if (i + 1 == P.count) ghi = ngrab;
+				for (uint64_t g = glo; g < ghi && g < ngrab; ++g) P.xwq[g] = (uint32_t)i;
+			}
+		}
 	}
 	W = scan_sadd(W);
 	B = scan_sadd(B);
@@ -1156,6 +1185,10 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	if (extent) {
 		P.xhdr = xs->xhdr;
 		P.epoch = xs->epoch;
+		if (xs->ctr) {
+			P.xwq = xs->wq;
+			P.xcapg = xs->capg;
+		}
 	}
 	P.hdr = reinterpret_cast<uint64_t*>(wp);      // [0..3] totals and quantum, [kHdrRefused] refusal flag
 	P.tsum = reinterpret_cast<uint64_t*>(wp + 64);

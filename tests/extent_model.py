@@ -144,7 +144,7 @@ def ranges_per(nblk, nwave, unit=4):
     return (per + unit - 1) // unit * unit
 
 
-def extent_crcs_ranges(mem, offsets, lengths, seed, nwave):
+def extent_crcs_ranges(mem, offsets, lengths, seed, nwave, per=None):
     """The same CRCs the way the kernels compute them since round 4, without a
     scan over all blocks: wave w streams the blocks [k0, k1) = [w*per, ...) of
     its RANGE and keeps the range-local prefix X (0 at k0) itself, block by
@@ -177,7 +177,10 @@ def extent_crcs_ranges(mem, offsets, lengths, seed, nwave):
             acc ^= gf2_mul(int(spans[64 * k + l]), lane_w[l])
             h.append(acc)
         H.append(h)
-    per = ranges_per(nblk, nwave) if nblk else 4
+    if per is None:
+        per = ranges_per(nblk, nwave) if nblk else 4
+    else:  # k_xgrab's grabs of `per` blocks
+        nwave = max(1, -(-nblk // per))
     Z, A = [0] * nblk, []
     for w in range(nwave):
         k0, k1 = min(w * per, nblk), min(w * per + per, nblk)

@@ -93,3 +93,85 @@ def schedule(P0, P1, nwave):
             finish(km, k1)
         flush()
     return vs, ve, blk, S, nblk
+
+
+def grab_map(P0, P1, gsz):
+    """k_v7count's wq[]: per grab, the first buffer ending past its start."""
+    S = P0[0] & ~15
+    Eend = (P1[-1] + 15) & ~15
+    nblk = (Eend - S + 4095) >> 12
+    ngrab = -(-nblk // gsz)
+    tg = 4096 * gsz
+    wq = [None] * ngrab
+    for i in range(len(P0)):
+        ep = P1[i - 1] - S if i else 0
+        ei = P1[i] - S
+        lo = -(-ep // tg) if i else 0
+        hi = ngrab if i + 1 == len(P0) else -(-ei // tg)
+        for g in range(lo, min(hi, ngrab)):
+            wq[g] = i
+    return wq, S, nblk, ngrab
+
+
+def schedule_grabs(P0, P1, gsz, order):
+    """k_xgrab's control flow: grab g (gsz blocks) is processed from a window
+    starting at wq[g], in steps of 4 blocks, retiring windows inside the grab
+    and flushing only the points of the grab's blocks.  `order` is the
+    sequence in which grabs are processed (any order: they are independent).
+    Returns (vs, ve, blk) as schedule() does, blk[k] = grabs that folded block k."""
+    n = len(P0)
+    wq, S, nblk, ngrab = grab_map(P0, P1, gsz)
+    assert all(v is not None for v in wq), "every grab has its first buffer"
+    vs = [[] for _ in range(n)]
+    ve = [[] for _ in range(n)]
+    blk = [[] for _ in range(nblk)]
+    for g in order:
+        gb0, gb1 = g * gsz, min(g * gsz + gsz, nblk)
+        win = {}
+
+        def make_window(q0):
+            win.clear()
+            win.update({"q": q0, "bs": [], "be": [], "cs": [], "ce": [], "Vs": [0] * 64, "Ve": [0] * 64})
+            for j in range(64):
+                if q0 + j < n:
+                    s, e = P0[q0 + j] - S, P1[q0 + j] - S
+                    win["bs"].append(x_blk(s)); win["be"].append(x_blk(e))
+                    win["cs"].append(x_cnt(s, x_blk(s))); win["ce"].append(x_cnt(e, x_blk(e)))
+                else:
+                    win["bs"].append(-2); win["be"].append(-2); win["cs"].append(0); win["ce"].append(0)
+            win["last"] = win["be"][63] if q0 + 64 <= n else float("inf")
+
+        def flush():
+            q0 = win["q"]
+            for j in range(64):
+                if q0 + j >= n:
+                    continue
+                if gb0 <= win["bs"][j] < gb1:
+                    vs[q0 + j].append((g, win["Vs"][j]))
+                if gb0 <= win["be"][j] < gb1:
+                    ve[q0 + j].append((g, win["Ve"][j]))
+
+        def capture(kb, valid):
+            for j in range(64):
+                if valid and win["bs"][j] == kb:
+                    c = win["cs"][j]
+                    win["Vs"][j] = (kb, c - 1) if c else 0
+                if valid and win["be"][j] == kb:
+                    c = win["ce"][j]
+                    win["Ve"][j] = (kb, c - 1) if c else 0
+
+        make_window(wq[g])
+        for k in range(gb0, gb1, 4):
+            for j in range(4):
+                if k + j < gb1:
+                    blk[k + j].append(g)
+            for j in range(4):
+                capture(k + j, k + j < gb1)
+            kn = min(k + 4, gb1)
+            while win["last"] < kn:
+                flush()
+                make_window(win["q"] + 64)
+                for j in range(4):
+                    capture(k + j, k + j < gb1)
+        flush()
+    return vs, ve, blk, S, nblk

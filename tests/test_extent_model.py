@@ -128,3 +128,65 @@ def test_range_form_across_block_groups(nwave):
     want = O.batch_varlen(mem, np.array(offs, np.uint64), np.array(lens, np.uint64), seed=7)
     got = X.extent_crcs_ranges(mem, offs, lens, 7, nwave)
     assert np.array_equal(got, want)
+
+
+def _check_grabs(P0, P1, gsz, rng):
+    from tests import extent_sched_model as M
+    wq, S, nblk, ngrab = M.grab_map(P0, P1, gsz)
+    order = list(rng.permutation(ngrab))
+    vs, ve, blk, S, nblk = M.schedule_grabs(P0, P1, gsz, order)
+    assert all(len(b) == 1 for b in blk), "every block folded into its grab's prefix exactly once"
+    for i, (a, b) in enumerate(zip(P0, P1)):
+        for p, rec in ((a - S, vs[i]), (b - S, ve[i])):
+            k = M.x_blk(p)
+            c = M.x_cnt(p, k)
+            want = (k, c - 1) if c else 0
+            if p == 0:
+                assert len(rec) <= 1 and all(v == 0 for _, v in rec)
+                continue
+            assert len(rec) == 1, (i, p, rec)
+            assert rec[0][1] == want, (i, p, rec, want)
+            assert rec[0][0] == k // gsz
+
+
+@pytest.mark.parametrize("gsz", [8, 16, 24])
+def test_grab_schedule_captures_every_point_once(gsz):
+    """k_xgrab's control flow (grabs in any order, each from the window
+    k_v7count's grab map gives it, windows retired inside a grab, only the
+    grab's points flushed): every point is captured exactly once, by its
+    block's grab, from the right block and lane span."""
+    rng = np.random.default_rng(gsz)
+    for trial in range(12):
+        P0, P1, pos = [], [], int(rng.integers(0, 4096))
+        n = int(rng.integers(1, 600))
+        kind = trial % 4
+        for _ in range(n):
+            L = int({0: rng.integers(1, 300), 1: rng.integers(0, 20000), 2: rng.choice([0, 1, 63, 64, 65, 4096]),
+                     3: rng.integers(2000, 70000)}[kind])
+            g = int(rng.integers(0, min(max(L, 256), 4095) + 1)) if trial % 3 else 0
+            P0.append(pos)
+            P1.append(pos + L)
+            pos += L + g
+        _check_grabs(P0, P1, gsz, rng)
+    _check_grabs([0], [1 << 20], gsz, rng)
+    _check_grabs([5], [5 + 4091], gsz, rng)
+    _check_grabs([16, 100], [50, 4000], gsz, rng)
+
+
+@pytest.mark.parametrize("gsz", [8, 16])
+def test_grab_form_matches_oracle(gsz):
+    """The grab form's arithmetic: per = gsz blocks chained by the finishing
+    pass (straddling buffers: Horner over the grab aggregates)."""
+    rng = np.random.default_rng(70 + gsz)
+    mem = sm(900 << 10, 0x6A + gsz)
+    offs, lens, pos = [], [], 3
+    while True:
+        L = int(rng.integers(0, 30000)) if rng.random() < 0.8 else int(rng.integers(60000, 300000))
+        if pos + L > mem.size - 64:
+            break
+        offs.append(pos)
+        lens.append(L)
+        pos += L + int(rng.integers(0, min(max(L, 256), 4095) + 1))
+    want = O.batch_varlen(mem, np.array(offs, np.uint64), np.array(lens, np.uint64), seed=11)
+    got = X.extent_crcs_ranges(mem, offs, lens, 11, None, per=gsz)
+    assert np.array_equal(got, want)
