@@ -150,19 +150,22 @@ int launch_chain_fold(const uint64_t* starts, uint64_t nchains, const uint64_t* 
                       hipStream_t stream);
 // Big-buffer block route (crc32c_kernels.hip): buffers the varlen prep kernel
 // routed to 4 KiB blocks aligned to their end.  Entry q of the route's list
-// (in buffer order) is buffer eidx[q]: its blocks are [es[q], es[q+1]) of the
-// route (hdr[2] blocks, hdr[3] entries in total), eE[q] is its end rounded up
-// to 16 bytes, elot[q] = lo/16 | k0 << 8 | t << 12 (lo: bytes of its first
-// block before its first 16-byte chunk, k0: its start mod 16, t: bytes from
-// its end to eE) and esd[q] = ~seed.  out[] starts at ~0 (prep); every block
+// (in buffer order) is buffer ent[q].idx: its blocks are [ent[q].s,
+// ent[q+1].s) of the route (hdr[2] blocks, hdr[3] entries in total), ent[q].E
+// is its end rounded up to 16 bytes, ent[q].lot = lo/16 | k0 << 8 | t << 12
+// (lo: bytes of its first block before its first 16-byte chunk, k0: its start
+// mod 16, t: bytes from its end to E) and ent[q].sd = ~seed.  out[] starts at ~0 (prep); every block
 // XORs in its raw register weighted to the buffer's end.
+struct BigEnt {     // one routed buffer (24 bytes: one dwordx4 + one dwordx2 load per lane)
+	uint64_t E;     // end rounded up to 16 bytes
+	uint32_t s;     // first block of the route
+	uint32_t idx;   // output index
+	uint32_t lot;   // lo / 16 | k0 << 8 | t << 12
+	uint32_t sd;    // ~seed
+};
 struct BigParams {
 	const uint64_t* hdr;
-	const uint32_t* es;
-	const uint64_t* eE;
-	const uint32_t* eidx;
-	const uint32_t* elot;
-	const uint32_t* esd;
+	const BigEnt* ent;
 	uint32_t* out;
 	uint32_t* ctr;  // kPageCtrWords per workgroup, zeroed by prep
 	const DevTables* tabs;

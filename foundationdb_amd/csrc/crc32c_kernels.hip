@@ -303,9 +303,11 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	// entry search and the window load (dependent round trips) proceed
 	FillRegs fill;
 	fill_issue_1024(fill, P.tabs);
-	const uint64_t count = rdfirst64(gl64(P.hdr + 2));  // blocks
+	// (32-bit block, entry and grab numbers: the planner refuses batches of
+	// 2^32 - 1 or more blocks)
+	const uint32_t count = (uint32_t)rdfirst64(gl64(P.hdr + 2));  // blocks
 	if (count == 0) return;
-	const uint64_t nbig = rdfirst64(gl64(P.hdr + 3));   // entries
+	const uint32_t nbig = (uint32_t)rdfirst64(gl64(P.hdr + 3));   // entries
 	constexpr uint32_t C = 2 * U;   // blocks per grab
 	constexpr uint32_t F = 64 / C;  // grabs per store group
 	__shared__ uint32_t lds[kLdsBytesB / 4];
@@ -317,54 +319,67 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
 	const uint32_t wpb = blockDim.x >> 6;
 	const uint32_t wi = rdfirst(threadIdx.x >> 6);
-	const uint64_t ngrab = (count + C - 1) / C;
-	const uint64_t per = (ngrab + gridDim.x - 1) / gridDim.x;
-	const uint64_t g0 = (uint64_t)blockIdx.x * per;
-	const uint64_t g1 = g0 + per < ngrab ? g0 + per : ngrab;
+	const uint32_t ngrab = (uint32_t)(((uint64_t)count + C - 1) / C);
+	const uint32_t per = (ngrab + gridDim.x - 1) / gridDim.x;
+	const uint32_t g0 = blockIdx.x * per;
+	const uint32_t g1 = g0 + per < ngrab ? g0 + per : ngrab;
 	uint32_t* const my_ctr = P.ctr + kPageCtrWords * blockIdx.x;
 	const uint32_t last = (uint32_t)(count - 1);
 
 	// ---- window of route entries [wj, wj + 64) ----------------------------
-	uint64_t wj = 0;
+	uint32_t wj = 0;
 	uint32_t ws = 0, wI = 0, wL = 0, wS = 0, wend = 0;  // first block (~0: none), output index, lo | k0 | t, ~seed
 	uint64_t wE = 0;                                   // 16-byte-rounded end
-	auto load_window = [&](uint64_t j0) {
-		const uint64_t q = j0 + lane;
-		const uint64_t qc = q < nbig ? q : nbig - 1;  // clamped: every load is unconditional
-		const uint32_t s = gl32(P.es + qc);
-		wE = gl64(P.eE + qc);
-		wI = gl32(P.eidx + qc);
-		wL = gl32(P.elot + qc);
-		wS = gl32(P.esd + qc);
-		const uint64_t qe = j0 + 64 < nbig ? j0 + 64 : nbig - 1;
-		const uint32_t se = gl32(P.es + qe);
-		ws = q < nbig ? s : (q == nbig ? (uint32_t)count : ~0u);
-		wend = j0 + 64 < nbig ? rdfirst(se) : (uint32_t)count;
+	auto ent = [&](uint32_t q) -> BigEnt {
+		const uint64_t* w = reinterpret_cast<const uint64_t*>(P.ent + q);
+		const uint64_t w0 = gl64(w), w1 = gl64(w + 1), w2 = gl64(w + 2);
+		BigEnt e;
+		e.E = w0;
+		e.s = (uint32_t)w1;
+		e.idx = (uint32_t)(w1 >> 32);
+		e.lot = (uint32_t)w2;
+		e.sd = (uint32_t)(w2 >> 32);
+		return e;
+	};
+	auto ent_s = [&](uint32_t q) -> uint32_t { return gl32(&P.ent[q].s); };
+	auto load_window = [&](uint32_t j0) {
+		const uint32_t q = j0 + lane;
+		const uint32_t qc = q < nbig ? q : nbig - 1;  // clamped: every load is unconditional
+		const BigEnt e = ent(qc);
+		const uint32_t s = e.s;
+		wE = e.E;
+		wI = e.idx;
+		wL = e.lot;
+		wS = e.sd;
+		const uint32_t qe = (uint64_t)j0 + 64 < nbig ? j0 + 64 : nbig - 1;
+		const uint32_t se = ent_s(qe);
+		ws = q < nbig ? s : (q == nbig ? count : ~0u);
+		wend = (uint64_t)j0 + 64 < nbig ? rdfirst(se) : count;
 		wj = j0;
 	};
 	// the entry holding block b: the last q with es[q] <= b (64-ary narrowing)
 	// (256-ary narrowing: four samples per lane per round trip -- two rounds
 	// up to 16 Ki entries, three up to 4 Mi)
-	auto find = [&](uint32_t b) -> uint64_t {
-		uint64_t q0 = 0, n = nbig;  // es[q0] <= b
+	auto find = [&](uint32_t b) -> uint32_t {
+		uint32_t q0 = 0, n = nbig;  // es[q0] <= b
 		for (;;) {
 			if (n <= 64) {
-				const uint32_t v = gl32(P.es + q0 + (lane < n ? lane : 0));
+				const uint32_t v = ent_s(q0 + (lane < n ? lane : 0));
 				const bool le = lane < n && v <= b;
-				return q0 + __builtin_popcountll(__ballot(le)) - 1;
+				return q0 + (uint32_t)__builtin_popcountll(__ballot(le)) - 1;
 			}
-			const uint64_t stp = (n + 255) >> 8;
+			const uint32_t stp = (n + 255) >> 8;
 			uint32_t v[4];
 #pragma unroll
 			for (uint32_t u = 0; u < 4; ++u) {
 				const uint64_t k = (4 * (uint64_t)lane + u) * stp;
-				v[u] = gl32(P.es + q0 + (k < n ? k : 0));
+				v[u] = ent_s(q0 + (uint32_t)(k < n ? k : 0));
 			}
-			uint64_t cnt = 0;
+			uint32_t cnt = 0;
 #pragma unroll
 			for (uint32_t u = 0; u < 4; ++u) {
 				const uint64_t k = (4 * (uint64_t)lane + u) * stp;
-				cnt += __builtin_popcountll(__ballot(k < n && v[u] <= b));
+				cnt += (uint32_t)__builtin_popcountll(__ballot(k < n && v[u] <= b));
 			}
 			if (stp == 1) return q0 + cnt - 1;
 			q0 += (cnt - 1) * stp;
@@ -372,28 +387,28 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		}
 	};
 
-	// ---- per-grab metadata (wave-uniform) ----------------------------------
+	// ---- per-grab metadata, one block per lane -----------------------------
+	// Lane j < C holds block j of the grab: its address, its index from the
+	// buffer's end | t << 28, its first-block lead (lo/16 | k0 << 8), ~seed and
+	// output index.  (Held as wave-uniform values -- 24 SGPRs per grab, two
+	// grabs live -- they spilled 113 SGPRs.)  A block's fields are read with
+	// v_readlane where it is loaded and checksummed.
 	struct Meta {
-		uint64_t a[C];    // block address
-		uint32_t kt[C];   // block index from the buffer's end | t << 28
-		uint32_t ek[C];   // first block: lo/16 | k0 << 8, else 0
-		uint32_t sd[C];   // first block: ~seed, else 0
-		uint32_t idx[C];  // output index (~0: no block, result discarded)
+		uint32_t alo, ahi, kt, ek, sd, idx;
 	};
-	auto meta_of = [&](uint64_t g, Meta& M) {
-		const uint64_t bf = g * C;
+	auto rd = [](uint32_t v, uint32_t j) { return rdlane(v, (int)j); };
+	auto meta_of = [&](uint32_t g, Meta& M) {
+		const uint64_t bf = (uint64_t)g * C;
 		if (bf >= count) {  // nothing left: duplicates of the window's first entry's last block, discarded
 			const uint64_t a0 = rdlane64(wE, 0) - 4096;
 			// a buffer of one block starts lo bytes into it: its loads clamp there
 			const uint32_t lo16 = rdlane(ws, 1) - rdlane(ws, 0) == 1 ? rdlane(wL, 0) & 0xFFu : 0u;
-#pragma unroll
-			for (uint32_t j = 0; j < C; ++j) {
-				M.a[j] = a0;
-				M.kt[j] = 0;
-				M.ek[j] = lo16;
-				M.sd[j] = 0;
-				M.idx[j] = ~0u;
-			}
+			M.alo = (uint32_t)a0;
+			M.ahi = (uint32_t)(a0 >> 32);
+			M.kt = 0;
+			M.ek = lo16;
+			M.sd = 0;
+			M.idx = ~0u;
 			return;
 		}
 		const uint32_t b0 = (uint32_t)bf;
@@ -402,54 +417,42 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 			const uint32_t adv = b0 < wend ? (uint32_t)__builtin_popcountll(__ballot(ws <= b0)) - 1u : 64u;
 			load_window(wj + adv);
 		}
-		const int e0 = (int)__builtin_popcountll(__ballot(ws <= b0)) - 1;
-		const uint32_t se0 = rdlane(ws, e0);
-		const uint32_t sn0 = e0 < 63 ? rdlane(ws, e0 + 1) : wend;
-		if (bl < sn0) {  // the whole grab in one buffer (the common case): one lookup
-			const uint32_t m0 = b0 - se0;
-			const uint32_t k0 = sn0 - se0 - 1 - m0;
-			const uint32_t lot = rdlane(wL, e0), ix = rdlane(wI, e0);
-			const uint64_t a0 = rdlane64(wE, e0) - 4096ull * (k0 + 1);
-			const uint32_t t28 = (lot >> 12) << 28;
+		// lane j (< C): block b0 + j (past the batch's last block: a duplicate
+		// of it, result discarded); its entry e = the last window entry whose
+		// first block is <= b, one ballot per block
+		const uint32_t j = lane & (C - 1);
+		int e = 0;
 #pragma unroll
-			for (uint32_t j = 0; j < C; ++j) {
-				// blocks past the batch's last one: duplicates of it (in this same
-				// buffer), their results discarded
-				const bool valid = b0 + j <= last;
-				M.a[j] = a0 + 4096ull * (valid ? j : last - b0);
-				M.kt[j] = (k0 - j) | t28;
-				M.ek[j] = 0;
-				M.sd[j] = 0;
-				M.idx[j] = valid ? ix : ~0u;
-			}
-			if (m0 == 0) {  // ... starting at its first block
-				M.ek[0] = lot & 0xFFFu;
-				M.sd[0] = rdlane(wS, e0);
-			}
-			return;
+		for (uint32_t t = 0; t < C; ++t) {
+			const uint32_t bt = b0 + t <= last ? b0 + t : last;
+			const int et = (int)__builtin_popcountll(__ballot(ws <= bt)) - 1;
+			e = j == t ? et : e;
 		}
-#pragma unroll
-		for (uint32_t j = 0; j < C; ++j) {
-			const bool valid = b0 + j <= last;
-			const uint32_t b = valid ? b0 + j : last;
-			const int e = (int)__builtin_popcountll(__ballot(ws <= b)) - 1;
-			const uint32_t se = rdlane(ws, e);
-			const uint32_t sn = e < 63 ? rdlane(ws, e + 1) : wend;
-			const uint32_t m = b - se;             // block index from the buffer's start
-			const uint32_t k = sn - se - 1 - m;    // ... from its end
-			const uint32_t lot = rdlane(wL, e);
-			M.a[j] = rdlane64(wE, e) - 4096ull * (k + 1);
-			M.kt[j] = k | ((lot >> 12) << 28);
-			M.ek[j] = m == 0 ? lot & 0xFFFu : 0u;
-			M.sd[j] = m == 0 ? rdlane(wS, e) : 0u;
-			M.idx[j] = valid ? rdlane(wI, e) : ~0u;
-		}
+		const uint32_t b = b0 + j <= last ? b0 + j : last;
+		const int src = e << 2;
+		const uint32_t se = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ws);
+		const uint32_t sn1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4, (int)ws);
+		const uint32_t sn = e < 63 ? sn1 : wend;
+		const uint32_t lot = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wL);
+		const uint32_t eEl = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)wE);
+		const uint32_t eEh = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(wE >> 32));
+		const uint32_t sdv = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wS);
+		const uint32_t ixv = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wI);
+		const uint32_t m = b - se;           // block index from the buffer's start
+		const uint32_t k = sn - se - 1 - m;  // ... from its end
+		const uint64_t a = (((uint64_t)eEh << 32) | eEl) - 4096ull * (k + 1);
+		M.alo = (uint32_t)a;
+		M.ahi = (uint32_t)(a >> 32);
+		M.kt = k | ((lot >> 12) << 28);
+		M.ek = m == 0 ? lot & 0xFFFu : 0u;
+		M.sd = m == 0 ? sdv : 0u;
+		M.idx = b0 + j <= last ? ixv : ~0u;
 	};
 	auto load_u = [&](Block (&u)[U], const Meta& M, uint32_t j0) {
 #pragma unroll
 		for (uint32_t j = 0; j < U; ++j) {
-			const uint8_t* blk = reinterpret_cast<const uint8_t*>(M.a[j0 + j]);
-			const uint32_t lo = (M.ek[j0 + j] & 0xFFu) << 4;
+			const uint8_t* blk = reinterpret_cast<const uint8_t*>(((uint64_t)rd(M.ahi, j0 + j) << 32) | rd(M.alo, j0 + j));
+			const uint32_t lo = (rd(M.ek, j0 + j) & 0xFFu) << 4;
 			// load k = 2kb + ka reads block bytes ld_off + 2048ka + 1024kb
 #pragma unroll
 			for (int k = 0; k < 4; ++k) {
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		uint32_t spill[U];
 #pragma unroll
 		for (uint32_t j = 0; j < U; ++j) {
-			const uint32_t kt = M.kt[j0 + j], ek = M.ek[j0 + j], sd = M.sd[j0 + j];
+			const uint32_t kt = rd(M.kt, j0 + j), ek = rd(M.ek, j0 + j), sd = rd(M.sd, j0 + j);
 			spill[j] = 0;
 			if (ek | sd) {  // first block
 				const uint32_t lo = (ek & 0xFFu) << 4, k0 = ek >> 8;
@@ -526,13 +529,13 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		midx = ~0u;
 	};
 
-	auto clampg = [&](uint64_t g) { return g < g1 ? g : ngrab; };  // ngrab: nothing left
+	auto clampg = [&](uint32_t g) { return g < g1 ? g : ngrab; };  // ngrab: nothing left
 	auto request = [&]() -> uint32_t {
 		uint32_t r = 0;
 		if (lane == 0) r = atomicAdd(my_ctr, 1u);
 		return r;
 	};
-	uint64_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
+	uint32_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
 	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
 	load_window(find(g0 * C < count ? (uint32_t)(g0 * C) : last));
 	Meta MA, MB;
@@ -551,23 +554,21 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		__builtin_amdgcn_sched_barrier(0);
 		crc_u(u0, X, 0, crc);
 #pragma unroll
-		for (uint32_t j = 0; j < U; ++j) {
-			const bool me = lane == l0 + j;
-			mine = me ? crc[j] : mine;
-			mkt = me ? X.kt[j] : mkt;
-			midx = me ? X.idx[j] : midx;
+		for (uint32_t j = 0; j < U; ++j) mine = lane == l0 + j ? crc[j] : mine;
+		{  // lanes l0 .. l0 + C - 1 take the grab's blocks' kt and output index from lanes 0 .. C - 1
+			const bool mine_grab = lane - l0 < C;
+			const int src = (int)(((lane - l0) & (C - 1)) << 2);
+			const uint32_t kt = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)X.kt);
+			const uint32_t ix = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)X.idx);
+			mkt = mine_grab ? kt : mkt;
+			midx = mine_grab ? ix : midx;
 		}
 		__builtin_amdgcn_sched_barrier(0);
 		load_u(u0, Y, 0);  // the next grab's first unit
 		__builtin_amdgcn_sched_barrier(0);
 		crc_u(u1, X, U, crc);
 #pragma unroll
-		for (uint32_t j = 0; j < U; ++j) {
-			const bool me = lane == l0 + U + j;
-			mine = me ? crc[j] : mine;
-			mkt = me ? X.kt[U + j] : mkt;
-			midx = me ? X.idx[U + j] : midx;
-		}
+		for (uint32_t j = 0; j < U; ++j) mine = lane == l0 + U + j ? crc[j] : mine;
 		__builtin_amdgcn_sched_barrier(0);
 		gA = gB;
 		gB = clampg(g0 + 2 * wpb + rdlane(req, 0));

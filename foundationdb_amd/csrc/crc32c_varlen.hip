@@ -371,11 +371,7 @@ struct V7Params {
 	uint64_t bigmin;
 	uint64_t* bsum;            // per tile: blocks of its routed buffers (like tsum)
 	uint64_t* nsum;            // per tile: routed buffers
-	uint32_t* es;              // per entry: first block
-	uint64_t* eE;              // per entry: 16-byte-rounded end
-	uint32_t* eidx;            // per entry: buffer index
-	uint32_t* elot;            // per entry: lo / 16 | k0 << 8 | t << 12
-	uint32_t* esd;             // per entry: ~seed
+	BigEnt* ent;               // per entry (routed buffer): end, first block, index, lo | k0 | t, ~seed
 	uint32_t* bctr;            // block kernel grab counters (zeroed here)
 	uint32_t nbctr;            // ... words
 	uint64_t* hstat;           // route statistics of tile 0 (host-mapped, may be null): RouteStat
@@ -719,11 +715,13 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		const uint64_t q = exclN + inN + inclN - 1;
 		const uint64_t E = (P0 + len + 15) & ~uint64_t(15);
 		const uint32_t lo = (uint32_t)(4096ull * g.nb - (E - g.A));
-		P.es[q] = (uint32_t)(exclB + inB + inclB - B);
-		P.eE[q] = E;
-		P.eidx[q] = (uint32_t)i;
-		P.elot[q] = (lo >> 4) | (g.k0 << 8) | (g.zt << 12);
-		P.esd[q] = s0;
+		BigEnt ent;
+		ent.E = E;
+		ent.s = (uint32_t)(exclB + inB + inclB - B);
+		ent.idx = (uint32_t)i;
+		ent.lot = (lo >> 4) | (g.k0 << 8) | (g.zt << 12);
+		ent.sd = s0;
+		P.ent[q] = ent;
 		P.out[i] = ~0u;
 		return;
 	}
@@ -1201,16 +1199,8 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	P.dummy = P.cl + count;
 	uint8_t* rp = reinterpret_cast<uint8_t*>(P.dummy + 64 * nwave + nwave) + 64;
 	rp = reinterpret_cast<uint8_t*>(al16(reinterpret_cast<uint64_t>(rp)));
-	P.eE = reinterpret_cast<uint64_t*>(rp);
-	rp += 8 * count;
-	P.es = reinterpret_cast<uint32_t*>(rp);
-	rp += al16(4 * count);
-	P.eidx = reinterpret_cast<uint32_t*>(rp);
-	rp += al16(4 * count);
-	P.elot = reinterpret_cast<uint32_t*>(rp);
-	rp += al16(4 * count);
-	P.esd = reinterpret_cast<uint32_t*>(rp);
-	rp += al16(4 * count);
+	P.ent = reinterpret_cast<BigEnt*>(rp);
+	rp += al16(sizeof(BigEnt) * count);
 	P.bctr = reinterpret_cast<uint32_t*>(rp);
 	P.nbctr = (uint32_t)(kPageCtrWords * grid);
 	// tile prefixes: each prep block sums its predecessors (up to kScanTiles tiles);
@@ -1239,7 +1229,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 		k_v7prep_w<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.bigmin) {
 		BigParams B{};
-		B.hdr = P.hdr; B.es = P.es; B.eE = P.eE; B.eidx = P.eidx; B.elot = P.elot; B.esd = P.esd;
+		B.hdr = P.hdr; B.ent = P.ent;
 		B.out = out; B.ctr = P.bctr; B.tabs = tabs;
 		launch_bigblocks(B, num_cus, stream);
 	}
