@@ -283,9 +283,14 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 			St.v[i][1] = x[1];
 		}
 	};
-	// keys of the current seed: stripe g + 4i (secret + 8s + 16k), last stripe (secret + 121 + 16k)
-	uint64_t k0[4], k1[4], l0, l1, kseed = S.seed;
-	auto keys = [&](uint64_t sd) {
+	// keys: stripe g + 4i (secret + 8s + 16k), last stripe (secret + 121 + 16k).
+	// Seeded (SEEDS): the default secret's words are held and each key is
+	// derived at use -- word j + seed for even j, - seed for odd j
+	// (xxhash.h:3550-3566) -- instead of re-deriving a set of keys whenever the
+	// seed changes (the two sets live across the branch spilled 10 VGPRs).
+	uint64_t k0[4], k1[4], l0, l1, b15, b16, b17;
+	{
+		const uint64_t sd = SEEDS ? 0 : S.seed;
 #pragma unroll
 		for (int i = 0; i < 4; ++i) {
 			k0[i] = swd(g + 4 * i + 2 * k, sd);
@@ -293,15 +298,18 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 		}
 		l0 = sat(15 + 2 * k, 1, sd);
 		l1 = sat(16 + 2 * k, 1, sd);
-	};
-	keys(kseed);
+		b15 = kSecS[15 + 2 * k];
+		b16 = kSecS[16 + 2 * k];
+		b17 = kSecS[17 + 2 * k];
+	}
 	uint32_t tag_at = 0, tag_v = 0;  // the last computed step's tag, not yet published
 	auto compute = [&](const PStep& St) __attribute__((always_inline)) {
 		if (St.nrows == 0) return;
-		if (SEEDS && St.seed != kseed) {
-			kseed = St.seed;
-			keys(kseed);
-		}
+		// seeded keys: + seed on even secret words, - seed on odd ones (the
+		// stripe keys' word parity is g's; the last stripe's straddle two words)
+		const uint64_t sp = SEEDS ? ((g & 1) ? 0 - St.seed : St.seed) : 0;
+		const uint64_t lk0 = SEEDS ? (((b15 - St.seed) >> 8) | ((b16 + St.seed) << 56)) : l0;
+		const uint64_t lk1 = SEEDS ? (((b16 + St.seed) >> 8) | ((b17 - St.seed) << 56)) : l1;
 		const uint64_t blk = 4ull * St.t + r;
 		const uint64_t nfull = (St.len - 1) >> 10;
 		const uint32_t ns = (uint32_t)(((St.len - 1) - (nfull << 10)) >> 6);
@@ -312,8 +320,8 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 			const uint32_t s = g + 4 * i;
 			const bool last = fin && s == 15;
 			const bool on = !fin || s < ns || last;
-			const uint64_t x0 = St.v[i][0] ^ (last ? l0 : k0[i]);
-			const uint64_t x1 = St.v[i][1] ^ (last ? l1 : k1[i]);
+			const uint64_t x0 = St.v[i][0] ^ (last ? lk0 : k0[i] + sp);
+			const uint64_t x1 = St.v[i][1] ^ (last ? lk1 : k1[i] - sp);
 			const uint64_t c0 = St.v[i][1] + (uint64_t)(uint32_t)x0 * (x0 >> 32);
 			const uint64_t c1 = St.v[i][0] + (uint64_t)(uint32_t)x1 * (x1 >> 32);
 			d0 += on ? c0 : 0;
