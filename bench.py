@@ -268,6 +268,7 @@ def main():
                 "avg_launch_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": wl.algorithmic_bytes_per_step,
                 "traffic": W.pmc_traffic(args.workload),
+                "traffic_commit": W.pmc_commit(args.workload),
             },
         }
         if dry:

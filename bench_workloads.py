@@ -28,14 +28,27 @@ def _golden():
         return json.load(fh)
 
 
-def pmc_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any."""
+def pmc_record(workload):
+    """The committed rocprofv3 --pmc summary of a workload (profiles/pmc_<w>.json), if any."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None
     with open(path) as fh:
-        d = json.load(fh)
-    return d.get("hbm_bytes_per_launch")
+        return json.load(fh)
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any."""
+    d = pmc_record(workload)
+    return None if d is None else d.get("hbm_bytes_per_launch")
+
+
+def pmc_commit(workload):
+    """The commit whose code the committed --pmc summary measured: the bench
+    line carries it next to `traffic`, so a reader can tell whether the
+    counter figure is from the code being benched."""
+    d = pmc_record(workload)
+    return None if d is None else d.get("commit")
 
 
 class CpuSample:

@@ -426,10 +426,15 @@ __global__ __launch_bounds__(kCB) void k_dq_classify(const uint8_t* __restrict__
 	for (uint32_t k = 0; k < kPer; ++k) {
 		const uint64_t i = i0 + k * kCB + threadIdx.x;
 		const bool in = i < count;
-		const uint32_t ver = in ? (ld32(pages + i * 4096 + 8) >> 16) : 0xFFFFu;  // implementationVersion, bytes 10..11
+		// the page's first 16 bytes in one load (pages are 16-byte aligned): the
+		// stored hash (bytes 0..7) and implementationVersion (bytes 10..11)
+		typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+		typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+		const u32x4 h = in ? *((g_u32x4*)reinterpret_cast<uintptr_t>(pages + i * 4096)) : u32x4{0u, 0u, 0u, 0u};
+		const uint32_t ver = in ? (h[2] >> 16) : 0xFFFFu;
 		if (in) {
 			ok[i] = ver <= 2 ? kPending : 0;
-			hs[i] = ld64(pages + i * 4096);
+			hs[i] = (uint64_t)h[0] | ((uint64_t)h[1] << 32);
 		}
 		stage_push(S, 0, in && ver == 1, (uint32_t)i);
 		stage_push(S, 1, in && ver == 2, (uint32_t)i);
@@ -442,34 +447,44 @@ __global__ __launch_bounds__(kCB) void k_dq_classify(const uint8_t* __restrict__
 	if (threadIdx.x == 0 && s_bad) atomicAdd(&ctr[3], (unsigned long long)s_bad);
 }
 
-__global__ __launch_bounds__(256) void k_dq_compare(const uint8_t* __restrict__ pages, const uint32_t* __restrict__ v1_l,
+// The two lists' results against the saved hashes.  kSpan entries per
+// workgroup (kPer per thread), so the failure count takes one global atomic
+// per 4096 entries: with 256-entry workgroups and a failure in nearly every
+// one (1/16 of the bench's pages), the 4096 atomics on one word serialised
+// to ~45 us (~12 ns each).
+__global__ __launch_bounds__(kCB) void k_dq_compare(const uint8_t* __restrict__ pages, const uint32_t* __restrict__ v1_l,
                                                     const uint32_t* __restrict__ v2_l, const unsigned long long* __restrict__ ctr,
                                                     const uint32_t* __restrict__ crc_out, const uint64_t* __restrict__ xxh_out,
                                                     uint8_t* __restrict__ ok, unsigned long long* __restrict__ ctr_bad,
                                                     const uint64_t* __restrict__ hs) {
-	const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const uint64_t n1 = ctr[0], n2 = ctr[1];
-	if ((uint64_t)blockIdx.x * blockDim.x >= (n1 > n2 ? n1 : n2)) return;
+	const uint64_t j0 = (uint64_t)blockIdx.x * kSpan;
+	if (j0 >= (n1 > n2 ? n1 : n2)) return;  // uniform: the whole workgroup leaves
 	__shared__ uint32_t s_bad;
 	if (threadIdx.x == 0) s_bad = 0;
 	__syncthreads();
-	bool bad = false;
-	if (j < n1) {
-		const uint64_t i = v1_l[j];
-		const bool g = crc_out[j] == (uint32_t)hs[i];
-		ok[i] = g ? 1 : 0;
-		bad = !g;
+	uint32_t nbad = 0;
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; ++k) {
+		const uint64_t j = j0 + k * kCB + threadIdx.x;
+		if (j < n1) {
+			const uint64_t i = v1_l[j];
+			const bool g = crc_out[j] == (uint32_t)hs[i];
+			ok[i] = g ? 1 : 0;
+			nbad += g ? 0 : 1;
+		}
+		if (j < n2) {
+			const uint64_t i = v2_l[j];
+			const bool g = xxh_out[j] == hs[i];
+			ok[i] = g ? 1 : 0;
+			nbad += g ? 0 : 1;
+		}
 	}
-	const uint64_t m = __ballot(bad);
-	if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(&s_bad, (uint32_t)__builtin_popcountll(m));
-	bad = false;
-	if (j < n2) {
-		const uint64_t i = v2_l[j];
-		const bool g = xxh_out[j] == hs[i];
-		ok[i] = g ? 1 : 0;
-		bad = !g;
-	}
-	count_bad(bad, &s_bad, ctr_bad);
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) nbad += (uint32_t)__shfl_xor((int)nbad, o);
+	if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(&s_bad, nbad);
+	__syncthreads();
+	if (threadIdx.x == 0 && s_bad) atomicAdd(ctr_bad, (unsigned long long)s_bad);
 }
 
 // V0 pages: hashlittle2 over [16, 4096) -> UID(c << 32 | b, 0xFDB)
@@ -594,7 +609,7 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	P.idx = w.list_b;
 	P.d_count = n2;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_dq_compare<<<blocks(count), 256, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok, &w.ctr[3],
+	k_dq_compare<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok, &w.ctr[3],
 	                                           w.trl);
 	k_dq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ok, w.ctr);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
