@@ -68,13 +68,17 @@ int launch_pages_window_list(const uint8_t* pages, uint64_t stride, const uint32
 // device checks the packing first (k_v7count), and a batch that is not packed
 // (or whose extent outgrew the stream's arrays) is checksummed buffer by
 // buffer by the finishing kernel's fallback -- correct, slow, and the stream's
-// next batches leave the route (kHstatXfail).
+// next kXfailBackoff batches leave the route (kHstatXfail).
 enum : int { kRouteBoth = 0, kRouteWindows = 1, kRouteBlocks = 2, kRouteExtent = 3 };
 // Host-mapped per-stream words (u64 indices): [0..2] span classes of the last
 // batch's first 256 buffers, [3] extent blocks the last extent-checked batch
 // needed, [4] 1 if the last batch's first 256 buffers were packed, [5] 1 if
 // the last extent-route batch failed the full packing check, [6] refusal flag.
 constexpr int kHstatNblk = 3, kHstatPacked = 4, kHstatXfail = 5;
+// After a batch fails the extent route's packing check, the stream's next
+// kXfailBackoff batches that look packed still take the window engine (each
+// window/block-route batch counts the word down), then the route is tried again.
+constexpr uint64_t kXfailBackoff = 16;
 inline int route_for_stats(const volatile uint64_t* s) {
 	const uint64_t win = s[0], mid = s[1], large = s[2];
 	const bool big = large != 0 && large >= win + mid;  // 16 KiB+ spans hold most bytes: the block route's ground
@@ -82,7 +86,7 @@ inline int route_for_stats(const volatile uint64_t* s) {
 	// buffers (file chunks) stay on the blocks, which measured faster for them
 	// (chunks: 0.204 ms on blocks, 0.220 ms on the extent: its finishing pass
 	// and the fallback's guarded launches cost more than the blocks' padding)
-	if (s[kHstatPacked] == 1 && s[kHstatXfail] != 1 && !big) return kRouteExtent;
+	if (s[kHstatPacked] == 1 && s[kHstatXfail] == 0 && !big) return kRouteExtent;
 	if (!big) return kRouteWindows;  // (nothing windowed at all: windows, the cheaper launch)
 	return win == 0 ? kRouteBlocks : kRouteBoth;
 }

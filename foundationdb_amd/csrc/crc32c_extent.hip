@@ -772,7 +772,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	__shared__ uint32_t lds[kFinWords];
 	const bool packed = x_packed(P);
 	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat)  // for the stream's next route choice
-		P.hstat[kHstatXfail] = x_unordered(P) ? 1 : 0;
+		P.hstat[kHstatXfail] = x_unordered(P) ? kXfailBackoff : 0;
 	const DevTables* T = P.tabs;
 	if (!packed) {
 		for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) lds[kFinS4 + k] = xld32(&T->slice4[0][0] + k);

@@ -424,6 +424,10 @@ __device__ void v7_route_stats(const V7Params& P, uint64_t i, uint64_t off, uint
 	if (threadIdx.x == 0) {
 		for (int k = 0; k < 3; ++k) P.hstat[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
 		P.hstat[kHstatPacked] = (s_stat[0][3] | s_stat[1][3] | s_stat[2][3] | s_stat[3][3]) ? 0 : 1;
+		// a window/block-route batch counts the extent route's back-off down
+		// (the count kernel of an extent-route batch calls this too: k_xfin then
+		// sets the word again from that batch's check)
+		if (P.hstat[kHstatXfail] > 0 && P.hstat[kHstatXfail] <= kXfailBackoff) --P.hstat[kHstatXfail];
 	}
 }
 __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
