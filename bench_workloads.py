@@ -179,7 +179,7 @@ def _spot_check(buf, offsets, lengths, seed, got, n=512):
 
 
 class VarLen:
-    kernel_name = ("varlen engine, the batch's route: extent (k_v7count + k_xstream + k_xz + k_xfin), "
+    kernel_name = ("varlen engine, the batch's route: extent (k_v7count + k_xgrab + k_xfin), "
                    "blocks (k_v7prep_b + k_bigblocks) or windows (k_v7prep_w + k_varlen7)")
 
     def __init__(self, dev, rank, lengths, align, desc, seed=0, metric=None, shape=None):
@@ -632,6 +632,78 @@ class Xxh3Chunks(Xxh3Zipf):
                          port=lambda O_: O_.xxh3_batch_varlen(host, offs, lens, threads=1))
 
 
+class PacketsVerify:
+    """FlowTransport receive verification (scanPackets, fdbrpc/FlowTransport.cpp:1260-1366)
+    over many connections' receive buffers at once (fdb_packets_verify, include/fdb_packets.h):
+    the configs[2] Zipf packet sizes (64 B - 16 KiB payloads) framed as
+    [u32 len][u64 XXH3_64bits(payload)][payload], packed back to back into
+    64 KiB receive buffers (each holds whole frames).  The headers' checksums
+    come from the reference's own flow/xxhash.c on the host, so verify() is a
+    real check: every buffer must come back with all its frames delivered."""
+    metric = ("device-resident FlowTransport receive verification GiB/s (Zipf 64 B-16 KiB packets framed in "
+              "64 KiB receive buffers); % of HBM-read peak")
+    kernel_name = "fdbpkt::k_pkt_walk + XXH3 planner + k_xxh3_vrows + k_pkt_check + k_pkt_final"
+
+    def __init__(self, dev, rank, rbuf=64 << 10):
+        import foundationdb_amd.packets as PK
+        from oracle import oracle as O
+        self.PK = PK
+        lens = zipf_lengths().astype(np.int64)
+        lens = np.maximum(lens, 16)  # (a frame shorter than sizeof(UID) is an error: keep every frame valid)
+        frame = lens + 12
+        # receive buffers: whole frames up to rbuf bytes each
+        cs = np.cumsum(frame)
+        bid = (np.concatenate([[0], cs[:-1]]) // rbuf).astype(np.int64)
+        starts = np.concatenate([[0], cs[:-1]])
+        total = int(cs[-1])
+        first = np.flatnonzero(np.concatenate([[True], bid[1:] != bid[:-1]]))
+        boff = starts[first]
+        blen = np.diff(np.concatenate([boff, [total]]))
+        host = O.splitmix64((total + 7) // 8, STATE).view(np.uint8)[:total].copy()
+        poff = (starts + 12).astype(np.uint64)
+        ck = O.ref_xxh3_batch_varlen(host, poff, lens.astype(np.uint64)) if O.xxh3_reference_available() else \
+            O.xxh3_batch_varlen(host, poff, lens.astype(np.uint64))
+        hdr = np.zeros((lens.size, 12), np.uint8)
+        hdr[:, 0:4] = lens.astype("<u4").view(np.uint8).reshape(-1, 4)
+        hdr[:, 4:12] = ck.astype("<u8").view(np.uint8).reshape(-1, 8)
+        idx = (starts[:, None] + np.arange(12)[None, :]).reshape(-1)
+        host[idx] = hdr.reshape(-1)
+        self.buf = torch.from_numpy(host).to(dev)
+        self.h_boff, self.h_blen, self.nframes = boff, blen, np.bincount(bid)
+        self.boff = torch.from_numpy(boff.astype(np.int64)).to(dev)
+        self.blen = torch.from_numpy(blen.astype(np.int64)).to(dev)
+        self.V = PK.PacketVerifier(dev, boff.size, int(lens.size) + 1024, total)
+        self.bytes_per_step = total
+        # the receive buffers read, plus per buffer offset + length (16 B) and a 16-byte result
+        self.algorithmic_bytes_per_step = total + 32 * boff.size
+        self.data_desc = (f"synthetic: splitmix64 payloads (state 0x{STATE:X}), headers with the reference "
+                          "flow/xxhash.c XXH3_64bits; framed Zipf packets in HBM")
+        self.config = {"workload": f"{lens.size} Zipf(1.0) 64 B - 16 KiB packets framed [len][XXH3][payload] in "
+                                   f"{boff.size} receive buffers of <= {rbuf >> 10} KiB",
+                       "buffers": int(boff.size), "frames": int(lens.size), "total_bytes": total}
+        self.host = host
+
+    def step(self, stream):
+        self.V.verify(self.buf, self.boff, self.blen, stream=stream)
+
+    def verify(self):
+        r = self.V.results_numpy()
+        return bool((r["status"] == 0).all() and np.array_equal(r["frames"], self.nframes.astype(np.uint32))
+                    and np.array_equal(r["consumed"], self.h_blen.astype(np.uint64)))
+
+    def cpu_sample(self):
+        k = int(np.searchsorted(np.cumsum(self.h_blen), 256 << 20)) + 1
+        k = min(k, self.h_boff.size)
+        end = int(self.h_boff[k - 1] + self.h_blen[k - 1])
+        host = self.host[:end]
+        bo, bl = self.h_boff[:k].astype(np.uint64), self.h_blen[:k].astype(np.uint64)
+        return CpuSample(f"first {k} receive buffers ({end >> 20} MiB): scanPackets' checks restated in C "
+                         "(oracle/packets_oracle.c) over the reference's own flow/xxhash.c XXH3_64bits", end, host,
+                         ref=lambda O_: O_.packets_verify(host, bo, bl, ref=True),
+                         port=lambda O_: O_.packets_verify(host, bo, bl),
+                         ref_available=lambda O_: O_.packets_reference_available())
+
+
 WORKLOADS = {
     "pages4k": lambda dev, rank: Pages(dev, rank, 4096, 1 << 20, 0),
     "pages8k": lambda dev, rank: Pages(dev, rank, 8192, 1 << 19, 0xFDBEEFDB),
@@ -651,4 +723,5 @@ WORKLOADS = {
     "sqlite-verify": lambda dev, rank: SqliteVerify(dev, rank),
     "sqlite-verify-host": lambda dev, rank: SqliteVerifyHost(dev, rank),
     "diskqueue-verify": lambda dev, rank: DiskQueueVerify(dev, rank),
+    "packets-verify": lambda dev, rank: PacketsVerify(dev, rank),
 }
