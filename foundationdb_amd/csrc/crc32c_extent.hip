@@ -524,9 +524,17 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		uint32_t Z[2 * kXU];
 #pragma unroll
 		for (uint32_t j = 0; j < 2 * kXU; ++j) {
+#ifdef FDBX_NOMUL
+			Z[j] = X;
+#else
 			Z[j] = mulM(X);
+#endif
 			if (k + j < kend) X = Z[j] ^ rdlane(H[j], 63);
 		}
+#ifdef FDBX_NOCAP
+		if (X == 0x12345678u) Vs ^= H[0] ^ H[1] ^ H[2] ^ H[3] ^ Y[0][0] ^ Y[1][1] ^ Y[2][2] ^ Y[3][0];
+		return;
+#endif
 #pragma unroll
 		for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
 		const uint32_t kn = k + 2 * kXU < kend ? k + 2 * kXU : kend;
