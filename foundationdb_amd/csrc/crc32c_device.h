@@ -100,10 +100,16 @@ constexpr uint64_t kXMaxExtent = 1ull << 40;  // 32-bit block numbers with room
 // extent has more than capg grabs of that size, so the per-grab arrays never
 // overflow whatever the extent.
 constexpr uint64_t kXGrabMin = 8;
+// (a power of two: grab numbers are shifts, not 64-bit divisions)
 __host__ __device__ inline uint64_t x_gsz(uint64_t nblk, uint64_t capg) {
-	const uint64_t g = (nblk + kXGrabMin - 1) / kXGrabMin;
-	const uint64_t f = capg ? (g + capg - 1) / capg : 1;
-	return kXGrabMin * (f ? f : 1);
+	uint64_t gsz = kXGrabMin;
+	while (capg && (nblk + gsz - 1) / gsz > capg) gsz <<= 1;
+	return gsz;
+}
+__host__ __device__ inline uint32_t x_log2(uint64_t v) {  // v a power of two
+	uint32_t l = 0;
+	while ((1ull << l) < v) ++l;
+	return l;
 }
 constexpr uint64_t kXGrabCap = 1ull << 18;  // grabs the per-stream state holds (2 MiB)
 struct XState {

@@ -391,7 +391,6 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
 	const uint32_t wpb = blockDim.x >> 6;
 	const uint32_t wi = rdfirst(threadIdx.x >> 6);
-	const uint32_t w = blockIdx.x * wpb + wi;
 	// (32-bit block, grab and buffer numbers: the extent is below 2^40 bytes,
 	// the grabs at most kXGrabCap, the route takes batches of < 2^32 buffers)
 	const uint32_t nblk = (uint32_t)G.nblk;
@@ -424,7 +423,6 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	// dynamic unit is loaded after that
 	const bool lastg = blockIdx.x == 0 && wi == 0;
 	if (!lastg && gA < nd) load_step_unit(u0, gA, 0, 0);  // (nd > 0: block 0 is a full block)
-	uint32_t* const dmy = P.x.dummy + 128 * w;
 
 	// ---- window of 64 buffers (lane j <-> buffer q + j) ---------------------
 	uint32_t q = 0;
@@ -432,6 +430,9 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	uint32_t Vs = 0, Ve = 0, Ys = 0, Ye = 0;
 	uint64_t pf0 = 0, pf1 = 0;  // the next window's buffer (prefetched)
 	auto prefetch = [&](uint32_t q0) {
+#ifdef FDBX_NOWIN
+		if (q0 != 0x7FFFFFFFu) { pf0 = G.S + 64 * q0 + lane; pf1 = pf0 + 100; return; }
+#endif
 		const uint32_t j = q0 + lane < cnt32 ? q0 + lane : cnt32 - 1;
 		x_buffer(P, j, pf0, pf1);
 	};
@@ -447,13 +448,46 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		wlast = (uint64_t)q0 + 64 <= cnt32 ? rdlane(wbe, 63) : 0xFFFFFFFFu;  // the batch's last window never retires
 		Vs = Ve = Ys = Ye = 0;
 	};
-	// the window's points in blocks [kb0, kb1) leave (unconditional stores)
+	// The window's points in blocks [kb0, kb1) leave through a QUEUE of 64
+	// point values in the wave's lanes (lane p: point id 2i + end, G, Y),
+	// stored only when it fills: a store in the stream loop holds up every
+	// later wait on the loads issued behind it (in-order vmcnt), and one store
+	// per grab cost ~9 % of the stream (zipf, same-box A/B).  Points move into
+	// the queue with ds_permute: the window lanes with a point go to the next
+	// free slots in lane order, the others to the remaining lanes (a bijection,
+	// so every destination is written once).
+	uint32_t qid = 0, qv = 0, qy = 0, qn = 0;
+	auto store_queue = [&]() {
+		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+		if (lane < qn) *reinterpret_cast<u32x2*>((qid & 1 ? P.x.pe : P.x.ps) + 2ull * (qid >> 1)) = u32x2{qv, qy};
+		qn = 0;
+	};
+	auto push = [&](bool on, uint32_t pid, uint32_t v, uint32_t y) {
+		const uint64_t m = __ballot(on);
+		const uint32_t n = (uint32_t)__builtin_popcountll(m);
+		if (n == 0) return;
+		const uint32_t below = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+		const uint32_t dst = on ? qn + below : (qn + n + (lane - below)) & 63u;
+		const int a = (int)(dst << 2);
+		const uint32_t rp = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)pid);
+		const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)v);
+		const uint32_t ry = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)y);
+		const bool mine = lane - qn < n;  // (unsigned: lanes qn .. qn + n - 1)
+		qid = mine ? rp : qid;
+		qv = mine ? rv : qv;
+		qy = mine ? ry : qy;
+		qn += n;
+	};
 	auto flush = [&](uint32_t q0, uint32_t kb0, uint32_t kb1) {
+#ifdef FDBX_NOFLUSH
+		if (Vs != 0x12345u) return;
+#endif
 		const bool ok = q0 + lane < cnt32;
 		const bool os = ok && wbs >= kb0 && wbs < kb1, oe = ok && wbe >= kb0 && wbe < kb1;
-		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-		*reinterpret_cast<u32x2*>(os ? P.x.ps + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Vs, Ys};
-		*reinterpret_cast<u32x2*>(oe ? P.x.pe + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Ve, Ye};
+		if (qn + (uint32_t)__builtin_popcountll(__ballot(os)) > 64) store_queue();
+		push(os, 2 * (q0 + lane), Vs, Ys);
+		if (qn + (uint32_t)__builtin_popcountll(__ballot(oe)) > 64) store_queue();
+		push(oe, 2 * (q0 + lane) + 1, Ve, Ye);
 	};
 	auto wq_of = [&](uint32_t g) -> uint32_t { return rdfirst(xld32(P.x.wq + g)); };
 	if (gA < nd) {
@@ -621,6 +655,7 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			++s;
 		}
 	}
+	store_queue();
 	// every request of every wave has returned: the counter goes back to zero
 	__builtin_amdgcn_s_waitcnt(0);
 	__syncthreads();
@@ -797,6 +832,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	}
 	// the chained units: k_xgrab's grabs or k_xstream's static ranges
 	const uint64_t per = P.grabs ? x_gsz(G.nblk, P.x.capg) : x_per(G.nblk, P.nwave);
+	const uint32_t lgp = P.grabs ? x_log2(per) : 64u;  // grabs: a power of two
 	const uint32_t* const agg = P.grabs ? P.x.gagg : P.x.ragg;
 	const uint32_t* s4 = lds + kFinS4;
 #ifndef FDBX_NOFILL
@@ -817,24 +853,67 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	__syncthreads();
 	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 	typedef __attribute__((address_space(1))) const u32x2 xg_u2;
-	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t i = i0 + threadIdx.x;
-		const bool ok = i < P.count;
-		const uint64_t ic = ok ? i : P.count - 1;
-		// the captured point values do not depend on the metadata: one round trip
-		const u32x2 cs = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.ps + 2 * ic));
-		const u32x2 ce = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.pe + 2 * ic));
+	// Two buffers per thread per pass, their loads issued together: the pass
+	// is a chain of dependent round trips (metadata and point values, then the
+	// points' chunks), so two in flight halve the passes (1 Mi packets:
+	// 1.5 -> 0.8 passes of one 1024-thread workgroup per CU).
+	struct In {
+		u32x2 cs, ce;
 		uint64_t P0, P1;
-		x_buffer(P, ic, P0, P1);
-		const uint32_t sd = P.seeds ? xld32(P.seeds + ic) : P.seed;
-		const uint64_t sp = P0 - G.S, ep = P1 - G.S;
+		uint32_t sd;
+		bool ok;
+		u32x4 chs, che;
+	};
+	const uint64_t last_chunk = G.Eend - 16;
+	auto load_in = [&](In& I, uint64_t i) {
+		I.ok = i < P.count;
+		const uint64_t ic = I.ok ? i : P.count - 1;
+		// the captured point values do not depend on the metadata
+		I.cs = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.ps + 2 * ic));
+		I.ce = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.pe + 2 * ic));
+		x_buffer(P, ic, I.P0, I.P1);
+		I.sd = P.seeds ? xld32(P.seeds + ic) : P.seed;
+	};
+	// the 16-byte chunk holding point p's last < 16 bytes (unconditional:
+	// clamped into the extent; unused when p is 16-byte aligned)
+	auto chunk_of = [&](uint64_t p) -> u32x4 {
+		const uint64_t a = G.S + p - (p & 15u);
+		return ld16(reinterpret_cast<const uint8_t*>(a <= last_chunk ? a : last_chunk));
+	};
+	// R(p): the prefix register at point p (0 at p = 0).  p = 4096k + 64 cnt
+	// + 16 cq + r: G(p) back to p64, on by 16 cq bytes plus Y (the span's
+	// register after its first cq chunks), then the r < 16 bytes of the
+	// chunk at p - r.
+	auto R = [&](uint64_t p, uint32_t g, uint32_t y, const u32x4& ch) -> uint32_t {
+		const uint32_t k = x_blk(p);
+		const uint32_t cnt = x_cnt(p, k);
+		const uint32_t rem = (uint32_t)(p - 4096ull * k) & 63u;  // (cnt = 64: rem 0)
+		const uint32_t cq = rem >> 4, r16 = rem & 15u;
+		uint32_t r = lmul(lds, kFinXinv + 128 * (64 - cnt), g);
+		r = cq ? lmul(lds, kFinPow1 + 128 * (16 * cq), r) ^ y : r;
+		r = p ? r : 0u;
+		if (r16) {
+#pragma unroll
+			for (uint32_t t = 0; t < 3; ++t) {
+				if (4 * t + 4 <= r16) {
+					r ^= ch[t];
+					r = s4[r & 255u] ^ s4[256 + ((r >> 8) & 255u)] ^ s4[512 + ((r >> 16) & 255u)] ^ s4[768 + (r >> 24)];
+				}
+			}
+			const uint32_t wd = r16 >> 2, nb = r16 & 3u;
+			const uint32_t word = wd == 0 ? ch[0] : wd == 1 ? ch[1] : wd == 2 ? ch[2] : ch[3];
+			for (uint32_t b = 0; b < nb; ++b) r = (r >> 8) ^ s4[768 + ((r ^ (word >> (8 * b))) & 255u)];
+		}
+		return r;
+	};
+	auto finish = [&](const In& I) -> uint32_t {
+		const uint64_t sp = I.P0 - G.S, ep = I.P1 - G.S;
 		const uint32_t ks = x_blk(sp), ke = x_blk(ep);
-		// G(p): the range-local prefix at p64, positioned at its block's end
-		const uint32_t gs = cs[0];
-		uint32_t ge = ce[0];
-		// A buffer spanning ranges ws < we: the end point takes the aggregates of
-		// the ranges from ws to we - 1 (the start point's range start is the origin)
-		const uint64_t ws = ks / per, we = ke / per;
+		// G(p): the unit-local prefix at p64, positioned at its block's end
+		uint32_t ge = I.ce[0];
+		// A buffer spanning units ws < we: the end point takes the aggregates of
+		// the units from ws to we - 1 (the start point's unit start is the origin)
+		const uint64_t ws = lgp < 64 ? ks >> lgp : ks / per, we = lgp < 64 ? ke >> lgp : ke / per;
 		if (ws != we) {
 			uint32_t D = 0;
 			for (uint64_t v = ws; v < we; v += 8) {  // eight aggregates in flight per round trip
@@ -848,41 +927,10 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 			const uint32_t j = (uint32_t)(ke - we * per + 1);
 			ge ^= j < 64 ? lmul(lds, kFinBp0 + 128 * j, D) : xmul_blocks(T, D, j);
 		}
-		// R(p): the prefix register at point p (0 at p = 0).  p = 4096k + 64 cnt
-		// + 16 cq + r: G(p) back to p64, on by 16 cq bytes plus Y (the span's
-		// register after its first cq chunks), then the r < 16 bytes of the
-		// chunk at p - r (one 16-byte load).
-		auto R = [&](uint64_t p, uint32_t g, uint32_t y) -> uint32_t {
-			const uint32_t k = x_blk(p);
-			const uint32_t cnt = x_cnt(p, k);
-			const uint32_t rem = (uint32_t)(p - 4096ull * k) & 63u;  // (cnt = 64: rem 0)
-			const uint32_t cq = rem >> 4, r16 = rem & 15u;
-			uint32_t r = lmul(lds, kFinXinv + 128 * (64 - cnt), g);
-			r = cq ? lmul(lds, kFinPow1 + 128 * (16 * cq), r) ^ y : r;
-			r = p ? r : 0u;
-#ifdef FDBX_NOREM
-			if (false) {
-#else
-			if (r16) {
-#endif
-				const u32x4 ch = ld16(reinterpret_cast<const uint8_t*>(G.S + p - r16));
-#pragma unroll
-				for (uint32_t t = 0; t < 3; ++t) {
-					if (4 * t + 4 <= r16) {
-						r ^= ch[t];
-						r = s4[r & 255u] ^ s4[256 + ((r >> 8) & 255u)] ^ s4[512 + ((r >> 16) & 255u)] ^ s4[768 + (r >> 24)];
-					}
-				}
-				const uint32_t wd = r16 >> 2, nb = r16 & 3u;
-				const uint32_t word = wd == 0 ? ch[0] : wd == 1 ? ch[1] : wd == 2 ? ch[2] : ch[3];
-				for (uint32_t b = 0; b < nb; ++b) r = (r >> 8) ^ s4[768 + ((r ^ (word >> (8 * b))) & 255u)];
-			}
-			return r;
-		};
-		const uint32_t re = R(ep, ge, ce[1]);
-		uint32_t rs = R(sp, gs, cs[1]) ^ ~sd;
+		const uint32_t re = R(ep, ge, I.ce[1], I.che);
+		uint32_t rs = R(sp, I.cs[0], I.cs[1], I.chs) ^ ~I.sd;
 		// rs * x^(8 len), len = 4096a + 64c + d
-		const uint64_t len = P1 - P0;
+		const uint64_t len = I.P1 - I.P0;
 		rs = lmul(lds, kFinPow1 + 128 * (uint32_t)(len & 63u), rs);
 		rs = lmul(lds, kFinPow64 + 128 * (uint32_t)((len >> 6) & 63u), rs);
 		const uint64_t nbk = len >> 12;
@@ -890,7 +938,21 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 			rs = xmul_blocks(T, rs, (uint32_t)nbk);
 		else if (nbk)
 			rs = lmul(lds, kFinBp0 + 128 * (uint32_t)nbk, rs);
-		if (ok) P.out[i] = ~(re ^ rs);
+		return ~(re ^ rs);
+	};
+	const uint64_t span = (uint64_t)gridDim.x * blockDim.x;
+	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += 2 * span) {
+		In A, B;
+		load_in(A, i0 + threadIdx.x);
+		load_in(B, i0 + span + threadIdx.x);
+		A.chs = chunk_of(A.P0 - G.S);
+		A.che = chunk_of(A.P1 - G.S);
+		B.chs = chunk_of(B.P0 - G.S);
+		B.che = chunk_of(B.P1 - G.S);
+		const uint32_t ra = finish(A);
+		const uint32_t rb = finish(B);
+		if (A.ok) P.out[i0 + threadIdx.x] = ra;
+		if (B.ok) P.out[i0 + span + threadIdx.x] = rb;
 	}
 }
 
@@ -943,7 +1005,7 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 			k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
 	} else {
 		// persistent, but no more workgroups than the buffers fill (each fills 133 KiB of LDS)
-		const uint64_t g = (count + kFinThreads - 1) / kFinThreads;
+		const uint64_t g = (count + 2 * kFinThreads - 1) / (2 * kFinThreads);  // (two buffers per thread per pass)
 		k_xfin<<<(unsigned)(g < (uint64_t)num_cus ? g : (uint64_t)num_cus), kFinThreads, 0, stream>>>(P);
 	}
 	return 0;

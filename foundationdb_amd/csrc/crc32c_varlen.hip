@@ -469,7 +469,8 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 			const uint64_t S = (reinterpret_cast<uint64_t>(P.base) + o0) & ~uint64_t(15);
 			const uint64_t E = (reinterpret_cast<uint64_t>(P.base) + o1 + l1 + 15) & ~uint64_t(15);
 			const uint64_t nblk = E > S ? (E - S + 4095) >> 12 : 0;
-			const uint64_t gsz = x_gsz(nblk, P.xcapg), ngrab = (nblk + gsz - 1) / gsz, tg = 4096 * gsz;
+			const uint64_t gsz = x_gsz(nblk, P.xcapg), ngrab = (nblk + gsz - 1) / gsz;
+			const uint32_t lt = 12 + x_log2(gsz);  // bytes per grab: 2^lt
 			const uint64_t Pe = reinterpret_cast<uint64_t>(P.base) + off + len;
 			uint64_t pe = 0;
 			if (i) {
@@ -479,8 +480,8 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 			}
 			if (nblk && E - S < kXMaxExtent && Pe >= S && (i == 0 || (pe >= S && pe <= Pe))) {
 				const uint64_t ep = i ? pe - S : 0, ei = Pe - S;
-				const uint64_t glo = (ep + tg - 1) / tg;
-				uint64_t ghi = (ei + tg - 1) / tg;
+				const uint64_t glo = (ep + (1ull << lt) - 1) >> lt;
+				uint64_t ghi = (ei + (1ull << lt) - 1) >> lt;
 				if (i + 1 == P.count) ghi = ngrab;
 				for (uint64_t g = glo; g < ghi && g < ngrab; ++g) P.xwq[g] = (uint32_t)i;
 			}
@@ -1182,7 +1183,7 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	if (route == kRouteBlocks && P.bigmin == 0) route = kRouteWindows;
 	P.hstat = hstat;
 	P.err = err;
-	const bool extent = route == kRouteExtent && xs != nullptr;
+	const bool extent = route == kRouteExtent && xs != nullptr && count < (1ull << 31);  // (point ids 2i + end: 32 bits)
 	if (route == kRouteExtent) route = kRouteWindows;  // the fallback: windows
 	if (extent) {
 		P.xhdr = xs->xhdr;
