@@ -456,10 +456,22 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	// the queue with ds_permute: the window lanes with a point go to the next
 	// free slots in lane order, the others to the remaining lanes (a bijection,
 	// so every destination is written once).
+	// A second bank holds the previous 64 (a full bank moves there; a store
+	// only when both are full): one store per ~128 points.
 	uint32_t qid = 0, qv = 0, qy = 0, qn = 0;
-	auto store_queue = [&]() {
+	uint32_t bid = 0, bv = 0, by = 0;
+	bool bfull = false;
+	auto store_bank = [&](uint32_t id, uint32_t v, uint32_t y, uint32_t n) {
 		typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-		if (lane < qn) *reinterpret_cast<u32x2*>((qid & 1 ? P.x.pe : P.x.ps) + 2ull * (qid >> 1)) = u32x2{qv, qy};
+		if (lane < n) *reinterpret_cast<u32x2*>((id & 1 ? P.x.pe : P.x.ps) + 2ull * (id >> 1)) = u32x2{v, y};
+	};
+	auto store_queue = [&]() {  // bank A is full (or the wave is done)
+		if (bfull) store_bank(bid, bv, by, 64);
+		bid = qid;
+		bv = qv;
+		by = qy;
+		bfull = qn == 64;
+		if (!bfull) store_bank(qid, qv, qy, qn);
 		qn = 0;
 	};
 	auto push = [&](bool on, uint32_t pid, uint32_t v, uint32_t y) {
@@ -484,6 +496,15 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 #endif
 		const bool ok = q0 + lane < cnt32;
 		const bool os = ok && wbs >= kb0 && wbs < kb1, oe = ok && wbe >= kb0 && wbe < kb1;
+#ifdef FDBX_DIRECT
+		{
+			typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+			uint32_t* const dmy = P.x.dummy + 128 * (blockIdx.x * wpb + wi);
+			*reinterpret_cast<u32x2*>(os ? P.x.ps + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Vs, Ys};
+			*reinterpret_cast<u32x2*>(oe ? P.x.pe + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Ve, Ye};
+			return;
+		}
+#endif
 		if (qn + (uint32_t)__builtin_popcountll(__ballot(os)) > 64) store_queue();
 		push(os, 2 * (q0 + lane), Vs, Ys);
 		if (qn + (uint32_t)__builtin_popcountll(__ballot(oe)) > 64) store_queue();
@@ -551,13 +572,16 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			Ye = he ? y : Ye;
 		}
 	};
-	// blocks k .. k + 3 of grab [gb0, gb1) (those before kend): the prefix
-	// chain, the points, windows retired inside the grab
-	auto finish = [&](const uint32_t (&H)[2 * kXU], const uint32_t (&Y)[2 * kXU][3], uint32_t k, uint32_t kend,
-	                  uint32_t gb0, uint32_t gb1) {
-		uint32_t Z[2 * kXU];
+	// the unit of blocks k, k + 1 of grab [gb0, gb1) (those before kend): the
+	// prefix chain, the points, windows retired inside the grab.  Per unit, so
+	// only one unit's H and Y are live: a window retired here can only hold
+	// points in this unit's blocks or later (its buffers start after the
+	// previous window's last end, which lies in this unit or later).
+	auto finish = [&](const uint32_t (&H)[kXU], const uint32_t (&Y)[kXU][3], uint32_t k, uint32_t kend, uint32_t gb0,
+	                  uint32_t gb1) {
+		uint32_t Z[kXU];
 #pragma unroll
-		for (uint32_t j = 0; j < 2 * kXU; ++j) {
+		for (uint32_t j = 0; j < kXU; ++j) {
 #ifdef FDBX_NOMUL
 			Z[j] = X;
 #else
@@ -565,20 +589,16 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 #endif
 			if (k + j < kend) X = Z[j] ^ rdlane(H[j], 63);
 		}
-#ifdef FDBX_NOCAP
-		if (X == 0x12345678u) Vs ^= H[0] ^ H[1] ^ H[2] ^ H[3] ^ Y[0][0] ^ Y[1][1] ^ Y[2][2] ^ Y[3][0];
-		return;
-#endif
 #pragma unroll
-		for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
-		const uint32_t kn = k + 2 * kXU < kend ? k + 2 * kXU : kend;
+		for (uint32_t j = 0; j < kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
+		const uint32_t kn = k + kXU < kend ? k + kXU : kend;
 		while (wlast < kn) {  // every buffer of the window ends in the blocks so far: the next 64
 			flush(q, gb0, gb1);
 			q += 64;
 			make_window(q);
 			prefetch(q + 64);
 #pragma unroll
-			for (uint32_t j = 0; j < 2 * kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
+			for (uint32_t j = 0; j < kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
 		}
 	};
 
@@ -593,9 +613,9 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		prefetch(q + 64);
 		X = 0;
 		for (uint32_t s = 0; s < spg && gb0 + 4 * s < nblk; ++s) {
-			uint32_t H[2 * kXU], Y[2 * kXU][3];
 #pragma unroll
 			for (uint32_t h = 0; h < 2; ++h) {
+				uint32_t H[kXU], Y[kXU][3];
 #pragma unroll
 				for (uint32_t j = 0; j < kXU; ++j) {
 					const uint64_t a = G.S + 4096ull * (gb0 + 4 * s + 2 * h + j) + c.ld_off;
@@ -605,9 +625,9 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 						u1[j].r[q2] = ld16(reinterpret_cast<const uint8_t*>(o <= last_chunk ? o : last_chunk));
 					}
 				}
-				unit_h(u1, reinterpret_cast<uint32_t(&)[kXU]>(H[2 * h]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[2 * h]));
+				unit_h(u1, H, Y);
+				finish(H, Y, gb0 + 4 * s + 2 * h, gb1, gb0, gb1);
 			}
-			finish(H, Y, gb0 + 4 * s, gb1, gb0, gb1);
 		}
 		flush(q, gb0, gb1);
 		if (lane == 0) P.x.gagg[nd] = X;
@@ -624,7 +644,7 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	while (gA < nd) {
 		const uint32_t gb0 = gA * gsz, gb1 = gb0 + gsz;
 		const uint32_t k = gb0 + 4 * s;
-		uint32_t H[2 * kXU], Y[2 * kXU][3];
+		uint32_t qnx = 0;
 		if (s == 0) {  // the grab's window (its metadata was prefetched a grab ahead)
 			make_window(q);
 			prefetch(q + 64);
@@ -632,20 +652,31 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		}
 		load_step_unit(u1, gA, s, 1);
 		__builtin_amdgcn_sched_barrier(0);
-		unit_h(u0, reinterpret_cast<uint32_t(&)[kXU]>(H[0]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[0]));
-		__builtin_amdgcn_sched_barrier(0);
+		{
+			uint32_t H[kXU], Y[kXU][3];
+			unit_h(u0, H, Y);
+			__builtin_amdgcn_sched_barrier(0);
+			const bool last_step = s + 1 == spg;
+			uint32_t qnx0 = 0;
+			if (last_step && gB < nd) qnx0 = wq_of(gB);  // (ahead of the next unit's loads)
+			qnx = qnx0;
+			// the next unit's loads go out before this unit's points are captured
+			load_step_unit(u0, last_step ? gB : gA, last_step ? 0u : s + 1, 0);
+			__builtin_amdgcn_sched_barrier(0);
+			finish(H, Y, k, gb1, gb0, gb1);
+		}
 		const bool last_step = s + 1 == spg;
-		uint32_t qn = 0;
-		if (last_step && gB < nd) qn = wq_of(gB);  // (scalar load, ahead of the next unit's loads)
-		load_step_unit(u0, last_step ? gB : gA, last_step ? 0u : s + 1, 0);
 		__builtin_amdgcn_sched_barrier(0);
-		unit_h(u1, reinterpret_cast<uint32_t(&)[kXU]>(H[kXU]), reinterpret_cast<uint32_t(&)[kXU][3]>(Y[kXU]));
-		__builtin_amdgcn_sched_barrier(0);
-		finish(H, Y, k, gb1, gb0, gb1);
+		{
+			uint32_t H[kXU], Y[kXU][3];
+			unit_h(u1, H, Y);
+			__builtin_amdgcn_sched_barrier(0);
+			finish(H, Y, k + kXU, gb1, gb0, gb1);
+		}
 		if (last_step) {
 			flush(q, gb0, gb1);
 			if (lane == 0) P.x.gagg[gA] = X;
-			q = qn;
+			q = qnx;
 			if (gB < nd) prefetch(q);  // the next grab's window, consumed a step later
 			gA = gB;
 			gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
@@ -655,7 +686,8 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			++s;
 		}
 	}
-	store_queue();
+	if (bfull) store_bank(bid, bv, by, 64);
+	store_bank(qid, qv, qy, qn);
 	// every request of every wave has returned: the counter goes back to zero
 	__builtin_amdgcn_s_waitcnt(0);
 	__syncthreads();
@@ -855,16 +887,13 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	typedef __attribute__((address_space(1))) const u32x2 xg_u2;
 	// Two buffers per thread per pass, their loads issued together: the pass
 	// is a chain of dependent round trips (metadata and point values, then the
-	// points' chunks), so two in flight halve the passes (1 Mi packets:
-	// 1.5 -> 0.8 passes of one 1024-thread workgroup per CU).
+	// points' chunks), so two in flight halve the passes (zipf: 17.9 -> 16.7 us).
 	struct In {
 		u32x2 cs, ce;
 		uint64_t P0, P1;
 		uint32_t sd;
 		bool ok;
-		u32x4 chs, che;
 	};
-	const uint64_t last_chunk = G.Eend - 16;
 	auto load_in = [&](In& I, uint64_t i) {
 		I.ok = i < P.count;
 		const uint64_t ic = I.ok ? i : P.count - 1;
@@ -874,17 +903,11 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		x_buffer(P, ic, I.P0, I.P1);
 		I.sd = P.seeds ? xld32(P.seeds + ic) : P.seed;
 	};
-	// the 16-byte chunk holding point p's last < 16 bytes (unconditional:
-	// clamped into the extent; unused when p is 16-byte aligned)
-	auto chunk_of = [&](uint64_t p) -> u32x4 {
-		const uint64_t a = G.S + p - (p & 15u);
-		return ld16(reinterpret_cast<const uint8_t*>(a <= last_chunk ? a : last_chunk));
-	};
 	// R(p): the prefix register at point p (0 at p = 0).  p = 4096k + 64 cnt
 	// + 16 cq + r: G(p) back to p64, on by 16 cq bytes plus Y (the span's
 	// register after its first cq chunks), then the r < 16 bytes of the
 	// chunk at p - r.
-	auto R = [&](uint64_t p, uint32_t g, uint32_t y, const u32x4& ch) -> uint32_t {
+	auto R = [&](uint64_t p, uint32_t g, uint32_t y) -> uint32_t {
 		const uint32_t k = x_blk(p);
 		const uint32_t cnt = x_cnt(p, k);
 		const uint32_t rem = (uint32_t)(p - 4096ull * k) & 63u;  // (cnt = 64: rem 0)
@@ -892,7 +915,8 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		uint32_t r = lmul(lds, kFinXinv + 128 * (64 - cnt), g);
 		r = cq ? lmul(lds, kFinPow1 + 128 * (16 * cq), r) ^ y : r;
 		r = p ? r : 0u;
-		if (r16) {
+		if (r16) {  // (a divergent load: unconditional chunk loads for every point cost ~10 us on zipf)
+			const u32x4 ch = ld16(reinterpret_cast<const uint8_t*>(G.S + p - r16));
 #pragma unroll
 			for (uint32_t t = 0; t < 3; ++t) {
 				if (4 * t + 4 <= r16) {
@@ -927,8 +951,8 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 			const uint32_t j = (uint32_t)(ke - we * per + 1);
 			ge ^= j < 64 ? lmul(lds, kFinBp0 + 128 * j, D) : xmul_blocks(T, D, j);
 		}
-		const uint32_t re = R(ep, ge, I.ce[1], I.che);
-		uint32_t rs = R(sp, I.cs[0], I.cs[1], I.chs) ^ ~I.sd;
+		const uint32_t re = R(ep, ge, I.ce[1]);
+		uint32_t rs = R(sp, I.cs[0], I.cs[1]) ^ ~I.sd;
 		// rs * x^(8 len), len = 4096a + 64c + d
 		const uint64_t len = I.P1 - I.P0;
 		rs = lmul(lds, kFinPow1 + 128 * (uint32_t)(len & 63u), rs);
@@ -941,14 +965,19 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		return ~(re ^ rs);
 	};
 	const uint64_t span = (uint64_t)gridDim.x * blockDim.x;
+#ifdef FDBX_FIN1
+	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += span) {
+		In A;
+		load_in(A, i0 + threadIdx.x);
+		const uint32_t ra = finish(A);
+		if (A.ok) P.out[i0 + threadIdx.x] = ra;
+	}
+	return;
+#endif
 	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += 2 * span) {
 		In A, B;
 		load_in(A, i0 + threadIdx.x);
 		load_in(B, i0 + span + threadIdx.x);
-		A.chs = chunk_of(A.P0 - G.S);
-		A.che = chunk_of(A.P1 - G.S);
-		B.chs = chunk_of(B.P0 - G.S);
-		B.che = chunk_of(B.P1 - G.S);
 		const uint32_t ra = finish(A);
 		const uint32_t rb = finish(B);
 		if (A.ok) P.out[i0 + threadIdx.x] = ra;
@@ -1005,7 +1034,11 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 			k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
 	} else {
 		// persistent, but no more workgroups than the buffers fill (each fills 133 KiB of LDS)
+#ifdef FDBX_FIN1
+		const uint64_t g = (count + kFinThreads - 1) / kFinThreads;
+#else
 		const uint64_t g = (count + 2 * kFinThreads - 1) / (2 * kFinThreads);  // (two buffers per thread per pass)
+#endif
 		k_xfin<<<(unsigned)(g < (uint64_t)num_cus ? g : (uint64_t)num_cus), kFinThreads, 0, stream>>>(P);
 	}
 	return 0;
