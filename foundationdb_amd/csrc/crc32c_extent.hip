@@ -870,9 +870,12 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 #ifndef FDBX_NOFILL
 	fin_fill(lds, T);
 #endif
-	// nibble tables of C = M^per (the range stride), for the straddling
-	// buffers' aggregate chains: entry [n][v] = (v x^4n) * C, bit by bit
-	if (threadIdx.x < 128) {
+	// nibble tables of C = M^per (the unit stride), for the straddling
+	// buffers' aggregate chains: entry [n][v] = (v x^4n) * C, bit by bit --
+	// except for grabs of fewer than 64 blocks, whose M^gsz is one of the
+	// block-power tables already copied (no build, no barrier wait on it)
+	const uint32_t cbase = per < 64 ? kFinBp0 + 128 * (uint32_t)per : kFinC;
+	if (per >= 64 && threadIdx.x < 128) {
 		const uint32_t C = xmul_blocks(T, 0x80000000u, (uint32_t)per);
 		uint32_t a = (threadIdx.x & 15u) << (4 * (threadIdx.x >> 4)), b = C, r = 0;
 		for (int q = 0; q < 32; ++q) {
@@ -946,7 +949,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 				for (uint32_t t = 0; t < 8; ++t) a[t] = xld32(agg + (v + t < we ? v + t : we - 1));
 #pragma unroll
 				for (uint32_t t = 0; t < 8; ++t)
-					if (v + t < we) D = lmul(lds, kFinC, D) ^ a[t];
+					if (v + t < we) D = lmul(lds, cbase, D) ^ a[t];
 			}
 			const uint32_t j = (uint32_t)(ke - we * per + 1);
 			ge ^= j < 64 ? lmul(lds, kFinBp0 + 128 * j, D) : xmul_blocks(T, D, j);

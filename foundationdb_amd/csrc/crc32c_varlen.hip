@@ -505,6 +505,53 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 	}
 }
 
+// The extent route's only planning pass (crc32c_extent.hip): the packing and
+// extent checks (epoch-tagged flags), the stream's route statistics (tile 0)
+// and k_xgrab's grab map, from one coalesced load of each buffer's offset and
+// length (the next buffer's come from the neighbouring lane).  Buffer i + 1 is
+// the first to end past the start T(g) of the grabs with end(i) <= T(g) <
+// end(i + 1); buffer 0 covers the grabs before its end, the last buffer's
+// index + 1 (= count) the grabs after it.
+__global__ __launch_bounds__(256) void k_xcount(V7Params P) {
+	__shared__ uint64_t s_stat[4][4];
+	const uint64_t i = (uint64_t)blockIdx.x * kTileW + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63;
+	const bool in = i < P.count;
+	uint64_t off = 0, len = 0;
+	if (in) v7_buffer(P, i, off, len);
+	uint64_t on = __shfl_down(off, 1), ln = __shfl_down(len, 1);
+	if (lane == 63 && i + 1 < P.count) v7_buffer(P, i + 1, on, ln);
+	const bool has_next = i + 1 < P.count;
+	const uint64_t e = off + len;
+	const bool bad = in && has_next && !(on >= e && on - e < 4096 && on - e <= (len > 256 ? len : 256));
+	if (__ballot(bad) && lane == 0) P.xhdr[0] = P.epoch;
+	uint64_t o0, l0, o1, l1;
+	v7_buffer(P, 0, o0, l0);
+	v7_buffer(P, P.count - 1, o1, l1);
+	const uint64_t S = (reinterpret_cast<uint64_t>(P.base) + o0) & ~uint64_t(15);
+	const uint64_t E = (reinterpret_cast<uint64_t>(P.base) + o1 + l1 + 15) & ~uint64_t(15);
+	// (an unordered batch may give E < S: the packing check refuses it anyway)
+	const uint64_t nblk = E > S ? (E - S + 4095) >> 12 : 0;
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		if (E - S >= kXMaxExtent) P.xhdr[1] = P.epoch;
+		if (P.hstat) P.hstat[kHstatNblk] = nblk;
+	}
+	if (blockIdx.x == 0 && P.hstat) v7_route_stats(P, i, off, len, s_stat);
+	if (P.xwq && in && nblk && E - S < kXMaxExtent && !bad) {
+		const uint64_t gsz = x_gsz(nblk, P.xcapg), ngrab = (nblk + gsz - 1) / gsz;
+		const uint32_t lt = 12 + x_log2(gsz);  // bytes per grab: 2^lt
+		const uint64_t base = reinterpret_cast<uint64_t>(P.base);
+		const uint64_t ei = base + e - S;  // (>= 0 for an ordered pair)
+		auto ceil_g = [&](uint64_t p) { return (p + (1ull << lt) - 1) >> lt; };
+		if (i == 0)
+			for (uint64_t g = 0; g < ceil_g(ei) && g < ngrab; ++g) P.xwq[g] = 0;
+		const uint64_t glo = ceil_g(ei);
+		const uint64_t ghi = has_next ? ceil_g(base + on + ln - S) : ngrab;
+		const uint32_t v = has_next ? (uint32_t)(i + 1) : (uint32_t)P.count;
+		for (uint64_t g = glo; g < ghi && g < ngrab; ++g) P.xwq[g] = v;
+	}
+}
+
 // BIG: the block route is on (bigmin != 0); without it the route's sums
 // and entries are compiled out (fewer registers: 8 blocks per CU).
 template <bool BIG>
@@ -1217,14 +1264,15 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 	// kScanTiles tiles one scan block is cheaper)
 	P.scanned = ntile > kScanTiles;
 	P.selfsum = ntile <= kSelfSumTiles;
-	if (!P.selfsum || extent) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);  // (extent: the packing check)
 	if (extent) {
+		k_xcount<<<(unsigned)ntile, 256, 0, stream>>>(P);  // the packing check and the grab map
 		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
 		              0);
 		launch_extent(base, offsets, lengths, stride, length, count, seed, seeds, out, tabs, num_cus, *xs, hstat, stream,
 		              1);
 		return 0;
 	}
+	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.scanned)
 		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4, P.bigmin ? P.bsum : nullptr,
 		                               P.bigmin ? P.nsum : nullptr);
