@@ -81,6 +81,13 @@ def shape(name):
     return lengths, offsets, extent
 
 
+def xxh3_seeds(n):
+    """Per-buffer seeds of the seeded exact-batch XXH3 digests (Redwood's
+    XXH3_64bits_withSeed call sites, fdbserver/kvstore/IPager.h:325-361)."""
+    i = np.arange(n, dtype=np.uint64)
+    return (i * np.uint64(0x9E3779B97F4A7C15)) ^ np.uint64(0xFDBEEFDB)
+
+
 def digest(crcs):
     crcs = np.asarray(crcs, dtype=np.uint32)
     return {"xor": int(np.bitwise_xor.reduce(crcs)) if crcs.size else 0, "sum": int(crcs.astype(np.uint64).sum())}

@@ -600,6 +600,21 @@ __device__ __forceinline__ uint64_t rdfirst64v(uint64_t v) {
 	return ((uint64_t)hi << 32) | lo;
 }
 
+// lanes below this one with their bit set in m
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t permute64(int addr, uint64_t v) {
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)(uint32_t)v);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)(uint32_t)(v >> 32));
+	return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t bpermute64(int addr, uint64_t v) {
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)v);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(v >> 32));
+	return ((uint64_t)hi << 32) | lo;
+}
+
 struct VStep {
 	uint64_t v[4][2];
 	uint64_t len, buf, seed;  // this row's buffer
@@ -631,35 +646,54 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 
 	// ---- long buffers: rows
 	const uint64_t dummy = reinterpret_cast<uint64_t>(P.wave_first);
-	// Two pool banks: picks come from A; B is refilled only at the top of a
-	// half-iteration, so a pick never waits for a load.
-	uint64_t am = 0, bm = 0, ab = 0, bb = 0, pnext = begin;
+	// Two pool banks.  B holds the next 64 buffers as loaded; its loads are
+	// issued a pool ahead and read only when A runs dry, so the wait finds
+	// them long complete.  A holds the row buffers of a taken pool COMPACTED
+	// (ds_permute) into lanes 0 .. na-1, handed out in order from the cursor
+	// ac: the rows that need a buffer pull theirs with ds_bpermute, all rows
+	// at once (a serial pick per row cost ~40 instructions a buffer, the
+	// bound for buffers of a block or two).
+	uint64_t ab = 0, bb = 0, pnext = begin;
 	uint64_t alen = 0, aoff = 0, aseed = 0, blen = 0, boff = 0, bseed = 0;
-	auto fill_b = [&]() __attribute__((always_inline)) {
-		while (bm == 0 && pnext < end) {
-			bb = rdfirst64v(pnext);  // keep the pool cursor in SGPRs
-			pnext = bb + 64;
-			const uint64_t i = bb + lane;
-			const bool in = i < end;
-			blen = in ? lengths[i] : 0;
-			boff = in ? offsets[i] : 0;
-			if (SEEDS) bseed = in ? seeds[i] : 0;
-			const bool sp = lflag && in && blen > kXSplitMin && lflag[i];
-			bm = __ballot(blen > 240 && !sp);
+	uint32_t aj = 0, bfl = 0, na = 0, ac = 0;
+	bool bpend = false;  // B loaded, not yet taken (uniform)
+	auto issue_b = [&]() __attribute__((always_inline)) {
+		bb = rdfirst64v(pnext);  // keep the pool cursor in SGPRs
+		pnext = bb + 64;
+		const uint64_t i = bb + lane;
+		const bool in = i < end;
+		blen = in ? lengths[i] : 0;
+		boff = in ? offsets[i] : 0;
+		if (SEEDS) bseed = in ? seeds[i] : 0;
+		bfl = (lflag && in) ? lflag[i] : 0;
+		bpend = true;
+	};
+	// A <- B, compacted (A exhausted); false when the wave's range has no row buffer left
+	auto take_b = [&]() __attribute__((always_inline)) -> bool {
+		for (;;) {
+			if (!bpend) {
+				if (pnext >= end) return false;
+				issue_b();
+			}
+			bpend = false;
+			const bool on = blen > 240 && !(blen > kXSplitMin && bfl);
+			const uint64_t m = __ballot(on);
+			const uint32_t n = (uint32_t)__builtin_popcountll(m);
+			if (n == 0) continue;
+			const uint32_t below = mbcnt64(m);
+			const int d = (int)(((on ? below : n + (uint32_t)lane - below) & 63u) << 2);
+			alen = permute64(d, blen);
+			aoff = permute64(d, boff);
+			if (SEEDS) aseed = permute64(d, bseed);
+			aj = (uint32_t)__builtin_amdgcn_ds_permute(d, (int)(uint32_t)(bb - begin + (uint64_t)lane));
+			na = n;
+			ac = 0;
+			return true;
 		}
-		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): bank B complete
 	};
 	auto refill = [&]() __attribute__((always_inline)) {
-		if (am == 0) {
-			if (bm == 0) fill_b();
-			am = bm;
-			ab = bb;
-			alen = blen;
-			aoff = boff;
-			aseed = bseed;
-			bm = 0;
-		}
-		if (bm == 0 && pnext < end) fill_b();
+		if (ac == na && bpend) take_b();
+		if (!bpend && pnext < end) issue_b();
 	};
 	// load cursor of this lane's row (row-uniform)
 	uint64_t lp = dummy, llen = 1024, lbuf = 0, lseed = seed0;
@@ -667,31 +701,32 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 	bool lact = false;
 
 	auto grab = [&]() __attribute__((always_inline)) {
-		uint64_t need = __ballot(l == 0 && lblk == lnblk);
-		while (need != 0) {
-			const int rr = __builtin_ctzll(need) >> 4;
-			need &= need - 1;
-			if (am == 0) {
-				if (bm == 0) break;  // nothing loaded: idle until the next refill
-				am = bm;
-				ab = bb;
-				alen = blen;
-				aoff = boff;
-				aseed = bseed;
-				bm = 0;
-			}
-			const int j = __builtin_ctzll(am);
-			am &= am - 1;
-			const uint64_t len = rdlane64(alen, j), off = rdlane64(aoff, j);
-			const uint64_t sd = SEEDS ? rdlane64(aseed, j) : seed0;
-			if (r == rr) {
-				llen = len;
-				lp = base + off;
-				lblk = 0;
-				lnblk = (uint32_t)((len - 1) >> 10) + 1;
-				lbuf = ab + j;
-				lseed = sd;
-				lact = true;
+		const uint64_t need = __ballot(l == 0 && lblk == lnblk);
+		if (need != 0) {
+			const bool mine = lblk == lnblk;
+			// this row's rank among the rows that need one
+			const uint32_t rk = mbcnt64(need) - (mine && l != 0 ? 1u : 0u);
+			const uint32_t nn = (uint32_t)__builtin_popcountll(need);
+			uint32_t got = 0;
+			while (got < nn) {
+				if (ac == na && !take_b()) break;
+				const uint32_t t = min(nn - got, na - ac);
+				const bool pick = mine && rk - got < t;  // unsigned: rk in [got, got + t)
+				const int src = (int)((ac + rk - got) & 63u) << 2;
+				const uint64_t len = bpermute64(src, alen), off = bpermute64(src, aoff);
+				const uint64_t sd = SEEDS ? bpermute64(src, aseed) : seed0;
+				const uint32_t j = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)aj);
+				if (pick) {
+					llen = len;
+					lp = base + off;
+					lblk = 0;
+					lnblk = (uint32_t)((len - 1) >> 10) + 1;
+					lbuf = begin + j;
+					lseed = sd;
+					lact = true;
+				}
+				ac += t;
+				got += t;
 			}
 		}
 		if (lblk == lnblk) {  // no buffer for this row: read the dummy KiB
@@ -725,18 +760,15 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 		++lblk;
 	};
 
-	// Results collect in lanes (rx = hash, ri = buffer index, rn used) and
-	// leave together: a store's source registers may not be rewritten until it
-	// has completed, and in-order vmcnt would make that a wait for every load in
-	// flight, so stores happen once per 56+ buffers rather than per buffer.
-	uint64_t rx = 0, ri = 0;
-	uint32_t rn = 0;
+	// Results collect in lanes (rx = hash, rj = buffer - begin, rn used; the
+	// finishing rows' values move in with ds_permute) and leave 64 at a time:
+	// a store in the loop holds up every later wait on the loads issued
+	// behind it (in-order vmcnt).
+	uint64_t rx = 0;
+	uint32_t rj = 0, rn = 0;
 	auto flush = [&]() __attribute__((always_inline)) {
-		if ((uint32_t)lane < rn) out[ri] = rx;
+		if ((uint32_t)lane < rn) out[begin + rj] = rx;
 		rn = 0;
-		// wait here, on the rare flush path, so that no later register write
-		// has to wait for the store on the common path
-		__builtin_amdgcn_s_waitcnt(0x0F70);
 	};
 	RowKeys K = row_keys(lane, seed0);
 	uint64_t a0 = 0, a1 = 0;
@@ -782,15 +814,19 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 			a0 = ((a0 ^ (a0 >> 47)) ^ K.c0) * P32_1;
 			a1 = ((a1 ^ (a1 >> 47)) ^ K.c1) * P32_1;
 		}
-		while (done != 0) {
-			const int src = __builtin_ctzll(done);
-			done &= done - 1;
-			const uint64_t hv = rdlane64(h, src), iv = rdlane64(S.buf, src);
-			rx = (uint32_t)lane == rn ? hv : rx;
-			ri = (uint32_t)lane == rn ? iv : ri;
-			++rn;
+		if (done != 0) {
+			const uint32_t n = (uint32_t)__builtin_popcountll(done);
+			if (rn + n > 64) flush();
+			const bool on = l == 0 && fin && S.act;
+			const uint32_t below = mbcnt64(done);
+			const int d = (int)(((on ? rn + below : rn + n + (uint32_t)lane - below) & 63u) << 2);
+			const uint64_t rh = permute64(d, h);
+			const uint32_t rr = (uint32_t)__builtin_amdgcn_ds_permute(d, (int)(uint32_t)(S.buf - begin));
+			const bool in = (uint32_t)lane - rn < n;
+			rx = in ? rh : rx;
+			rj = in ? rr : rj;
+			rn += n;
 		}
-		if (rn > 56) flush();
 	};
 
 	// Two steps per half-iteration, the other half's two steps in flight; the
@@ -807,7 +843,7 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 	s0.act = s1.act = false;
 	s0.any = s1.any = false;
 	for (;;) {
-		if (!s0.any && !s1.any && am == 0 && bm == 0 && pnext >= end) break;
+		if (!s0.any && !s1.any && ac == na && !bpend && pnext >= end) break;
 		refill();
 		load(t0);
 		load(t1);
@@ -815,7 +851,7 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 		compute(s0);
 		compute(s1);
 		__builtin_amdgcn_sched_barrier(0);
-		if (!t0.any && !t1.any && am == 0 && bm == 0 && pnext >= end) break;
+		if (!t0.any && !t1.any && ac == na && !bpend && pnext >= end) break;
 		refill();
 		load(s0);
 		load(s1);
@@ -1051,27 +1087,27 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 		constexpr int kR = 21;
 		__shared__ uint64_t red[kR][4];
 		uint64_t r[kR] = {};
-		if (t < Q.ntile) {
-			const uint64_t cr = Q.tiles[t], cu = Q.tcns[t], nb = Q.tneed[t];
-			const bool before = t < blockIdx.x;
-			r[18] = cr;
-			r[19] = cu;
-			r[20] = nb;
+		for (uint32_t k = t; k < Q.ntile; k += 256) {  // (thread t takes tiles t, t + 256, ...)
+			const uint64_t cr = Q.tiles[k], cu = Q.tcns[k], nb = Q.tneed[k];
+			const bool before = k < blockIdx.x;
+			r[18] += cr;
+			r[19] += cu;
+			r[20] += nb;
 			if (before) {
-				r[16] = cr;
-				r[17] = cu;
+				r[16] += cr;
+				r[17] += cu;
 			}
 			if (nb)
 #pragma unroll
 				for (uint32_t w = 0; w < 4; ++w) {
-					const uint64_t f = Q.tcls[w * Q.ntile + t];
+					const uint64_t f = Q.tcls[w * Q.ntile + k];
 					const uint64_t a = (f & 0xFFFFull) | ((f >> 16 & 0xFFFFull) << 32);
 					const uint64_t b = (f >> 32 & 0xFFFFull) | ((f >> 48) << 32);
-					r[2 * w] = a;
-					r[2 * w + 1] = b;
+					r[2 * w] += a;
+					r[2 * w + 1] += b;
 					if (before) {
-						r[8 + 2 * w] = a;
-						r[8 + 2 * w + 1] = b;
+						r[8 + 2 * w] += a;
+						r[8 + 2 * w + 1] += b;
 					}
 				}
 		}

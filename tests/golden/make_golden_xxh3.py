@@ -7,7 +7,8 @@ splitmix64 streams (same generator as crc32c_golden.json), so the JSON holds
 parameters and the reference's outputs only.
 
 Usage (in the container that has /root/reference):
-    make -C oracle && python tests/golden/make_golden_xxh3.py
+    make -C oracle && python tests/golden/make_golden_xxh3.py [--varlen]
+(--varlen: only (re)compute the varlen_full section, keeping the rest.)
 """
 import json
 import os
@@ -30,7 +31,45 @@ def sm_bytes(nbytes, state):
     return w.view(np.uint8)[:nbytes].copy()
 
 
+def varlen_full(g):
+    """BASELINE configs[2] (Zipf packets) and configs[4] (backup chunks) at the
+    exact bench shapes (bench_shapes.py), the bytes bench.py hashes (splitmix64,
+    bench_shapes.STATE): the reference's XXH3_64bits over every buffer, and
+    XXH3_64bits_withSeed with per-buffer seeds (bench_shapes.xxh3_seeds), as xor/sum digests
+    plus the first 64 digests."""
+    import ctypes
+    import bench_shapes as S
+    L = O.xxh3_reference()
+    f = L.XXH3_64bits_withSeed
+    out = {}
+    for name in ("zipf", "chunks"):
+        lengths, offsets, extent = S.shape(name)
+        data = O.splitmix64(extent // 8, S.STATE).view(np.uint8)
+        ent = {"state": S.STATE, "count": int(lengths.size), "lengths_sha256": S.lengths_digest(lengths),
+               "digests": []}
+        plain = O.ref_xxh3_batch_varlen(data, offsets, lengths)
+        sd = S.xxh3_seeds(lengths.size)
+        base = data.ctypes.data
+        seeded = np.array([f(ctypes.c_void_p(base + int(o)), int(n), int(s))
+                           for o, n, s in zip(offsets, lengths, sd)], dtype=np.uint64)
+        for kind, h in (("seed0", plain), ("seeds", seeded)):
+            ent["digests"].append({"kind": kind, "xor": "%016x" % int(np.bitwise_xor.reduce(h)),
+                                   "sum": "%016x" % int(h.sum(dtype=np.uint64)),
+                                   "first64": ["%016x" % int(v) for v in h[:64]]})
+        out[name] = ent
+        del data
+    g["varlen_full"] = out
+
+
 def main():
+    if "--varlen" in sys.argv:
+        with open(OUT) as fh:
+            g = json.load(fh)
+        varlen_full(g)
+        with open(OUT, "w") as fh:
+            json.dump(g, fh, indent=0)
+        print("wrote", OUT, os.path.getsize(OUT), "bytes")
+        return
     g = {"generator": "splitmix64 (see crc32c_golden.json)",
          "source": "oracle/_ref/libxxhash_ref.so = /root/reference/flow/xxhash.c + flow/Hash3.c (unmodified)"}
     data = sm_bytes((1 << 20) + 64, 0x5EED)
@@ -76,6 +115,7 @@ def main():
         hl.append({"page": i, "sqlite": list(O.ref_hashlittle2(pg[:4088], i + 1, 0x5ca1ab1e)),
                    "diskqueue": list(O.ref_hashlittle2(pg[16:], 0x12345678, 0xbeefabcd))})
     g["hashlittle2"] = {"kat": kat, "pages": hl}
+    varlen_full(g)
     with open(OUT, "w") as f:
         json.dump(g, f, indent=0)
     print("wrote", OUT, os.path.getsize(OUT), "bytes")

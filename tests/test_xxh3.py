@@ -79,6 +79,22 @@ def test_hashlittle2_known_answers(xg):
 
 
 @pytest.mark.skipif(not O.xxh3_reference_available(), reason="reference build absent")
+@pytest.mark.parametrize("name", ["zipf", "chunks"])
+def test_oracle_varlen_configs_exact_batches(xg, name):
+    """The oracle restatement over the exact bench batches matches the
+    reference's digests (make_golden_xxh3.py --varlen)."""
+    import bench_shapes as S
+    ent = xg["varlen_full"][name]
+    lengths, offsets, extent = S.shape(name)
+    assert S.lengths_digest(lengths) == ent["lengths_sha256"]
+    data = O.splitmix64(extent // 8, ent["state"]).view(np.uint8)
+    for d in ent["digests"]:
+        seeds = S.xxh3_seeds(lengths.size) if d["kind"] == "seeds" else None
+        got = O.xxh3_batch_varlen(data, offsets, lengths, seeds=seeds, threads=8)
+        assert hexs(got[:64]) == d["first64"]
+        assert digest(got) == {"xor": d["xor"], "sum": d["sum"]}
+
+
 def test_oracle_against_reference_random():
     rng = np.random.default_rng(11)
     data = rng.integers(0, 256, 1 << 18, dtype=np.uint8)
@@ -168,6 +184,32 @@ def test_gpu_varlen_random_vs_oracle(cuda):
     offs2 = np.array([0, 5, 1 << 21, 77, (1 << 22) + 9, 1 << 23], dtype=np.int64)
     got = host(X.batch_varlen(d, i64(offs2, cuda), i64(lens2, cuda), seed=7))
     assert np.array_equal(got, O.xxh3_batch_varlen(h, offs2, lens2, seed=7))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["zipf", "chunks"])
+def test_gpu_varlen_configs_exact_batches(xg, cuda, name):
+    """The exact xxh3-zipf (406 k packets, 64 B - 16 KiB) and xxh3-chunks
+    (5773 chunks, 4 KiB - 1 MiB: the split route) batches bench.py measures,
+    over the same splitmix64 bytes, unseeded and with per-buffer seeds, against
+    the digests the reference's flow/xxhash.c produced for every buffer
+    (make_golden_xxh3.py --varlen); the first 64 one by one."""
+    import torch
+    import bench_shapes as S
+    import foundationdb_amd as F
+    import foundationdb_amd.xxh3 as X
+    ent = xg["varlen_full"][name]
+    lengths, offsets, extent = S.shape(name)
+    assert S.lengths_digest(lengths) == ent["lengths_sha256"] and lengths.size == ent["count"]
+    buf = torch.empty(extent, dtype=torch.uint8, device=cuda)
+    F.fill_splitmix64(buf, ent["state"])
+    d_off, d_len = i64(offsets, cuda), i64(lengths, cuda)
+    for d in ent["digests"]:
+        seeds = torch.tensor(S.xxh3_seeds(lengths.size).view(np.int64), device=cuda) if d["kind"] == "seeds" else None
+        got = host(X.batch_varlen(buf, d_off, d_len, seeds=seeds))
+        assert hexs(got[:64]) == d["first64"], (name, d["kind"])
+        assert digest(got) == {"xor": d["xor"], "sum": d["sum"]}, (name, d["kind"])
+    del buf
 
 
 @pytest.mark.gpu

@@ -39,6 +39,18 @@ run("4096 x 256K aligned", [4096] * (1 << 18), 4096)
 run("1024 x 1M", [1024] * (1 << 20), 1024)
 run("256 x 1M", [256] * (1 << 20), 256)
 run("64 x 1M", [64] * (1 << 20), 64)
+run("16384 x 64K", [16384] * (1 << 16), 256)
+run("8192 x 128K", [8192] * (1 << 17), 256)
+run("5000 x 200K", [5000] * 200000, 256)
+_r = np.random.default_rng(4)
+run("rand 4-16K", _r.integers(4097, 16385, 90000), 256)
+run("alt 5000/15000", [5000, 15000] * 50000, 256)
+_z = W.zipf_lengths()
+run("zipf mid (>4K)", _z[_z > 4096], 256)
+run("zipf low (<=4K)", _z[_z <= 4096], 256)
+run("zipf short (<=240)", _z[_z <= 240], 256)
+run("zipf one (241-1K)", _z[(_z > 240) & (_z <= 1024)], 256)
+run("zipf few (1K-4K)", _z[(_z > 1024) & (_z <= 4096)], 256)
 run("zipf", W.zipf_lengths(), 256)
 run("chunks", W.chunk_lengths(), 4096)
 run("zipf unaligned", W.zipf_lengths(), 1)
