@@ -588,6 +588,61 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
 typedef __attribute__((address_space(1))) const u64x2u g_u64x2u;
 
+// xxh3_short for one lane's buffer with every data load issued up front: the
+// 17-240 B forms read up to sixteen 16-byte chunks (unaligned loads, all inside
+// the buffer; unused chunks re-read its first 16 bytes) and add the used ones'
+// mix16 terms (the sums are order-free); chunks no lane of the wave needs are
+// not loaded.  <= 16 B keeps the closed forms.
+__device__ __forceinline__ uint64_t xxh3_short_v(uint64_t p, uint64_t len, uint64_t seed) {
+	if (len <= 16) return xxh3_short(p, len, seed);
+	const bool big = len > 128;
+	const int pairs = (int)((len - 1) >> 5);  // 17-128 B: 0..3 extra pairs
+	const int rounds = (int)len >> 4;         // 129-240 B: 8..15 chunks
+	// chunks no lane of the wave uses are not loaded (uniform branches)
+	const bool anybig = __ballot(big) != 0;
+	const bool need1 = __ballot(!big && pairs >= 1) != 0, need2 = __ballot(!big && pairs >= 2) != 0,
+	           need3 = __ballot(!big && pairs >= 3) != 0;
+	u64x2u x[16];
+#pragma unroll
+	for (int k = 0; k < 16; ++k) {
+		const int q = k & 3;
+		const bool used = anybig || (k < 8 && (q == 0 || (q == 1 && need1) || (q == 2 && need2) || (q == 3 && need3)));
+		if (!used) {
+			x[k] = u64x2u{0, 0};
+			continue;
+		}
+		uint64_t a;
+		if (k < 8) {  // big: chunk k; else front chunk k (< 4) or back chunk k - 4
+			const uint64_t m = k < 4 ? p + 16 * k : p + len - 16 * (k - 3);
+			a = big ? p + 16 * k : ((k & 3) <= pairs ? m : p);
+		} else if (k < 15) {
+			a = big && k < rounds ? p + 16 * k : p;
+		} else {
+			a = big ? p + len - 16 : p;
+		}
+		x[k] = __builtin_nontemporal_load((g_u64x2u*)a);
+	}
+	auto mix = [&](int k, int soff) __attribute__((always_inline)) {
+		return mulfold(x[k][0] ^ (ksec(soff) + seed), x[k][1] ^ (ksec(soff + 8) - seed));
+	};
+	uint64_t acc = len * P64_1;
+	if (!big) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint64_t t = mix(i, 32 * i) + mix(4 + i, 32 * i + 16);
+			acc += i <= pairs ? t : 0;
+		}
+		return xxh3_aval(acc);
+	}
+#pragma unroll
+	for (int i = 0; i < 8; ++i) acc += mix(i, 16 * i);
+	acc = xxh3_aval(acc);
+#pragma unroll
+	for (int i = 8; i < 15; ++i) acc += i < rounds ? mix(i, 16 * (i - 8) + 3) : 0;
+	acc += mix(15, 136 - 17);
+	return xxh3_aval(acc);
+}
+
 __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int j) {
 	const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
 	const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
@@ -865,13 +920,30 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 	// wave starts streaming at once (their dependent length -> data loads kept
 	// HBM idle at the start of the launch: zipf 0.272 -> 0.253 ms, unaligned
 	// zipf 0.352 -> 0.303 ms), and a wave that finishes its rows early does its
-	// short buffers while the others still stream
+	// short buffers while the others still stream.  The next 64 buffers'
+	// lengths and offsets load while this 64's hash, and a hash issues all its
+	// data loads at once (xxh3_short_v): about one memory latency a pass.
+	uint64_t nlen = 0, noff = 0, nsd = seed0;
+	{
+		const uint64_t i = begin + lane;
+		if (i < end) {
+			nlen = lengths[i];
+			noff = offsets[i];
+			if (SEEDS) nsd = seeds[i];
+		}
+	}
 	for (uint64_t b0 = begin; b0 < end; b0 += 64) {
 		const uint64_t i = b0 + lane;
-		if (i < end) {
-			const uint64_t len = lengths[i];
-			if (len <= 240) out[i] = xxh3_short(base + offsets[i], len, SEEDS ? seeds[i] : seed0);
+		const uint64_t len = nlen, off = noff, sd = nsd;
+		const uint64_t i1 = i + 64;
+		if (i1 < end) {
+			nlen = lengths[i1];
+			noff = offsets[i1];
+			if (SEEDS) nsd = seeds[i1];
 		}
+		const bool sh = i < end && len <= 240;
+		if (__ballot(sh) == 0) continue;
+		if (sh) out[i] = xxh3_short_v(base + off, len, sd);
 	}
 }
 
