@@ -377,9 +377,17 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 // last grab, which holds the extent's partial last block, goes first to
 // wave 0 of workgroup 0 with clamped chunk addresses.
 // ---------------------------------------------------------------------------
+#ifdef FDBX_TIMES
+// development: per-wave start / end timestamps of k_xgrab (s_memrealtime, 100 MHz)
+__device__ uint64_t g_xt[16384][4];
+#endif
 __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	if (!x_packed(P)) return;  // k_xfin checksums this batch buffer by buffer
 	if (x_geo(P).nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
+#ifdef FDBX_TIMES
+	const uint64_t xt0 = __builtin_amdgcn_s_memrealtime();
+	uint32_t xt_grabs = 0;
+#endif
 	FillRegs fill;
 	fill_issue_1024(fill, P.tabs);
 	__shared__ uint32_t lds[kLdsBytesB / 4];
@@ -674,6 +682,9 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			finish(H, Y, k + kXU, gb1, gb0, gb1);
 		}
 		if (last_step) {
+#ifdef FDBX_TIMES
+			++xt_grabs;
+#endif
 			flush(q, gb0, gb1);
 			if (lane == 0) P.x.gagg[gA] = X;
 			q = qnx;
@@ -688,6 +699,15 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	}
 	if (bfull) store_bank(bid, bv, by, 64);
 	store_bank(qid, qv, qy, qn);
+#ifdef FDBX_TIMES
+	if (lane == 0) {
+		const uint32_t w = blockIdx.x * wpb + wi;
+		g_xt[w][0] = xt0;
+		g_xt[w][1] = __builtin_amdgcn_s_memrealtime();
+		g_xt[w][2] = xt_grabs;
+		g_xt[w][3] = g1 - g0;
+	}
+#endif
 	// every request of every wave has returned: the counter goes back to zero
 	__builtin_amdgcn_s_waitcnt(0);
 	__syncthreads();
@@ -1048,3 +1068,9 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 }
 
 }  // namespace fdbcrc
+
+#ifdef FDBX_TIMES
+extern "C" int fdbx_debug_times(void* host, uint64_t nwave) {
+	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbcrc::g_xt), nwave * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif

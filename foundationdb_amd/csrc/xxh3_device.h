@@ -29,6 +29,8 @@ constexpr unsigned kWavesPerBlock = 4;
 // computed by one CU's waves at once (k_xlong), largest first.  Planner
 // output in the workspace:
 constexpr uint64_t kXSplitMin = 16384;
+// varlen buffers of 241 B .. kXQuadMax go to lane quads, longer ones to the rows
+constexpr uint64_t kXQuadMax = 1024;
 struct XEnt {       // one long buffer
 	uint64_t p;     // its address
 	uint64_t len, seed, idx;

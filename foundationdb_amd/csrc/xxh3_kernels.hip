@@ -588,27 +588,29 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
 typedef __attribute__((address_space(1))) const u64x2u g_u64x2u;
 
-// xxh3_short for one lane's buffer with every data load issued up front: the
-// 17-240 B forms read up to sixteen 16-byte chunks (unaligned loads, all inside
-// the buffer; unused chunks re-read its first 16 bytes) and add the used ones'
-// mix16 terms (the sums are order-free); chunks no lane of the wave needs are
-// not loaded.  <= 16 B keeps the closed forms.
-__device__ __forceinline__ uint64_t xxh3_short_v(uint64_t p, uint64_t len, uint64_t seed) {
-	if (len <= 16) return xxh3_short(p, len, seed);
+// xxh3_short (17-240 B, xxhash.h:2847-2951) for one lane's buffer in two
+// halves, so that a pass issues every data load it has (these and the lane
+// quads') before it waits for any: the 17-240 B forms read up to sixteen
+// 16-byte chunks (unaligned loads, all inside the buffer; unused chunks
+// re-read its first 16 bytes) and add the used ones' mix16 terms (the sums are
+// order-free).  Chunks no lane of the wave uses are not loaded.  `on` lanes
+// only: the others pass a readable dummy.
+struct ShortLd {
+	u64x2u x[16];
+};
+__device__ __forceinline__ void short_load(ShortLd& S, uint64_t p, uint64_t len, bool on) {
 	const bool big = len > 128;
 	const int pairs = (int)((len - 1) >> 5);  // 17-128 B: 0..3 extra pairs
 	const int rounds = (int)len >> 4;         // 129-240 B: 8..15 chunks
-	// chunks no lane of the wave uses are not loaded (uniform branches)
-	const bool anybig = __ballot(big) != 0;
-	const bool need1 = __ballot(!big && pairs >= 1) != 0, need2 = __ballot(!big && pairs >= 2) != 0,
-	           need3 = __ballot(!big && pairs >= 3) != 0;
-	u64x2u x[16];
+	const bool anybig = __ballot(on && big) != 0;
+	const bool need1 = __ballot(on && !big && pairs >= 1) != 0, need2 = __ballot(on && !big && pairs >= 2) != 0,
+	           need3 = __ballot(on && !big && pairs >= 3) != 0;
 #pragma unroll
 	for (int k = 0; k < 16; ++k) {
 		const int q = k & 3;
 		const bool used = anybig || (k < 8 && (q == 0 || (q == 1 && need1) || (q == 2 && need2) || (q == 3 && need3)));
 		if (!used) {
-			x[k] = u64x2u{0, 0};
+			S.x[k] = u64x2u{0, 0};
 			continue;
 		}
 		uint64_t a;
@@ -620,10 +622,15 @@ __device__ __forceinline__ uint64_t xxh3_short_v(uint64_t p, uint64_t len, uint6
 		} else {
 			a = big ? p + len - 16 : p;
 		}
-		x[k] = __builtin_nontemporal_load((g_u64x2u*)a);
+		S.x[k] = __builtin_nontemporal_load((g_u64x2u*)a);
 	}
+}
+__device__ __forceinline__ uint64_t short_fin(const ShortLd& S, uint64_t len, uint64_t seed) {
+	const bool big = len > 128;
+	const int pairs = (int)((len - 1) >> 5);
+	const int rounds = (int)len >> 4;
 	auto mix = [&](int k, int soff) __attribute__((always_inline)) {
-		return mulfold(x[k][0] ^ (ksec(soff) + seed), x[k][1] ^ (ksec(soff + 8) - seed));
+		return mulfold(S.x[k][0] ^ (ksec(soff) + seed), S.x[k][1] ^ (ksec(soff + 8) - seed));
 	};
 	uint64_t acc = len * P64_1;
 	if (!big) {
@@ -641,6 +648,72 @@ __device__ __forceinline__ uint64_t xxh3_short_v(uint64_t p, uint64_t len, uint6
 	for (int i = 8; i < 15; ++i) acc += i < rounds ? mix(i, 16 * (i - 8) + 3) : 0;
 	acc += mix(15, 136 - 17);
 	return xxh3_aval(acc);
+}
+
+// XXH3 of 241 B - 1 KiB (one partial block, xxhash.h:3641-3718: no scramble)
+// on a lane quad: lane k keeps accumulator pair k over the (len-1)/64 stripes
+// and the last one, the four merge terms add over the quad.  Every data load
+// is issued up front; stripes no lane of the wave has are not loaded.
+// Secret word j (+-seed by parity, xxhash.h:3550-3566) from an LDS copy of
+// the default secret, at a lane-dependent index (constants would sit in
+// SGPRs across the whole kernel and spill).
+__device__ __forceinline__ uint64_t lword(const uint64_t* ks, int j, uint64_t seed) {
+	return (j & 1) ? ks[j] - seed : ks[j] + seed;
+}
+template <int S>
+__device__ __forceinline__ void quad_stripe(uint64_t& a0, uint64_t& a1, const u64x2u& v, bool on, int k,
+                                            const uint64_t* ks, uint64_t seed) {
+	const uint64_t x0 = v[0] ^ lword(ks, S + 2 * k, seed), x1 = v[1] ^ lword(ks, S + 2 * k + 1, seed);
+	a0 += on ? v[1] + (uint64_t)(uint32_t)x0 * (x0 >> 32) : 0;
+	a1 += on ? v[0] + (uint64_t)(uint32_t)x1 * (x1 >> 32) : 0;
+}
+// secret bytes [8j + r, 8j + r + 8), 0 < r < 8
+__device__ __forceinline__ uint64_t lat(const uint64_t* ks, int j, int r, uint64_t seed) {
+	return (lword(ks, j, seed) >> (8 * r)) | (lword(ks, j + 1, seed) << (64 - 8 * r));
+}
+struct QuadLd {
+	u64x2u v[15], vl;
+};
+__device__ __forceinline__ void quad_load(QuadLd& Q, uint64_t p, uint64_t len, int k) {
+	const int ns = (int)((len - 1) >> 6);  // 3..15 full stripes
+#pragma unroll
+	for (int st = 0; st < 15; ++st) {
+		if (st < 3 || __ballot(st < ns) != 0)
+			Q.v[st] = __builtin_nontemporal_load((g_u64x2u*)(p + 64 * st + 16 * k));
+		else
+			Q.v[st] = u64x2u{0, 0};
+	}
+	Q.vl = __builtin_nontemporal_load((g_u64x2u*)(p + len - 64 + 16 * k));
+}
+__device__ __forceinline__ uint64_t quad_fin(const QuadLd& Q, uint64_t len, uint64_t seed, int k, const uint64_t* ks) {
+	const int ns = (int)((len - 1) >> 6);
+	uint64_t a0 = k == 0 ? P32_3 : (k == 1 ? P64_2 : (k == 2 ? P64_4 : P64_5));
+	uint64_t a1 = k == 0 ? P64_1 : (k == 1 ? P64_3 : (k == 2 ? P32_2 : P32_1));
+	quad_stripe<0>(a0, a1, Q.v[0], true, k, ks, seed);
+	quad_stripe<1>(a0, a1, Q.v[1], true, k, ks, seed);
+	quad_stripe<2>(a0, a1, Q.v[2], true, k, ks, seed);
+	quad_stripe<3>(a0, a1, Q.v[3], 3 < ns, k, ks, seed);
+	quad_stripe<4>(a0, a1, Q.v[4], 4 < ns, k, ks, seed);
+	quad_stripe<5>(a0, a1, Q.v[5], 5 < ns, k, ks, seed);
+	quad_stripe<6>(a0, a1, Q.v[6], 6 < ns, k, ks, seed);
+	quad_stripe<7>(a0, a1, Q.v[7], 7 < ns, k, ks, seed);
+	quad_stripe<8>(a0, a1, Q.v[8], 8 < ns, k, ks, seed);
+	quad_stripe<9>(a0, a1, Q.v[9], 9 < ns, k, ks, seed);
+	quad_stripe<10>(a0, a1, Q.v[10], 10 < ns, k, ks, seed);
+	quad_stripe<11>(a0, a1, Q.v[11], 11 < ns, k, ks, seed);
+	quad_stripe<12>(a0, a1, Q.v[12], 12 < ns, k, ks, seed);
+	quad_stripe<13>(a0, a1, Q.v[13], 13 < ns, k, ks, seed);
+	quad_stripe<14>(a0, a1, Q.v[14], 14 < ns, k, ks, seed);
+	{  // the last stripe: secret + 121
+		const uint64_t x0 = Q.vl[0] ^ lat(ks, 15 + 2 * k, 1, seed), x1 = Q.vl[1] ^ lat(ks, 16 + 2 * k, 1, seed);
+		a0 += Q.vl[1] + (uint64_t)(uint32_t)x0 * (x0 >> 32);
+		a1 += Q.vl[0] + (uint64_t)(uint32_t)x1 * (x1 >> 32);
+	}
+	const uint64_t m = mulfold(a0 ^ lat(ks, 1 + 2 * k, 3, seed), a1 ^ lat(ks, 2 + 2 * k, 3, seed));  // merge: secret + 11
+	uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+	add_dpp<0xB1>(lo, hi);
+	add_dpp<0x4E>(lo, hi);
+	return xxh3_aval(len * P64_1 + (((uint64_t)hi << 32) | lo));
 }
 
 __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int j) {
@@ -678,13 +751,29 @@ struct VStep {
 	bool any;                 // some row has one (uniform)
 };
 
+#ifdef FDBXXH_TIMES
+// development: per-wave timestamps of the row kernel (start, rows done, end; s_memrealtime, 100 MHz)
+__device__ uint64_t g_vt[16384][4];
+#endif
+constexpr int kTailPasses = 4;                    // buffers listed at once: 64 each
+constexpr uint32_t kTailCap = 64 * kTailPasses;  // list entries per wave
 template <bool SEEDS>
-__global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_xxh3_vrows(XxhParams P) {
 	if (P.d_count) P.count = min(P.count, (uint64_t)*P.d_count);  // device-sized batch (the planner's too)
 	const int lane = threadIdx.x & 63;
 	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
+	__shared__ uint64_t ksl[24];  // the default secret (the quad path's keys)
+	// per wave: the tail's short (from the front) and quad (from the back) lists
+	__shared__ uint64_t tlen[4][kTailCap], toff[4][kTailCap];
+	__shared__ uint32_t tidx[4][kTailCap];
+	__shared__ uint64_t tsd[SEEDS ? 4 : 1][SEEDS ? kTailCap : 1];
+	if (threadIdx.x < 24) ksl[threadIdx.x] = SEEDS ? kSec[threadIdx.x] : sec_word((int)threadIdx.x, P.seed);
+	__syncthreads();
 	const uint64_t wpb = blockDim.x >> 6;
 	const uint64_t w = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef FDBXXH_TIMES
+	const uint64_t vt0 = __builtin_amdgcn_s_memrealtime();
+#endif
 	const uint64_t begin = rdfirst64v(P.wave_first[w]);
 	uint64_t end = rdfirst64v(P.wave_first[w + 1]);
 	end = end < P.count ? end : P.count;
@@ -731,7 +820,7 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 				issue_b();
 			}
 			bpend = false;
-			const bool on = blen > 240 && !(blen > kXSplitMin && bfl);
+			const bool on = blen > kXQuadMax && !(blen > kXSplitMin && bfl);
 			const uint64_t m = __ballot(on);
 			const uint32_t n = (uint32_t)__builtin_popcountll(m);
 			if (n == 0) continue;
@@ -916,35 +1005,114 @@ __global__ __launch_bounds__(256) void k_xxh3_vrows(XxhParams P) {
 		__builtin_amdgcn_sched_barrier(0);
 	}
 	flush();
-	// ---- short buffers, one lane each: after the long ones, so that every
-	// wave starts streaming at once (their dependent length -> data loads kept
-	// HBM idle at the start of the launch: zipf 0.272 -> 0.253 ms, unaligned
-	// zipf 0.352 -> 0.303 ms), and a wave that finishes its rows early does its
-	// short buffers while the others still stream.  The next 64 buffers'
-	// lengths and offsets load while this 64's hash, and a hash issues all its
-	// data loads at once (xxh3_short_v): about one memory latency a pass.
-	uint64_t nlen = 0, noff = 0, nsd = seed0;
-	{
-		const uint64_t i = begin + lane;
-		if (i < end) {
-			nlen = lengths[i];
-			noff = offsets[i];
-			if (SEEDS) nsd = seeds[i];
+	// ---- short buffers (<= 240 B, one lane each) and 241 B - 1 KiB ones (lane
+	// quads, xxh3_quad): after the long ones, so that every wave starts
+	// streaming at once (their dependent length -> data loads kept HBM idle at
+	// the start of the launch: zipf 0.272 -> 0.253 ms, unaligned zipf 0.352 ->
+	// 0.303 ms).  This part is a chain of memory round trips per wave (zipf: 30
+	// us of the row kernel), so it is made dense: the lengths and offsets of
+	// up to 512 buffers load at once, the short and quad ones are listed in the
+	// wave's LDS (compacted), and then every pass is full -- 64 short buffers,
+	// or 16 quads, one round trip each.  A pass's results are stored after the
+	// next pass's loads are issued (a store holds up every later wait on loads
+	// issued behind it: in-order vmcnt).
+#ifdef FDBXXH_NOTAIL
+	if (P.count != 12345) return;  // timing experiment: no short/quad phase (wrong results)
+#endif
+#ifdef FDBXXH_TIMES
+	const uint64_t vt1 = __builtin_amdgcn_s_memrealtime();
+#endif
+	const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	uint64_t* const tl_len = tlen[wv];
+	uint64_t* const tl_off = toff[wv];
+	uint32_t* const tl_idx = tidx[wv];
+	uint64_t* const tl_sd = SEEDS ? tsd[wv] : nullptr;
+	uint64_t pend_h = 0, pend_i = 0;
+	bool pend = false;
+	auto flushp = [&]() __attribute__((always_inline)) {  // after the next pass's loads
+		if (pend) out[pend_i] = pend_h;
+		pend = false;
+	};
+	auto put = [&](bool on, uint64_t h, uint64_t idx) __attribute__((always_inline)) {
+		pend_h = h;
+		pend_i = idx;
+		pend = on;
+	};
+	for (uint64_t c0 = begin; c0 < end; c0 += 64 * kTailPasses) {
+		uint64_t L[kTailPasses], O[kTailPasses], D[kTailPasses];
+#pragma unroll
+		for (int q = 0; q < kTailPasses; ++q) {
+			const uint64_t i = c0 + 64 * q + lane;
+			const bool in = i < end;
+			const uint64_t ic = in ? i : begin;  // (every load unconditional)
+			L[q] = lengths[ic];
+			O[q] = offsets[ic];
+			D[q] = SEEDS ? seeds[ic] : seed0;
+			if (!in) L[q] = ~0ull;  // (no class)
 		}
-	}
-	for (uint64_t b0 = begin; b0 < end; b0 += 64) {
-		const uint64_t i = b0 + lane;
-		const uint64_t len = nlen, off = noff, sd = nsd;
-		const uint64_t i1 = i + 64;
-		if (i1 < end) {
-			nlen = lengths[i1];
-			noff = offsets[i1];
-			if (SEEDS) nsd = seeds[i1];
+		uint32_t ns = 0, nq = 0;
+#pragma unroll
+		for (int q = 0; q < kTailPasses; ++q) {
+			const uint64_t i = c0 + 64 * q + lane;
+			const uint64_t len = L[q];
+			const bool tiny = len <= 16, sh = len > 16 && len <= 240, qd = len > 240 && len <= kXQuadMax;
+			if (__ballot(tiny) != 0 && tiny) out[i] = xxh3_short(base + O[q], len, D[q]);  // (rare)
+			const uint64_t ms = __ballot(sh), mq = __ballot(qd);
+			if (sh) {
+				const uint32_t e = ns + mbcnt64(ms);
+				tl_len[e] = len;
+				tl_off[e] = O[q];
+				tl_idx[e] = (uint32_t)(i - begin);
+				if (SEEDS) tl_sd[e] = D[q];
+			}
+			if (qd) {
+				const uint32_t e = kTailCap - 1 - (nq + mbcnt64(mq));
+				tl_len[e] = len;
+				tl_off[e] = O[q];
+				tl_idx[e] = (uint32_t)(i - begin);
+				if (SEEDS) tl_sd[e] = D[q];
+			}
+			ns += (uint32_t)__builtin_popcountll(ms);
+			nq += (uint32_t)__builtin_popcountll(mq);
 		}
-		const bool sh = i < end && len <= 240;
-		if (__ballot(sh) == 0) continue;
-		if (sh) out[i] = xxh3_short_v(base + off, len, sd);
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		for (uint32_t s0 = 0; s0 < ns; s0 += 64) {  // full passes of short buffers
+			const uint32_t e = s0 + lane;
+			const bool on = e < ns;
+			const uint32_t ec = on ? e : s0;
+			const uint64_t len = tl_len[ec], off = tl_off[ec], sd = SEEDS ? tl_sd[ec] : seed0;
+			const uint64_t idx = begin + tl_idx[ec];
+			ShortLd SL;
+			short_load(SL, base + off, len, on);
+			flushp();
+			put(on, short_fin(SL, len, sd), idx);
+		}
+		for (uint32_t t0 = 0; t0 < nq; t0 += 16) {  // full passes of sixteen quads
+			const uint32_t e = t0 + ((uint32_t)lane >> 2);
+			const bool act = e < nq;
+			const uint32_t ec = kTailCap - 1 - (act ? e : t0);
+			const uint64_t len = act ? tl_len[ec] : 256, off = act ? base + tl_off[ec] : dummy;
+			const uint64_t sd = SEEDS ? tl_sd[ec] : 0;
+			const uint64_t idx = begin + tl_idx[ec];
+			QuadLd QL;
+			quad_load(QL, off, len, lane & 3);
+			flushp();
+			put(act && (lane & 3) == 0, quad_fin(QL, len, sd, lane & 3, ksl), idx);  // (unseeded: ksl holds the seed's secret)
+		}
+		__builtin_amdgcn_wave_barrier();  // (the list is rewritten by the next chunk)
 	}
+	if (pend) out[pend_i] = pend_h;
+#ifdef FDBXXH_TIMES
+	const uint64_t vt2 = __builtin_amdgcn_s_memrealtime();
+	if (lane == 0 && w < 16384) {
+		g_vt[w][0] = vt0;
+		g_vt[w][1] = vt1;
+		g_vt[w][2] = vt2;
+		g_vt[w][3] = end - begin;
+	}
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -975,12 +1143,44 @@ struct XPlanP {
 	uint8_t* flag;            // per buffer: 1 if the long route took it
 	uint64_t* wave_first;
 	uint64_t ntile, nwave;
+	uint64_t older;           // waves of the first-dispatched workgroups (0: all weighted alike)
 	XEnt* ents;
 	uint64_t capS;            // entries the room holds (0: no room)
 	uint64_t* hneed;          // host-mapped word (may be null): blocks the batch's long buffers need
 	const uint64_t* dcount;   // may be null: the batch size is min(count, *dcount) (count bounds the grid)
 };
 constexpr uint64_t kTileRouted = 1ull << 63;
+// The row kernel's waves as placed on the CUs: with two workgroups per CU the
+// first-dispatched one's waves are older and win the SIMD's issue arbitration,
+// and stream the same bytes ~19 % sooner (zipf, per-wave timestamps: 142 vs
+// 169 us median).  Their ranges are longer by that ratio (kXOlderW / 16), so
+// both generations end together.  B(w) = w * qa for the `older` first waves,
+// then qb per wave.
+#ifndef FDBXXH_OLDER16
+#define FDBXXH_OLDER16 19
+#endif
+constexpr uint64_t kXOlderW = FDBXXH_OLDER16;
+struct XQuant {
+	uint64_t qa, qb, h;
+};
+__device__ __forceinline__ XQuant xquant(uint64_t total, uint64_t nwave, uint64_t older) {
+	XQuant W;
+	if (older == 0 || older >= nwave) {
+		W.qa = W.qb = max((total + nwave - 1) / nwave, (uint64_t)1);
+		W.h = 0;
+		return W;
+	}
+	const uint64_t den = 16 * (nwave - older) + kXOlderW * older;
+	W.qb = max((16 * total + den - 1) / den, (uint64_t)1);
+	W.qa = (W.qb * kXOlderW + 15) / 16;
+	W.h = older;
+	return W;
+}
+// the last wave w with B(w) <= x
+__device__ __forceinline__ uint64_t xquant_wave(const XQuant& W, uint64_t x) {
+	const uint64_t ha = W.h * W.qa;
+	return x < ha ? x / W.qa : W.h + (x - ha) / W.qb;
+}
 __device__ __forceinline__ uint64_t xp_len(const XPlanP& Q, uint64_t i) { return Q.lengths ? Q.lengths[i] : Q.length; }
 __device__ __forceinline__ uint64_t xp_off(const XPlanP& Q, uint64_t i) { return Q.offsets ? Q.offsets[i] : i * Q.stride; }
 __device__ __forceinline__ uint64_t xp_blocks(uint64_t len) { return ((len - 1) >> 10) + 1; }
@@ -1049,8 +1249,8 @@ __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
 // stream's last need; the _ws form's caller sizes it with
 // xxh3_gpu_varlen_workspace_bytes_for), else the row kernel takes the whole
 // batch.  In place: the exclusive prefixes of the routed tile costs,
-// tiles[ntile] = total cost, tiles[ntile + 1] = quantum Q = ceil(total /
-// nwave), the route flag in tneed; in sh[] the long buffers routed, the
+// tiles[ntile] = total cost (k_xassign derives the waves' quanta from it,
+// xquant), the route flag in tneed; in sh[] the long buffers routed, the
 // dequeue counter (0) and the size classes' cursors (their bases, largest
 // class first).
 __global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
@@ -1115,7 +1315,7 @@ __global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
 	if (t == 0) {
 		const uint64_t total = carry_s;
 		tiles[ntile] = total;
-		tiles[ntile + 1] = (total + Q.nwave - 1) / Q.nwave;
+		tiles[ntile + 1] = 0;  // (the quantum: xquant of the total)
 		Q.sh[0] = routed ? nlong : 0;
 		Q.sh[1] = 0;
 		Q.sh[2] = 0;
@@ -1150,7 +1350,8 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
 	const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
 	bool routed;
-	uint64_t q, tile_start;
+	uint64_t tile_start;
+	XQuant W;
 	if (FUSED) {
 		// r[0..7]: the classes' counts over all tiles, r[8..15] over the tiles
 		// before this one (32-bit fields, two classes a word); r[16], r[17]: the
@@ -1203,7 +1404,7 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 		routed = nlong != 0 && Q.capS && nlong <= Q.capS;
 		tile_start = routed ? tot[16] : tot[17];
 		const uint64_t total = routed ? tot[18] : tot[19];
-		q = (total + Q.nwave - 1) / Q.nwave;
+		W = xquant(total, Q.nwave, Q.older);
 		if (t < kXClasses) {
 			uint64_t b = 0;
 #pragma unroll
@@ -1221,7 +1422,7 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 		}
 	} else {
 		routed = (Q.tneed[blockIdx.x] & kTileRouted) != 0;
-		q = Q.tiles[Q.ntile + 1];
+		W = xquant(Q.tiles[Q.ntile], Q.nwave, Q.older);
 		tile_start = Q.tiles[blockIdx.x];
 	}
 	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
@@ -1251,11 +1452,11 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 			const uint64_t lp = xp_len(Q, i - 1);
 			prev = start - xp_cost(lp, routed && xp_long(lp));  // (the route is batch-wide)
 		}
-		const uint64_t w_lo = i == 0 ? 0 : prev / q + 1;
-		const uint64_t w_hi = start / q;
+		const uint64_t w_lo = i == 0 ? 0 : xquant_wave(W, prev) + 1;
+		const uint64_t w_hi = xquant_wave(W, start);
 		for (uint64_t w = w_lo; w <= w_hi && w < Q.nwave; ++w) Q.wave_first[w] = i;
 		if (i + 1 == Q.count)  // waves whose first byte lies past the last buffer's start: none
-			for (uint64_t w = start / q + 1; w <= Q.nwave; ++w) Q.wave_first[w] = Q.count;
+			for (uint64_t w = w_hi + 1; w <= Q.nwave; ++w) Q.wave_first[w] = Q.count;
 	}
 	if (lg) {
 		const uint64_t pos = cbase[cl] + rank;
@@ -1344,6 +1545,7 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		Q.wave_first = reinterpret_cast<uint64_t*>(w8 + L.wave_first);
 		Q.ntile = ntile;
 		Q.nwave = nwave;
+		Q.older = xxh3_blocks_per_cu() == 2 ? nwave / 2 : 0;
 		Q.ents = reinterpret_cast<XEnt*>(w8 + L.ents);
 		Q.capS = L.capS;
 		Q.hneed = P.hneed;
@@ -1414,3 +1616,9 @@ int launch_xxh3_pages_list(const XxhParams& P, int num_cus, hipStream_t stream) 
 }
 
 }  // namespace fdbxxh
+
+#ifdef FDBXXH_TIMES
+extern "C" int fdbxxh_debug_times(void* host, uint64_t nwave) {
+	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbxxh::g_vt), nwave * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -1,33 +1,57 @@
 """CPU model of the XXH3 varlen planner (k_xplan / k_xscan / k_xassign in
 foundationdb_amd/csrc/xxh3_kernels.hip): every wave w must get as its first
 buffer the first buffer whose start (in cost units, length + 64 per buffer)
-is >= w*Q, and the last entry must be `count`."""
+is >= B(w), and the last entry must be `count`.  B(w) = w * qa for the
+`older` first waves (the first-dispatched workgroups'), then qb per wave, qa
+= qb * 19 / 16 (xquant); older = 0 is the uniform split."""
 import numpy as np
 
+OLDER_W = 19  # kXOlderW (sixteenths)
 
-def plan(lengths, nwave):
+
+def xquant(total, nwave, older):
+    if older == 0 or older >= nwave:
+        q = max((total + nwave - 1) // nwave, 1)
+        return q, q, 0
+    den = 16 * (nwave - older) + OLDER_W * older
+    qb = max((16 * total + den - 1) // den, 1)
+    return (qb * OLDER_W + 15) // 16, qb, older
+
+
+def xquant_wave(W, x):
+    qa, qb, h = W
+    return x // qa if x < h * qa else h + (x - h * qa) // qb
+
+
+def boundary(W, w):
+    qa, qb, h = W
+    return w * qa if w <= h else h * qa + (w - h) * qb
+
+
+def plan(lengths, nwave, older=0):
     cost = lengths.astype(np.uint64) + 64
     start = np.concatenate([[0], np.cumsum(cost)[:-1]]).astype(np.uint64)
     total = int(cost.sum())
-    q = (total + nwave - 1) // nwave
+    W = xquant(total, nwave, older)
     wf = np.full(nwave + 1, -1, dtype=np.int64)
     n = lengths.size
     for i in range(n):  # one thread per buffer, as in k_xassign
         s = int(start[i])
         prev = 0 if i == 0 else s - int(lengths[i - 1] + 64)
-        w_lo = 0 if i == 0 else prev // q + 1
-        for w in range(w_lo, min(s // q, nwave - 1) + 1):
+        w_lo = 0 if i == 0 else xquant_wave(W, prev) + 1
+        w_hi = xquant_wave(W, s)
+        for w in range(w_lo, min(w_hi, nwave - 1) + 1):
             wf[w] = i
         if i + 1 == n:
-            for w in range(s // q + 1, nwave + 1):
+            for w in range(w_hi + 1, nwave + 1):
                 wf[w] = n
-    return wf, start, q
+    return wf, start, W
 
 
-def expected(start, q, nwave, n):
+def expected(start, W, nwave, n):
     wf = np.empty(nwave + 1, dtype=np.int64)
     for w in range(nwave + 1):
-        wf[w] = int(np.searchsorted(start, w * q, side="left")) if w < nwave else n
+        wf[w] = int(np.searchsorted(start, boundary(W, w), side="left")) if w < nwave else n
     return wf
 
 
@@ -45,10 +69,23 @@ def test_planner_covers_every_wave():
         else:
             lens = np.zeros(n, dtype=np.int64)
         nwave = int(rng.choice([64, 1024, 5120]))
-        wf, start, q = plan(lens, nwave)
+        older = nwave // 2 if trial % 2 else 0
+        wf, start, W = plan(lens, nwave, older)
         assert (wf >= 0).all(), "unassigned wave"
-        assert np.array_equal(wf, expected(start, q, nwave, n))
+        assert np.array_equal(wf, expected(start, W, nwave, n))
         assert (np.diff(wf) >= 0).all() and wf[-1] == n
+        # the boundaries cover the whole cost range: the last wave's start is within the total
+        assert boundary(W, nwave) >= int(start[-1]) if n else True
+
+
+def test_older_waves_get_longer_ranges():
+    """With two workgroup generations the first half of the waves gets 19/16
+    of the second half's cost each (so both end together on the GPU)."""
+    lens = np.full(200000, 5000)
+    wf, start, W = plan(lens, 2048, 1024)
+    per = np.diff(wf)[:-1]
+    a, b = per[:1024].mean(), per[1024:2047].mean()
+    assert abs(a / b - 19 / 16) < 0.02
 
 
 # ---- long-buffer route (k_xplan / k_xscan / k_xassign, then k_xlong's order)
@@ -100,5 +137,5 @@ def test_long_route_entries_by_size_class():
         else:
             assert order == [] and (cost == lens + 64).all()
         # the row kernel's waves still cover every buffer (the cost model above)
-        wf, start, q = plan(cost - 64, 64)
+        wf, start, W = plan(cost - 64, 64)
         assert (wf >= 0).all() and wf[-1] == n

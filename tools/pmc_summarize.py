@@ -92,15 +92,17 @@ def _varlen(fn, per_buffer=20):
     return f
 
 
-VARLEN_KERNELS = ("k_v7count", "k_v7prep", "k_scan", "k_varlen7", "k_bigblocks", "k_xstream", "k_xz", "k_xfin")
+VARLEN_KERNELS = ("k_v7count", "k_xcount", "k_v7prep", "k_scan", "k_varlen7", "k_bigblocks", "k_xstream", "k_xgrab",
+                  "k_xz", "k_xfin")
+XXH3_VARLEN_KERNELS = ("k_xplan", "k_xscan", "k_xassign", "k_xlong", "k_xxh3_vrows")
 PRESETS = {
     "pages4k": ("pages4k", "pages4k", ("k_pages4k",), (1 << 20) * 4100, 1 << 20),
     "pages8k": ("pages8k", "pages8k", ("k_pages4k",), (1 << 19) * 8196, 1 << 19),
     "xxh3": ("xxh3", "xxh3-pages4k", ("k_xxh3_rows",), (1 << 20) * (4088 + 8), 1 << 20),
     "zipf": ("zipf", "zipf", VARLEN_KERNELS, _varlen("zipf_lengths"), None),
     "chunks": ("chunks", "chunks", VARLEN_KERNELS, _varlen("chunk_lengths"), None),
-    "xchunks": ("xchunks", "xxh3-chunks", ("k_xplan", "k_xscan", "k_xassign", "k_xlong", "k_xxh3_vrows"),
-                _varlen("chunk_lengths", 24), None),
+    "xchunks": ("xchunks", "xxh3-chunks", XXH3_VARLEN_KERNELS, _varlen("chunk_lengths", 24), None),
+    "xzipf": ("xzipf", "xxh3-zipf", XXH3_VARLEN_KERNELS, _varlen("zipf_lengths", 24), None),
 }
 
 if __name__ == "__main__":

@@ -35,7 +35,7 @@ for w in pages8k zipf chunks xxh3-pages4k xxh3-zipf xxh3-chunks sqlite-verify di
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_$w -o $w -- python bench.py --workload $w --steps 20 --cpu-seconds 0 --no-verify > $R/prof_$w.log 2>&1 || exit 1
 done
 echo rocprof done
-for MODE in pages4k pages8k xxh3 zipf chunks xchunks; do
+for MODE in pages4k pages8k xxh3 zipf chunks xchunks xzipf; do
   for spec in "fetch FETCH_SIZE" "write WRITE_SIZE" "sq GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD"; do
     set -- $spec; name=$1; shift
     timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $P/$MODE -o ${name}_$MODE -- python tools/pmc_probe.py $MODE > $P/$MODE.log 2>&1 || exit 1
