@@ -291,11 +291,7 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 			const uint32_t y = pull(wcs, wqs);
 			Ys = hs ? y : Ys;
 		}
-#ifdef FDBX_NOPULL
-		if (false) {
-#else
 		if (__ballot(he && wqe)) {
-#endif
 			const uint32_t y = pull(wce, wqe);
 			Ye = he ? y : Ye;
 		}
@@ -305,11 +301,7 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 		uint32_t Z[2 * kXU];
 #pragma unroll
 		for (uint32_t j = 0; j < 2 * kXU; ++j) {
-#ifdef FDBX_NOMUL
-			Z[j] = X;
-#else
 			Z[j] = mulM(X);
-#endif
 			if (k + j < kend) X = Z[j] ^ rdlane(H[j], 63);
 		}
 #pragma unroll
@@ -417,6 +409,24 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		if (lane == 0) r = atomicAdd(my_ctr, 1u);
 		return r;
 	};
+#ifdef FDBX_STEAL
+	// A workgroup whose own grabs are all taken takes grabs of other
+	// workgroups' ranges from their counters (the CUs do not stream at one
+	// speed).  The counters are then reset by k_xfin, not here.
+	uint32_t sk = 0;
+	auto steal = [&]() -> uint32_t {
+		for (; sk < kXStealTries; ++sk) {
+			const uint32_t v = (blockIdx.x + 8 * (sk + 1)) % gridDim.x;  // (same XCD first)
+			const uint32_t v0 = v * gper < nd ? v * gper : nd;
+			const uint32_t v1 = v0 + gper < nd ? v0 + gper : nd;
+			uint32_t r = 0;
+			if (lane == 0) r = atomicAdd(P.ctr + kPageCtrWords * v, 1u);
+			const uint32_t g = v0 + 2 * wpb + rdlane(r, 0);
+			if (g < v1) return g;
+		}
+		return nd;
+	};
+#endif
 	auto blk_ptr = [&](uint32_t k) { return reinterpret_cast<const uint8_t*>(G.S + 4096ull * k); };
 	// a dynamic step's blocks (a step past the wave's grabs re-reads block 0: discarded)
 	auto load_step_unit = [&](Block (&u)[kXU], uint32_t g, uint32_t s, uint32_t half) {
@@ -438,9 +448,6 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	uint32_t Vs = 0, Ve = 0, Ys = 0, Ye = 0;
 	uint64_t pf0 = 0, pf1 = 0;  // the next window's buffer (prefetched)
 	auto prefetch = [&](uint32_t q0) {
-#ifdef FDBX_NOWIN
-		if (q0 != 0x7FFFFFFFu) { pf0 = G.S + 64 * q0 + lane; pf1 = pf0 + 100; return; }
-#endif
 		const uint32_t j = q0 + lane < cnt32 ? q0 + lane : cnt32 - 1;
 		x_buffer(P, j, pf0, pf1);
 	};
@@ -499,20 +506,8 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		qn += n;
 	};
 	auto flush = [&](uint32_t q0, uint32_t kb0, uint32_t kb1) {
-#ifdef FDBX_NOFLUSH
-		if (Vs != 0x12345u) return;
-#endif
 		const bool ok = q0 + lane < cnt32;
 		const bool os = ok && wbs >= kb0 && wbs < kb1, oe = ok && wbe >= kb0 && wbe < kb1;
-#ifdef FDBX_DIRECT
-		{
-			typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-			uint32_t* const dmy = P.x.dummy + 128 * (blockIdx.x * wpb + wi);
-			*reinterpret_cast<u32x2*>(os ? P.x.ps + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Vs, Ys};
-			*reinterpret_cast<u32x2*>(oe ? P.x.pe + 2ull * (q0 + lane) : dmy + 2 * lane) = u32x2{Ve, Ye};
-			return;
-		}
-#endif
 		if (qn + (uint32_t)__builtin_popcountll(__ballot(os)) > 64) store_queue();
 		push(os, 2 * (q0 + lane), Vs, Ys);
 		if (qn + (uint32_t)__builtin_popcountll(__ballot(oe)) > 64) store_queue();
@@ -590,11 +585,7 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		uint32_t Z[kXU];
 #pragma unroll
 		for (uint32_t j = 0; j < kXU; ++j) {
-#ifdef FDBX_NOMUL
-			Z[j] = X;
-#else
 			Z[j] = mulM(X);
-#endif
 			if (k + j < kend) X = Z[j] ^ rdlane(H[j], 63);
 		}
 #pragma unroll
@@ -690,8 +681,16 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			q = qnx;
 			if (gB < nd) prefetch(q);  // the next grab's window, consumed a step later
 			gA = gB;
+#ifdef FDBX_STEAL
+			{
+				const uint32_t gn = g0 + 2 * wpb + rdlane(req, 0);
+				gB = gn < g1 ? gn : steal();
+				if (gn < g1) req = request();
+			}
+#else
 			gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
 			req = request();
+#endif
 			s = 0;
 		} else {
 			++s;
@@ -708,10 +707,12 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		g_xt[w][3] = g1 - g0;
 	}
 #endif
+#ifndef FDBX_STEAL
 	// every request of every wave has returned: the counter goes back to zero
 	__builtin_amdgcn_s_waitcnt(0);
 	__syncthreads();
 	if (threadIdx.x == 0) *my_ctr = 0;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -866,6 +867,11 @@ __device__ void x_fallback(const XParams& P, const uint32_t* s4) {
 __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	__shared__ uint32_t lds[kFinWords];
 	const bool packed = x_packed(P);
+#ifdef FDBX_STEAL
+	// k_xgrab's counters (stolen from, so not reset by their own workgroups)
+	if (P.grabs && blockIdx.x == 0)
+		for (uint32_t k = threadIdx.x; k < (uint32_t)(P.nwave / 16); k += blockDim.x) P.ctr[kPageCtrWords * k] = 0;
+#endif
 	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat)  // for the stream's next route choice
 		P.hstat[kHstatXfail] = x_unordered(P) ? kXfailBackoff : 0;
 	const DevTables* T = P.tabs;
@@ -887,9 +893,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	const uint32_t lgp = P.grabs ? x_log2(per) : 64u;  // grabs: a power of two
 	const uint32_t* const agg = P.grabs ? P.x.gagg : P.x.ragg;
 	const uint32_t* s4 = lds + kFinS4;
-#ifndef FDBX_NOFILL
 	fin_fill(lds, T);
-#endif
 	// nibble tables of C = M^per (the unit stride), for the straddling
 	// buffers' aggregate chains: entry [n][v] = (v x^4n) * C, bit by bit --
 	// except for grabs of fewer than 64 blocks, whose M^gsz is one of the
@@ -988,15 +992,6 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		return ~(re ^ rs);
 	};
 	const uint64_t span = (uint64_t)gridDim.x * blockDim.x;
-#ifdef FDBX_FIN1
-	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += span) {
-		In A;
-		load_in(A, i0 + threadIdx.x);
-		const uint32_t ra = finish(A);
-		if (A.ok) P.out[i0 + threadIdx.x] = ra;
-	}
-	return;
-#endif
 	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += 2 * span) {
 		In A, B;
 		load_in(A, i0 + threadIdx.x);
@@ -1057,11 +1052,7 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 			k_xstream<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
 	} else {
 		// persistent, but no more workgroups than the buffers fill (each fills 133 KiB of LDS)
-#ifdef FDBX_FIN1
-		const uint64_t g = (count + kFinThreads - 1) / kFinThreads;
-#else
 		const uint64_t g = (count + 2 * kFinThreads - 1) / (2 * kFinThreads);  // (two buffers per thread per pass)
-#endif
 		k_xfin<<<(unsigned)(g < (uint64_t)num_cus ? g : (uint64_t)num_cus), kFinThreads, 0, stream>>>(P);
 	}
 	return 0;

@@ -973,6 +973,97 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 		}
 	};
 
+	// ---- sparse ranges: a wave whose range is one pool holding at most two
+	// row buffers (the chunks batch: its 4-16 KiB chunks beside the long
+	// route, about one per wave) spreads each buffer's blocks over its four
+	// rows -- block b on row b % 4 -- and chains the rows' stripe sums in
+	// block order (the decomposition of xxh3_split.hip): a 16 KiB buffer is
+	// four steps, not sixteen.
+	auto split_one = [&](uint64_t len, uint64_t off, uint64_t sd, uint64_t idx) __attribute__((always_inline)) {
+		const uint64_t p = base + off;
+		const uint32_t nb = (uint32_t)((len - 1) >> 10) + 1, nfull = nb - 1;
+		const uint32_t ns = (uint32_t)(((len - 1) - ((uint64_t)nfull << 10)) >> 6);
+		const uint32_t nsteps = (nb + 3) / 4;
+		if (SEEDS) K = row_keys(lane, sd);
+		auto ld = [&](uint64_t (&v)[4][2], uint32_t t) __attribute__((always_inline)) {
+			uint32_t b = 4 * t + (uint32_t)r;
+			b = b < nb ? b : nfull;  // (a row past the end re-reads the final block: discarded)
+			const bool fin = b == nfull;
+#pragma unroll
+			for (int i = 0; i < 4; ++i) {
+				const uint32_t st = g + 4 * i;
+				const bool tail = fin && (st == 15 || st >= ns);
+				const uint64_t a = tail ? p + len - 64 + 16 * k : p + ((uint64_t)b << 10) + 64 * st + 16 * k;
+				const u64x2u x = __builtin_nontemporal_load((g_u64x2u*)a);
+				v[i][0] = x[0];
+				v[i][1] = x[1];
+			}
+		};
+		uint64_t s0 = k == 0 ? P32_3 : (k == 1 ? P64_2 : (k == 2 ? P64_4 : P64_5));
+		uint64_t s1 = k == 0 ? P64_1 : (k == 1 ? P64_3 : (k == 2 ? P32_2 : P32_1));
+		uint64_t va[4][2], vb[4][2];
+		ld(va, 0);
+		for (uint32_t t = 0; t < nsteps; ++t) {
+			if (t + 1 < nsteps) ld(vb, t + 1);
+			uint32_t b = 4 * t + (uint32_t)r;
+			const bool fin = b == nfull;
+			uint64_t d0 = 0, d1 = 0;
+#pragma unroll
+			for (int i = 0; i < 4; ++i) {
+				const uint32_t st = g + 4 * i;
+				const bool last = fin && st == 15;
+				const bool on = !fin || st < ns || last;
+				const uint64_t x0 = va[i][0] ^ (last ? K.l0 : K.k0[i]);
+				const uint64_t x1 = va[i][1] ^ (last ? K.l1 : K.k1[i]);
+				d0 += on ? va[i][1] + (uint64_t)(uint32_t)x0 * (x0 >> 32) : 0;
+				d1 += on ? va[i][0] + (uint64_t)(uint32_t)x1 * (x1 >> 32) : 0;
+			}
+			uint32_t lo0 = (uint32_t)d0, hi0 = (uint32_t)(d0 >> 32), lo1 = (uint32_t)d1, hi1 = (uint32_t)(d1 >> 32);
+			add_dpp<0x124>(lo0, hi0);
+			add_dpp<0x124>(lo1, hi1);
+			add_dpp<0x128>(lo0, hi0);
+			add_dpp<0x128>(lo1, hi1);
+			d0 = ((uint64_t)hi0 << 32) | lo0;
+			d1 = ((uint64_t)hi1 << 32) | lo1;
+			// the four rows' sums in block order, in every lane of pair k
+#pragma unroll
+			for (int rr = 0; rr < 4; ++rr) {
+				const uint32_t bb = 4 * t + rr;
+				if (bb >= nb) break;  // (uniform)
+				const int a = (16 * rr + k) << 2;
+				s0 += bpermute64(a, d0);
+				s1 += bpermute64(a, d1);
+				if (bb < nfull) {
+					s0 = ((s0 ^ (s0 >> 47)) ^ K.c0) * P32_1;
+					s1 = ((s1 ^ (s1 >> 47)) ^ K.c1) * P32_1;
+				}
+			}
+#pragma unroll
+			for (int i = 0; i < 4; ++i) {
+				va[i][0] = vb[i][0];
+				va[i][1] = vb[i][1];
+			}
+		}
+		const uint64_t m = mulfold(s0 ^ K.g0, s1 ^ K.g1);
+		uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+		add_dpp<0xB1>(lo, hi);
+		add_dpp<0x4E>(lo, hi);
+		const uint64_t h = xxh3_aval(len * P64_1 + (((uint64_t)hi << 32) | lo));
+		if (lane == 0) out[idx] = h;
+	};
+	if (end - begin <= 64) {
+		issue_b();
+		if (take_b() && na <= 2) {
+			for (uint32_t j = 0; j < na; ++j) {
+				const int a = (int)(j << 2);
+				split_one(bpermute64(a, alen), bpermute64(a, aoff), SEEDS ? bpermute64(a, aseed) : seed0,
+				          begin + (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)aj));
+			}
+			ac = na;
+		}
+		if (SEEDS) K = row_keys(lane, seed0);
+	}
+
 	// Two steps per half-iteration, the other half's two steps in flight; the
 	// halves alternate register sets (no copies of data in flight).
 	// s0/s1 start as idle steps (nothing loaded), so no data load precedes the
@@ -1118,7 +1209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // ---------------------------------------------------------------------------
 // Varlen planning: whole buffers per wave, balanced by bytes.  Wave w takes
 // the buffers whose start lies in [w*Q, (w+1)*Q) of the concatenated stream
-// (cost = length + 64).  With room for the long-buffer route in the
+// (cost = length + 64 on the rows, kXTailCost for a short or quad buffer).  With room for the long-buffer route in the
 // workspace, the buffers longer than kXSplitMin take it (xxh3_split.hip) if
 // their entries fit the room (else the row kernel takes the whole batch).
 // No counters to reset: k_xplan writes per-tile sums, k_xscan scans them (the
@@ -1153,11 +1244,12 @@ constexpr uint64_t kTileRouted = 1ull << 63;
 // The row kernel's waves as placed on the CUs: with two workgroups per CU the
 // first-dispatched one's waves are older and win the SIMD's issue arbitration,
 // and stream the same bytes ~19 % sooner (zipf, per-wave timestamps: 142 vs
-// 169 us median).  Their ranges are longer by that ratio (kXOlderW / 16), so
-// both generations end together.  B(w) = w * qa for the `older` first waves,
+// 169 us median).  Their ranges are longer by about that ratio (kXOlderW /
+// 16: 21/16 measured a little faster end to end than 17/16, 19/16 or 23/16),
+// so both generations end together.  B(w) = w * qa for the `older` first waves,
 // then qb per wave.
 #ifndef FDBXXH_OLDER16
-#define FDBXXH_OLDER16 19
+#define FDBXXH_OLDER16 21
 #endif
 constexpr uint64_t kXOlderW = FDBXXH_OLDER16;
 struct XQuant {
@@ -1184,7 +1276,17 @@ __device__ __forceinline__ uint64_t xquant_wave(const XQuant& W, uint64_t x) {
 __device__ __forceinline__ uint64_t xp_len(const XPlanP& Q, uint64_t i) { return Q.lengths ? Q.lengths[i] : Q.length; }
 __device__ __forceinline__ uint64_t xp_off(const XPlanP& Q, uint64_t i) { return Q.offsets ? Q.offsets[i] : i * Q.stride; }
 __device__ __forceinline__ uint64_t xp_blocks(uint64_t len) { return ((len - 1) >> 10) + 1; }
-__device__ __forceinline__ uint64_t xp_cost(uint64_t len, bool routed) { return routed ? 64 : len + 64; }
+// A wave's cost of a buffer, in bytes of row streaming: its bytes + 64 on the
+// rows, a flat kXTailCost for the short and quad ones (<= kXQuadMax: their
+// part is a chain of memory round trips, ~0.24 us of the wave's time each on
+// zipf against 0.29 us per row KiB), 64 on the long route.
+#ifndef FDBXXH_TAIL_COST
+#define FDBXXH_TAIL_COST 896
+#endif
+constexpr uint64_t kXTailCost = FDBXXH_TAIL_COST;
+__device__ __forceinline__ uint64_t xp_cost(uint64_t len, bool routed) {
+	return routed ? 64 : (len <= kXQuadMax ? kXTailCost : len + 64);
+}
 // a long buffer (its blocks count in the stream's need whether or not there is room)
 __device__ __forceinline__ bool xp_long(uint64_t len) { return len > kXSplitMin; }
 // Size class of a long buffer: 0 for 2^19 blocks (512 MiB) or more, then one
@@ -1228,7 +1330,7 @@ __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
 	const bool lg = i < Q.count && xp_long(len);
 	const uint64_t nb = lg ? xp_blocks(len) : 0;
 	const uint32_t cl = lg ? xp_class(nb) : 0;
-	uint64_t v[8] = {i < Q.count ? xp_cost(len, lg) : 0, i < Q.count ? len + 64 : 0, nb, 0, 0, 0, 0, 0};
+	uint64_t v[8] = {i < Q.count ? xp_cost(len, lg) : 0, i < Q.count ? xp_cost(len, false) : 0, nb, 0, 0, 0, 0, 0};
 	if (lg) v[4 + (cl >> 2)] = 1ull << (16 * (cl & 3));
 #pragma unroll
 	for (int q = 0; q < 8; ++q) v[q] = rdlane63(dpp_incl64(v[q]));

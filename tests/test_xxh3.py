@@ -213,6 +213,31 @@ def test_gpu_varlen_configs_exact_batches(xg, cuda, name):
 
 
 @pytest.mark.gpu
+def test_gpu_varlen_sparse_ranges_split_over_rows(cuda):
+    """Batches with about one row buffer per wave (k_xxh3_vrows spreads such a
+    buffer's blocks over the wave's four rows and chains them in order):
+    every length class around the block edges, unaligned offsets, uniform and
+    per-buffer seeds, against the oracle."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    rng = np.random.default_rng(41)
+    h = sm_bytes(1 << 23, 0x5A5A)
+    d = dev_bytes(h, cuda)
+    edges = [1025, 1087, 1088, 2047, 2048, 2049, 3072, 4095, 4096, 4097, 8191, 8192, 15360, 16383, 16384]
+    for n in (1, 3, 100, 1500):
+        lens = np.array([edges[i % len(edges)] if i % 3 else int(rng.integers(1025, 16385)) for i in range(n)],
+                        dtype=np.int64)
+        if n == 1500:  # mixed with short and quad ones, as in the chunks batch's waves
+            lens[::5] = rng.integers(0, 1025, lens[::5].size)
+        offs = rng.integers(0, h.size - 16384, n).astype(np.int64)
+        seeds = rng.integers(0, 2 ** 63, n, dtype=np.int64)
+        got = host(X.batch_varlen(d, i64(offs, cuda), i64(lens, cuda), seed=0xFDBEEFDB))
+        assert np.array_equal(got, O.xxh3_batch_varlen(h, offs, lens, seed=0xFDBEEFDB)), n
+        got = host(X.batch_varlen(d, i64(offs, cuda), i64(lens, cuda), seeds=torch.tensor(seeds, device=cuda)))
+        assert np.array_equal(got, O.xxh3_batch_varlen(h, offs, lens, seeds=seeds.view(np.uint64))), n
+
+
+@pytest.mark.gpu
 def test_gpu_empty_and_workspace(cuda):
     import torch
     import foundationdb_amd.xxh3 as X

@@ -1,12 +1,20 @@
 """CPU model of the XXH3 varlen planner (k_xplan / k_xscan / k_xassign in
 foundationdb_amd/csrc/xxh3_kernels.hip): every wave w must get as its first
 buffer the first buffer whose start (in cost units, length + 64 per buffer)
-is >= B(w), and the last entry must be `count`.  B(w) = w * qa for the
+is >= B(w), and the last entry must be `count`; a buffer's cost is its
+length + 64, or a flat 896 for one of at most 1 KiB (xp_cost).  B(w) = w * qa for the
 `older` first waves (the first-dispatched workgroups'), then qb per wave, qa
-= qb * 19 / 16 (xquant); older = 0 is the uniform split."""
+= qb * 21 / 16 (xquant); older = 0 is the uniform split."""
 import numpy as np
 
-OLDER_W = 19  # kXOlderW (sixteenths)
+OLDER_W = 21  # kXOlderW (sixteenths)
+TAIL_COST, QUAD_MAX = 896, 1024  # kXTailCost, kXQuadMax
+
+
+def xp_cost(lengths):
+    """Row buffers: length + 64; short and quad ones (<= 1 KiB): a flat TAIL_COST."""
+    lengths = lengths.astype(np.uint64)
+    return np.where(lengths <= QUAD_MAX, np.uint64(TAIL_COST), lengths + np.uint64(64)).astype(np.uint64)
 
 
 def xquant(total, nwave, older):
@@ -29,7 +37,7 @@ def boundary(W, w):
 
 
 def plan(lengths, nwave, older=0):
-    cost = lengths.astype(np.uint64) + 64
+    cost = xp_cost(lengths)
     start = np.concatenate([[0], np.cumsum(cost)[:-1]]).astype(np.uint64)
     total = int(cost.sum())
     W = xquant(total, nwave, older)
@@ -37,7 +45,7 @@ def plan(lengths, nwave, older=0):
     n = lengths.size
     for i in range(n):  # one thread per buffer, as in k_xassign
         s = int(start[i])
-        prev = 0 if i == 0 else s - int(lengths[i - 1] + 64)
+        prev = 0 if i == 0 else s - int(cost[i - 1])
         w_lo = 0 if i == 0 else xquant_wave(W, prev) + 1
         w_hi = xquant_wave(W, s)
         for w in range(w_lo, min(w_hi, nwave - 1) + 1):
@@ -79,13 +87,13 @@ def test_planner_covers_every_wave():
 
 
 def test_older_waves_get_longer_ranges():
-    """With two workgroup generations the first half of the waves gets 19/16
+    """With two workgroup generations the first half of the waves gets 21/16
     of the second half's cost each (so both end together on the GPU)."""
     lens = np.full(200000, 5000)
     wf, start, W = plan(lens, 2048, 1024)
     per = np.diff(wf)[:-1]
     a, b = per[:1024].mean(), per[1024:2047].mean()
-    assert abs(a / b - 19 / 16) < 0.02
+    assert abs(a / b - 21 / 16) < 0.02
 
 
 # ---- long-buffer route (k_xplan / k_xscan / k_xassign, then k_xlong's order)
@@ -137,5 +145,5 @@ def test_long_route_entries_by_size_class():
         else:
             assert order == [] and (cost == lens + 64).all()
         # the row kernel's waves still cover every buffer (the cost model above)
-        wf, start, W = plan(cost - 64, 64)
+        wf, start, W = plan(np.where(cost == 64, 0, cost - 64), 64)
         assert (wf >= 0).all() and wf[-1] == n
