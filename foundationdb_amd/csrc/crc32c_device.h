@@ -79,8 +79,6 @@ constexpr int kHstatNblk = 3, kHstatPacked = 4, kHstatXfail = 5;
 // kXfailBackoff batches that look packed still take the window engine (each
 // window/block-route batch counts the word down), then the route is tried again.
 constexpr uint64_t kXfailBackoff = 16;
-// k_xgrab (FDBX_STEAL): other workgroups' counters tried once the own range is taken
-constexpr uint32_t kXStealTries = 4;
 inline int route_for_stats(const volatile uint64_t* s) {
 	const uint64_t win = s[0], mid = s[1], large = s[2];
 	const bool big = large != 0 && large >= win + mid;  // 16 KiB+ spans hold most bytes: the block route's ground

@@ -409,24 +409,6 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		if (lane == 0) r = atomicAdd(my_ctr, 1u);
 		return r;
 	};
-#ifdef FDBX_STEAL
-	// A workgroup whose own grabs are all taken takes grabs of other
-	// workgroups' ranges from their counters (the CUs do not stream at one
-	// speed).  The counters are then reset by k_xfin, not here.
-	uint32_t sk = 0;
-	auto steal = [&]() -> uint32_t {
-		for (; sk < kXStealTries; ++sk) {
-			const uint32_t v = (blockIdx.x + 8 * (sk + 1)) % gridDim.x;  // (same XCD first)
-			const uint32_t v0 = v * gper < nd ? v * gper : nd;
-			const uint32_t v1 = v0 + gper < nd ? v0 + gper : nd;
-			uint32_t r = 0;
-			if (lane == 0) r = atomicAdd(P.ctr + kPageCtrWords * v, 1u);
-			const uint32_t g = v0 + 2 * wpb + rdlane(r, 0);
-			if (g < v1) return g;
-		}
-		return nd;
-	};
-#endif
 	auto blk_ptr = [&](uint32_t k) { return reinterpret_cast<const uint8_t*>(G.S + 4096ull * k); };
 	// a dynamic step's blocks (a step past the wave's grabs re-reads block 0: discarded)
 	auto load_step_unit = [&](Block (&u)[kXU], uint32_t g, uint32_t s, uint32_t half) {
@@ -681,16 +663,8 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			q = qnx;
 			if (gB < nd) prefetch(q);  // the next grab's window, consumed a step later
 			gA = gB;
-#ifdef FDBX_STEAL
-			{
-				const uint32_t gn = g0 + 2 * wpb + rdlane(req, 0);
-				gB = gn < g1 ? gn : steal();
-				if (gn < g1) req = request();
-			}
-#else
 			gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
 			req = request();
-#endif
 			s = 0;
 		} else {
 			++s;
@@ -707,12 +681,10 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		g_xt[w][3] = g1 - g0;
 	}
 #endif
-#ifndef FDBX_STEAL
 	// every request of every wave has returned: the counter goes back to zero
 	__builtin_amdgcn_s_waitcnt(0);
 	__syncthreads();
 	if (threadIdx.x == 0) *my_ctr = 0;
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -867,11 +839,6 @@ __device__ void x_fallback(const XParams& P, const uint32_t* s4) {
 __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	__shared__ uint32_t lds[kFinWords];
 	const bool packed = x_packed(P);
-#ifdef FDBX_STEAL
-	// k_xgrab's counters (stolen from, so not reset by their own workgroups)
-	if (P.grabs && blockIdx.x == 0)
-		for (uint32_t k = threadIdx.x; k < (uint32_t)(P.nwave / 16); k += blockDim.x) P.ctr[kPageCtrWords * k] = 0;
-#endif
 	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat)  // for the stream's next route choice
 		P.hstat[kHstatXfail] = x_unordered(P) ? kXfailBackoff : 0;
 	const DevTables* T = P.tabs;

@@ -293,8 +293,15 @@ __device__ __forceinline__ void chunk_slot(uint32_t o, uint32_t& ln, uint32_t& r
 	ln = 32 * ((o >> 4) & 1) + 16 * ((o >> 5) & 1) + ((o >> 6) & 15);
 	ri = ((o >> 11) & 1) | (((o >> 10) & 1) << 1);
 }
+#ifdef FDBCRC_BTIMES
+// development: per-wave start / end timestamps of k_bigblocks (s_memrealtime, 100 MHz)
+__device__ uint64_t g_bt[16384][4];
+#endif
 template <int U>
 __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
+#ifdef FDBCRC_BTIMES
+	const uint64_t bt0 = __builtin_amdgcn_s_memrealtime();
+#endif
 	typedef __attribute__((address_space(1))) const uint64_t g_u64;
 	typedef __attribute__((address_space(1))) const uint32_t g_u32;
 	auto gl32 = [](const uint32_t* p) -> uint32_t { return *((g_u32*)reinterpret_cast<uintptr_t>(p)); };
@@ -587,6 +594,15 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		step(MB, MA);
 	}
 	if (f) store();
+#ifdef FDBCRC_BTIMES
+	if (lane == 0) {
+		const uint32_t w = blockIdx.x * wpb + wi;
+		g_bt[w][0] = bt0;
+		g_bt[w][1] = __builtin_amdgcn_s_memrealtime();
+		g_bt[w][2] = g1 - g0;
+		g_bt[w][3] = ngrab;
+	}
+#endif
 	// every request of every wave has returned: the counter goes back to zero
 	__builtin_amdgcn_s_waitcnt(0);
 	__syncthreads();
@@ -684,3 +700,9 @@ int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint
 }
 
 }  // namespace fdbcrc
+
+#ifdef FDBCRC_BTIMES
+extern "C" int fdbcrc_debug_btimes(void* host, uint64_t nwave) {
+	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbcrc::g_bt), nwave * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif
