@@ -99,7 +99,10 @@ constexpr uint64_t kXMaxExtent = 1ull << 40;  // 32-bit block numbers with room
 // Grabs of the dynamic stream kernel (k_xgrab): kXGrabMin blocks, more when the
 // extent has more than capg grabs of that size, so the per-grab arrays never
 // overflow whatever the extent.
-constexpr uint64_t kXGrabMin = 8;
+#ifndef FDBX_GRAB_MIN
+#define FDBX_GRAB_MIN 8
+#endif
+constexpr uint64_t kXGrabMin = FDBX_GRAB_MIN;
 // (a power of two: grab numbers are shifts, not 64-bit divisions)
 __host__ __device__ inline uint64_t x_gsz(uint64_t nblk, uint64_t capg) {
 	uint64_t gsz = kXGrabMin;

@@ -13,12 +13,11 @@
 //
 // Here the length walk and the hashing are separated, so the hashing is
 // balanced over the whole GPU instead of one buffer per thread:
-//   k_pkt_walk    one wave per receive buffer walks its frame headers -- a
+//   k_pkt_walk    one lane per receive buffer walks its frame headers -- a
 //                 serial chain, each header's length locating the next --
-//                 from windows of the buffer staged in LDS by coalesced loads
-//                 (one restage per window, not one HBM round trip per frame),
+//                 reading the header bytes only (a 64-byte register window),
 //                 and appends every complete, well-sized frame to a frame list
-//                 (64 at a time: one atomic per group of frames)
+//                 (one atomic per step of a wave)
 //   XXH3 varlen   the frame payloads through the XXH3 engine
 //                 (xxh3_kernels.hip / xxh3_split.hip), batch size read on the
 //                 device from the walk's frame counter
@@ -47,9 +46,6 @@ __device__ __forceinline__ uint64_t rdfirst64(uint64_t v) {
 	return ((uint64_t)rdfirst((uint32_t)(v >> 32)) << 32) | (uint64_t)rdfirst((uint32_t)v);
 }
 
-constexpr uint32_t kWalkWaves = 4;                 // buffers per 256-thread workgroup
-constexpr uint32_t kWin = 8192;                    // bytes of a buffer staged per window
-constexpr uint32_t kWinWords = kWin / 4 + 4;       // + slack: an unaligned word read past the window's last byte
 
 }  // namespace
 
@@ -63,94 +59,105 @@ struct WalkP {
 	Ws w;
 };
 
-// One wave per receive buffer.  Every lane runs the same walk (the header
-// words are LDS broadcasts), so control flow is uniform; a group of up to 64
-// frames collects in the lanes (lane j: frame j of the group) and leaves with
-// one atomic reservation.
+// One LANE per receive buffer: each lane walks its buffer's frame headers --
+// a serial chain, each header's length locating the next -- with loads of the
+// header bytes only, through a 64-byte window held in its registers (a header
+// inside the window costs no load: runs of small frames share lines).  The
+// first design staged every buffer whole in LDS (one wave per buffer), which
+// read the batch's bytes a second time: the walk was HBM-bound (257 us on the
+// bench's 1 GiB of Zipf packets).  Per step of the walk, the wave's frames
+// are reserved in the frame list with one atomic.
 __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
-	__shared__ uint32_t win[kWalkWaves][kWinWords];
-	const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-	const uint64_t b = (uint64_t)blockIdx.x * kWalkWaves + wv;
-	if (b >= P.nbuf) return;  // (uniform per wave; no workgroup barrier below)
-	uint32_t* const L = win[wv];
-	const uint64_t B0 = rdfirst64(reinterpret_cast<uint64_t>(P.base) + *((g_u64*)reinterpret_cast<uintptr_t>(P.boff + b)));
-	const uint64_t len = rdfirst64(*((g_u64*)reinterpret_cast<uintptr_t>(P.blen + b)));
+	const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t lane = threadIdx.x & 63;
+	const bool in = b < P.nbuf;
+	const uint64_t B0 = in ? reinterpret_cast<uint64_t>(P.base) + *((g_u64*)reinterpret_cast<uintptr_t>(P.boff + b)) : 0;
+	const uint64_t len = in ? *((g_u64*)reinterpret_cast<uintptr_t>(P.blen + b)) : 0;
 	const uint64_t E = B0 + len;
-	const uint64_t last_chunk = (E - 1) & ~uint64_t(15);  // (len > 0 wherever a window is staged)
-	uint64_t wbeg = ~uint64_t(0);  // window: bytes [wbeg, wbeg + kWin), wbeg 16-byte aligned
+	const uint64_t last_chunk = len ? (E - 1) & ~uint64_t(15) : 0;
+	uint64_t wbeg = ~uint64_t(0);  // window: bytes [wbeg, wbeg + 64), wbeg 16-byte aligned
+	u32x4 win[4];
 	auto restage = [&](uint64_t a) {
 		wbeg = a & ~uint64_t(15);
 #pragma unroll
-		for (uint32_t i = 0; i < kWin / 1024; ++i) {
-			const uint64_t c = wbeg + 16ull * (lane + 64 * i);
+		for (int i = 0; i < 4; ++i) {
 			// chunks past the buffer re-read its last one (never used: the walk
 			// checks every length against the buffer's end)
-			const u32x4 v = *((g_u32x4*)reinterpret_cast<uintptr_t>(c <= last_chunk ? c : last_chunk));
-			*reinterpret_cast<u32x4*>(L + 4 * (lane + 64 * i)) = v;
+			const uint64_t c = wbeg + 16ull * i;
+			win[i] = *((g_u32x4*)reinterpret_cast<uintptr_t>(c <= last_chunk ? c : last_chunk));
 		}
-		__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's LDS writes are done before its reads
-		__builtin_amdgcn_wave_barrier();
 	};
-	// little-endian u32 at absolute address a inside the window
+	// little-endian u32 at absolute address a inside the window (a - wbeg <= 60)
 	auto rd32 = [&](uint64_t a) -> uint32_t {
-		const uint32_t o = (uint32_t)(a - wbeg);
-		const uint32_t w0 = L[o >> 2], w1 = L[(o >> 2) + 1];
+		const uint32_t o = (uint32_t)(a - wbeg), wi = o >> 2;
+		uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 16; ++k) {
+			const uint32_t v = win[k >> 2][k & 3];
+			w0 = wi == k ? v : w0;
+			w1 = wi + 1 == k ? v : w1;
+		}
 		return __builtin_amdgcn_alignbyte(w1, w0, o & 3u);
 	};
-	uint64_t p = 0;     // bytes of the buffer walked
-	uint32_t ord = 0;   // frames walked
+	uint64_t p = 0;    // bytes of the buffer walked
+	uint32_t ord = 0;  // frames walked
 	int32_t status = FDB_PACKET_OK;
-	// the group of frames not yet written out
-	uint32_t pend = 0;
-	uint64_t g_off = 0, g_len = 0, g_exp = 0;
-	uint32_t g_ord = 0;
+	bool live = in, overflow = false;
 	uint64_t* const fcount = P.w.hdr;
-	bool overflow = false;
-	auto flush = [&]() {
-		if (pend == 0) return;
-		uint64_t at = 0;
-		if (lane == 0) at = atomicAdd((unsigned long long*)fcount, (unsigned long long)pend);
-		at = rdfirst64(at);  // (every lane is active: lane 0's reservation)
-		const uint64_t f = at + lane;
-		if (lane < pend && f < P.w.cap) {
-			P.w.foff[f] = g_off;
-			P.w.flen[f] = g_len;
-			P.w.fexp[f] = g_exp;
-			P.w.fbuf[f] = (uint32_t)b;
-			P.w.ford[f] = g_ord;
+	while (__ballot(live) != 0) {
+		bool frame = false;
+		uint32_t fl = 0;
+		uint64_t ck = 0, a = 0;
+		if (live) {
+			a = B0 + p;
+			if (len - p < 4) {                                   // FlowTransport.cpp:1285-1286
+				live = false;
+			} else if (P.hdr == 12 && len - p - 4 < 8) {         // :1293-1294
+				live = false;
+			} else {
+				if (a < wbeg || a + P.hdr > wbeg + 64) restage(a);
+				fl = rd32(a);
+				if (fl > P.limit) {                                // :1299-1304 (before the frame is complete)
+					status = FDB_PACKET_LIMIT_EXCEEDED;
+					live = false;
+				} else if (len - p - P.hdr < fl) {                 // :1306-1307
+					live = false;
+				} else if (fl < 16) {                              // :1309-1319 (sizeof(UID))
+					status = FDB_PACKET_TOO_SMALL;
+					live = false;
+				} else {
+					if (P.hdr == 12) ck = ((uint64_t)rd32(a + 8) << 32) | rd32(a + 4);
+					frame = true;
+				}
+			}
 		}
-		if (at + pend > P.w.cap) overflow = true;
-		pend = 0;
-	};
-	for (;;) {
-		if (len - p < 4) break;                              // FlowTransport.cpp:1285-1286
-		if (P.hdr == 12 && len - p - 4 < 8) break;           // :1293-1294
-		const uint64_t a = B0 + p;
-		if (a < wbeg || a + P.hdr > wbeg + kWin) restage(a);
-		const uint32_t fl = rdfirst(rd32(a));
-		if (fl > P.limit) {                                  // :1299-1304 (before the frame is complete)
-			status = FDB_PACKET_LIMIT_EXCEEDED;
-			break;
+		// this step's frames: one reservation for the wave (reserving a step
+		// ahead, so that the atomic's return is off the walk's chain, measured
+		// the same: the header loads are the chain)
+		const uint64_t m = __ballot(frame);
+		if (m != 0) {
+			const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+			uint64_t at = 0;
+			if (lane == lead) at = atomicAdd((unsigned long long*)fcount, (unsigned long long)__builtin_popcountll(m));
+			at = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), (int)lead) << 32) |
+			     (uint64_t)(uint32_t)__shfl((int)(uint32_t)at, (int)lead);
+			if (frame) {
+				const uint64_t f = at + (uint64_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+				if (f < P.w.cap) {
+					P.w.foff[f] = a + P.hdr - reinterpret_cast<uint64_t>(P.base);
+					P.w.flen[f] = fl;
+					P.w.fexp[f] = ck;
+					P.w.fbuf[f] = (uint32_t)b;
+					P.w.ford[f] = ord;
+				} else {
+					overflow = true;
+				}
+				p += P.hdr + fl;
+				++ord;
+			}
 		}
-		if (len - p - P.hdr < fl) break;                     // :1306-1307
-		if (fl < 16) {                                       // :1309-1319 (sizeof(UID))
-			status = FDB_PACKET_TOO_SMALL;
-			break;
-		}
-		uint64_t ck = 0;
-		if (P.hdr == 12) ck = ((uint64_t)rdfirst(rd32(a + 8)) << 32) | rdfirst(rd32(a + 4));
-		if (lane == pend) {
-			g_off = a + P.hdr - reinterpret_cast<uint64_t>(P.base);
-			g_len = fl;
-			g_exp = ck;
-			g_ord = ord;
-		}
-		if (++pend == 64) flush();
-		p += P.hdr + fl;
-		++ord;
 	}
-	flush();
-	if (lane == 0) {
+	if (in) {
 		P.w.walked[b] = ord;
 		P.w.wstat[b] = overflow ? FDB_PACKET_ECAPACITY : status;
 		P.w.wend[b] = p;
@@ -270,7 +277,7 @@ int launch_verify(const uint8_t* base, const uint64_t* boff, const uint64_t* ble
 	W.hdr = checksum ? 12u : 4u;
 	W.limit = limit;
 	W.w = w;
-	k_pkt_walk<<<(unsigned)((nbuf + kWalkWaves - 1) / kWalkWaves), 64 * kWalkWaves, 0, s>>>(W);
+	k_pkt_walk<<<(unsigned)((nbuf + 255) / 256), 256, 0, s>>>(W);
 	CheckP C{};
 	C.base = base;
 	C.boff = boff;
