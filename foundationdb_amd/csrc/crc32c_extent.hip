@@ -775,8 +775,8 @@ __device__ __forceinline__ uint32_t xpow8_any(const DevTables* T, uint64_t n) {
 // The batch failed the packing check (k_v7count): every buffer is
 // checksummed directly -- crc32c_append's register loop
 // (contrib/crc32/crc32c.cpp:346-356) with 4-byte slicing from LDS, 16-byte
-// loads -- and the stream's next batches take the window engine
-// (kHstatXfail).  Buffers under 4 KiB: one lane each.  Longer ones: one wave
+// loads -- and the stream's next kXfailBackoff (16) batches take the window
+// engine (kHstatXfail counts them down; then the extent route is tried again).  Buffers under 4 KiB: one lane each.  Longer ones: one wave
 // each, the 64 lanes on 64 equal parts aligned to the buffer's END (parts
 // before the buffer's start are empty -- leading zeros are free -- and the
 // lane whose part holds P0 starts from ~seed there), joined by a 6-level tree
