@@ -30,7 +30,10 @@ constexpr unsigned kWavesPerBlock = 4;
 // output in the workspace:
 constexpr uint64_t kXSplitMin = 16384;
 // varlen buffers of 241 B .. kXQuadMax go to lane quads, longer ones to the rows
-constexpr uint64_t kXQuadMax = 1024;
+#ifndef FDBXXH_QUAD_MAX
+#define FDBXXH_QUAD_MAX 1024
+#endif
+constexpr uint64_t kXQuadMax = FDBXXH_QUAD_MAX;
 struct XEnt {       // one long buffer
 	uint64_t p;     // its address
 	uint64_t len, seed, idx;
