@@ -1279,10 +1279,10 @@ __device__ __forceinline__ uint64_t xp_blocks(uint64_t len) { return ((len - 1) 
 // A wave's cost of a buffer, in bytes of row streaming: its bytes + 64 on the
 // rows, a flat kXTailCost for the short and quad ones (<= kXQuadMax: their
 // part is a chain of memory round trips, ~0.24 us of the wave's time each on
-// zipf against 0.29 us per row KiB; 1024 measured best of 640-1280), 64 on the
-// long route.
+// zipf against 0.29 us per row KiB; 1152-1280 measured best of 640-1280 under
+// the bench protocol), 64 on the long route.
 #ifndef FDBXXH_TAIL_COST
-#define FDBXXH_TAIL_COST 1024
+#define FDBXXH_TAIL_COST 1152
 #endif
 constexpr uint64_t kXTailCost = FDBXXH_TAIL_COST;
 __device__ __forceinline__ uint64_t xp_cost(uint64_t len, bool routed) {

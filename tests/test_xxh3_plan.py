@@ -1,14 +1,14 @@
 """CPU model of the XXH3 varlen planner (k_xplan / k_xscan / k_xassign in
 foundationdb_amd/csrc/xxh3_kernels.hip): every wave w must get as its first
 buffer the first buffer whose start (in cost units) is >= B(w), and the last
-entry must be `count`.  A buffer's cost is its length + 64, or a flat 1024
+entry must be `count`.  A buffer's cost is its length + 64, or a flat 1152
 for one of at most 1 KiB (xp_cost).  B(w) = w * qa for the `older` first
 waves (the first-dispatched workgroups'), then qb per wave, qa = qb * 21 / 16
 (xquant); older = 0 is the uniform split."""
 import numpy as np
 
 OLDER_W = 21  # kXOlderW (sixteenths)
-TAIL_COST, QUAD_MAX = 1024, 1024  # kXTailCost, kXQuadMax
+TAIL_COST, QUAD_MAX = 1152, 1024  # kXTailCost, kXQuadMax
 
 
 def xp_cost(lengths):
