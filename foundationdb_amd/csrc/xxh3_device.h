@@ -19,6 +19,7 @@ struct XxhParams {
 	uint64_t* hneed;             // varlen: host-mapped word for the blocks the long buffers needed (may be null)
 	const uint8_t* lflag;        // (set by launch_xxh3) per buffer: the split route took it (not the row kernel's)
 	uint32_t* err;               // stream's host-mapped status word (may be null): kErrXxhStall if a long-route wait ran out
+	uint32_t ngen;               // (set by the launcher) k_xxh3_rows: workgroups per CU, the dispatch generations
 };
 // Status word values shared with the CRC engine's refusal flag (crc32c_gpu_stream_status).
 constexpr uint32_t kErrRefused = 1, kErrXxhStall = 2;

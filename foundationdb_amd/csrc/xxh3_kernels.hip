@@ -437,6 +437,15 @@ struct RowData {
 
 // A16: base and stride 16-byte aligned (dwordx4 loads), else 8-byte aligned
 // (two dwordx2 loads per 16 B).
+#ifndef FDBXXH_G3W0
+#define FDBXXH_G3W0 42
+#define FDBXXH_G3W1 37
+#endif
+constexpr uint64_t kRowsG3W0 = FDBXXH_G3W0, kRowsG3W1 = FDBXXH_G3W1;  // k_xxh3_rows, three generations (32nds)
+#ifdef FDBXXH_TIMES
+// development: per-wave timestamps of the row kernels (start, rows done, end; s_memrealtime, 100 MHz)
+__device__ uint64_t g_vt[16384][4];
+#endif
 template <bool SEEDS, bool LIST = false, bool A16 = true>
 __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 	if (LIST) P.count = *P.d_count;
@@ -445,10 +454,34 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 	const uint64_t wpb = blockDim.x >> 6;
 	const uint64_t nwave = (uint64_t)gridDim.x * wpb;
 	const uint64_t w = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	uint64_t per = (P.count + nwave - 1) / nwave;
-	per = (per + 3) & ~uint64_t(3);
-	const uint64_t begin = w * per;
-	const uint64_t end = begin + per < P.count ? begin + per : P.count;
+#ifdef FDBXXH_TIMES
+	const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+	// Static page ranges weighted by dispatch generation: with ngen workgroups
+	// per CU, the waves of the first-dispatched ones win the SIMDs' issue
+	// arbitration (per-wave timestamps, 1 Mi 4 KiB pages, three generations:
+	// 573 / 613 / 669 us median for equal ranges), so their ranges are longer
+	// -- 42 : 37 : 32 (633 / 619 / 614 us; 37 : 35 : 32 left 584 / 612 / 642;
+	// two generations: 42 : 32) -- and the generations end together.
+	uint64_t begin, end;
+	if (P.ngen == 2 || P.ngen == 3) {
+		const uint64_t wpg = nwave / P.ngen;
+		const uint64_t gsel = w / wpg;
+		const uint64_t W0 = P.ngen == 3 ? kRowsG3W0 : 42, W1 = P.ngen == 3 ? kRowsG3W1 : 32, W2 = 32;
+		const uint64_t sumW = P.ngen == 3 ? W0 + W1 + W2 : W0 + W1;
+		const uint64_t unit = (P.count * 32 + wpg * sumW - 1) / (wpg * sumW);  // pages per wave at weight 32
+		auto per_of = [&](uint64_t Wg) { return ((unit * Wg + 31) / 32 + 3) & ~uint64_t(3); };
+		const uint64_t p0 = per_of(W0), p1 = per_of(W1), p2 = per_of(W2);
+		const uint64_t pg = gsel == 0 ? p0 : (gsel == 1 ? p1 : p2);
+		const uint64_t start = gsel == 0 ? 0 : (gsel == 1 ? wpg * p0 : wpg * (p0 + p1));
+		begin = start + (w - gsel * wpg) * pg;
+		end = begin + pg < P.count ? begin + pg : P.count;
+	} else {
+		uint64_t per = (P.count + nwave - 1) / nwave;
+		per = (per + 3) & ~uint64_t(3);
+		begin = w * per;
+		end = begin + per < P.count ? begin + per : P.count;
+	}
 	if (begin >= end) return;
 	const uint64_t len = P.length;
 	const uint64_t nfull = (len - 1) >> 10;
@@ -568,6 +601,14 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 		c0 = n0;
 		c1 = n1;
 	}
+#ifdef FDBXXH_TIMES
+	if (lane == 0 && w < 16384) {
+		g_vt[w][0] = rt0;
+		g_vt[w][1] = rt0;
+		g_vt[w][2] = __builtin_amdgcn_s_memrealtime();
+		g_vt[w][3] = end - begin;
+	}
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -751,10 +792,6 @@ struct VStep {
 	bool any;                 // some row has one (uniform)
 };
 
-#ifdef FDBXXH_TIMES
-// development: per-wave timestamps of the row kernel (start, rows done, end; s_memrealtime, 100 MHz)
-__device__ uint64_t g_vt[16384][4];
-#endif
 constexpr int kTailPasses = 4;                    // buffers listed at once: 64 each
 constexpr uint32_t kTailCap = 64 * kTailPasses;  // list entries per wave
 template <bool SEEDS>
@@ -1687,6 +1724,7 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 			return a < 1 ? 1 : a;
 		}();
 		const uint64_t g2 = (uint64_t)num_cus * rows_bpc;
+		P.ngen = (uint32_t)rows_bpc;
 		if (P.seeds && aligned)
 			k_xxh3_rows<true, false, true><<<(unsigned)g2, 256, 0, stream>>>(P);
 		else if (P.seeds)
@@ -1702,15 +1740,17 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 	return 0;
 }
 
-int launch_xxh3_pages_list(const XxhParams& P, int num_cus, hipStream_t stream) {
+int launch_xxh3_pages_list(const XxhParams& P0, int num_cus, hipStream_t stream) {
 	static const int bpc = [] {
 		int a = 0;
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_xxh3_rows<false, true>, 256, 0) != hipSuccess) a = 3;
 		return a < 1 ? 1 : a;
 	}();
 	const unsigned grid = (unsigned)((uint64_t)num_cus * bpc);
-	const bool a16 = ((reinterpret_cast<uint64_t>(P.base) | P.stride) & 15) == 0;
-	if (((reinterpret_cast<uint64_t>(P.base) | P.stride) & 7) != 0 || P.length <= 240) return -1;
+	const bool a16 = ((reinterpret_cast<uint64_t>(P0.base) | P0.stride) & 15) == 0;
+	if (((reinterpret_cast<uint64_t>(P0.base) | P0.stride) & 7) != 0 || P0.length <= 240) return -1;
+	XxhParams P = P0;
+	P.ngen = (uint32_t)bpc;
 	if (a16)
 		k_xxh3_rows<false, true, true><<<grid, 256, 0, stream>>>(P);
 	else
