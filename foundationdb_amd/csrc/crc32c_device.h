@@ -41,6 +41,29 @@ void build_dev_tables(DevTables* t);
 // per workgroup, owned by the launch stream (page kernels on one stream run in
 // order), zero between launches.  Allocated on a stream's first page launch.
 constexpr uint32_t kPageCtrWords = 32;
+
+// Static per-workgroup ranges of k_pages4k weighted by XCD parity: workgroup b
+// runs on XCD b % 8, and per-wave timestamps put the odd XCDs' workgroups ~6 %
+// behind the even ones' on equal ranges (1 Mi pages: 603-612 us on XCDs
+// 0/2/4/6, 641-646 us on 1/3/5/7), so an even workgroup's range is kXcdEvenW /
+// kXcdOddW as long (after: 621-635 us on every XCD; bench 0.686 -> 0.676 ms).
+// The same weighting in k_xgrab and k_bigblocks measured neutral (their grabs
+// are finer), so they keep equal ranges.  [g0, g1) of n items.
+#ifndef FDBCRC_XCD_EVEN_W
+#define FDBCRC_XCD_EVEN_W 33
+#define FDBCRC_XCD_ODD_W 31
+#endif
+constexpr uint64_t kXcdEvenW = FDBCRC_XCD_EVEN_W, kXcdOddW = FDBCRC_XCD_ODD_W;  // (32nds)
+__device__ __forceinline__ void xcd_range(uint64_t n, uint64_t b, uint64_t G, uint64_t& g0, uint64_t& g1) {
+	const uint64_t ne = (G + 1) / 2, no = G / 2;
+	const uint64_t den = ne * kXcdEvenW + no * kXcdOddW;
+	const uint64_t unit = (n * 32 + den - 1) / den;
+	const uint64_t pe = (unit * kXcdEvenW + 31) / 32, po = (unit * kXcdOddW + 31) / 32;
+	const uint64_t s0 = ((b + 1) / 2) * pe + (b / 2) * po;  // the even and odd workgroups before b
+	const uint64_t e0 = s0 + ((b & 1) ? po : pe);
+	g0 = s0 < n ? s0 : n;
+	g1 = e0 < n ? e0 : n;
+}
 int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr);  // crc32c_capi.cpp
 
 int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,

@@ -113,6 +113,10 @@ __device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t
 // i): the seed enters the first half, and at the group store lane 2m
 // combines raw(A)*x^(8*4096) ^ raw(B) with its neighbour (DPP lane swap +
 // one lane-parallel table multiply).
+#ifdef FDBCRC_BTIMES
+// development: per-wave start / end timestamps of k_pages4k and k_bigblocks (s_memrealtime, 100 MHz)
+__device__ uint64_t g_bt[16384][4];
+#endif
 template <int U, bool WINDOW = false, bool LIST = false, bool PAIR = false>
 __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
                                                   uint32_t seed, const uint32_t* __restrict__ seeds,
@@ -125,6 +129,9 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		if (count == 0) return;  // the list is empty: every wave leaves before touching the counters
 	}
 	if (PAIR) count *= 2;  // blocks
+#ifdef FDBCRC_BTIMES
+	const uint64_t pt0 = __builtin_amdgcn_s_memrealtime();
+#endif
 	constexpr uint32_t C = 2 * U;   // pages per grab
 	constexpr uint32_t F = 64 / C;  // grabs per store group
 	static_assert(64 % C == 0, "a store group fills the wave's lanes");
@@ -136,9 +143,9 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 	const uint32_t wpb = blockDim.x >> 6;
 	const uint32_t wi = rdfirst(threadIdx.x >> 6);
 	const uint64_t ngrab = (count + C - 1) / C;
-	const uint64_t per = (ngrab + gridDim.x - 1) / gridDim.x;
-	const uint64_t g0 = (uint64_t)blockIdx.x * per;
-	const uint64_t g1 = g0 + per < ngrab ? g0 + per : ngrab;
+	// per-workgroup grab ranges weighted by XCD parity (xcd_range)
+	uint64_t g0, g1;
+	xcd_range(ngrab, blockIdx.x, gridDim.x, g0, g1);
 	uint32_t* const my_ctr = ctr + kPageCtrWords * blockIdx.x;
 	const uint64_t last = count - 1;
 	// page index -> address, clamped into the batch: clamped duplicates are
@@ -252,6 +259,17 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 	}
 	if (f) store();
 	flush_held();
+#ifdef FDBCRC_BTIMES
+	if (c.lane == 0) {
+		const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+		if (w < 16384) {
+			g_bt[w][0] = pt0;
+			g_bt[w][1] = __builtin_amdgcn_s_memrealtime();
+			g_bt[w][2] = 0;
+			g_bt[w][3] = 0;
+		}
+	}
+#endif
 	// every request of every wave has returned: the counter goes back to zero
 	// for the next launch on this stream
 	__builtin_amdgcn_s_waitcnt(0);
@@ -293,10 +311,6 @@ __device__ __forceinline__ void chunk_slot(uint32_t o, uint32_t& ln, uint32_t& r
 	ln = 32 * ((o >> 4) & 1) + 16 * ((o >> 5) & 1) + ((o >> 6) & 15);
 	ri = ((o >> 11) & 1) | (((o >> 10) & 1) << 1);
 }
-#ifdef FDBCRC_BTIMES
-// development: per-wave start / end timestamps of k_bigblocks (s_memrealtime, 100 MHz)
-__device__ uint64_t g_bt[16384][4];
-#endif
 template <int U>
 __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 #ifdef FDBCRC_BTIMES
