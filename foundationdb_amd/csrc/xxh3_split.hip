@@ -103,11 +103,19 @@ struct LSlot {
 	uint64_t p, len, seed;
 	uint32_t closed, pad;     // the slot takes no more buffers
 };
+typedef __attribute__((address_space(3))) volatile LSlot lds_vslot;
+typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
+typedef __attribute__((address_space(3))) volatile uint64_t lds_vu64;
 struct LShared {
 	uint64_t ring[kLChains][kLRingSteps * 4][8];  // D of block row (gstep % 64) * 4 + r
 	uint32_t tag[kLChains][kLRingSteps];          // gstep + 1 once the step's D is in the ring
 	LSlot slot[kLChains];
 };
+
+#ifdef FDBXXH_TIMES
+// development: per-wave {start, producers' first idle / chains' last dequeue, end, steps | buffers + spins << 20}
+__device__ uint64_t g_lt[4096][4];
+#endif
 
 template <bool SEEDS>
 __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
@@ -115,6 +123,11 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 	const uint64_t nlong = rdf64(gld64(S.sh + 0));
 	if (nlong == 0) return;  // no long buffer this batch (uniform over the grid)
 	const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#ifdef FDBXXH_TIMES
+	const uint64_t lt0 = __builtin_amdgcn_s_memrealtime();
+	uint64_t lt1 = 0, lcnt = 0;
+	const uint32_t lw = blockIdx.x * 16 + wv;
+#endif
 	for (uint32_t q = threadIdx.x; q < kLChains * kLRingSteps; q += blockDim.x) (&L.tag[0][0])[q] = 0;
 	if (threadIdx.x < kLChains) {
 		LSlot& s = L.slot[threadIdx.x];
@@ -123,8 +136,12 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 		s.closed = 0;
 	}
 	__syncthreads();
-	volatile LSlot* VS = L.slot;
-	volatile uint32_t* VT = &L.tag[0][0];
+	// LDS-typed volatile pointers: address-space inference leaves volatile
+	// accesses alone, and through a generic pointer every slot or tag read was
+	// a FLAT load -- which waits vmcnt(0), i.e. for the producer's whole load
+	// stream, at every claim (one step in flight per wave: 5.4 TB/s)
+	lds_vslot* VS = (lds_vslot*)L.slot;
+	lds_vu32* VT = (lds_vu32*)&L.tag[0][0];
 
 	if (wv >= kLProd) {
 		// ---------------- chain wave: slot c ----------------
@@ -143,6 +160,10 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 			if (lane == 0) q = atomicAdd((unsigned long long*)S.sh + 1, 1ull);
 			q = rdf64(__shfl(q, 0));
 			if (q >= nlong) break;
+#ifdef FDBXXH_TIMES
+			lt1 = __builtin_amdgcn_s_memrealtime();
+			lcnt += 1;
+#endif
 			const XEnt E = S.ents[q];
 			const uint64_t p = rdf64(E.p), len = rdf64(E.len), seed = rdf64(E.seed), idx = rdf64(E.idx);
 			const uint64_t nfull = (len - 1) >> 10, nb = nfull + 1;
@@ -185,6 +206,9 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 						return;
 					}
 					__builtin_amdgcn_s_sleep(1);
+#ifdef FDBXXH_TIMES
+					lcnt += 1ull << 20;
+#endif
 				}
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 				const uint64_t b0 = 4ull * t;
@@ -219,6 +243,14 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 			if (lane == 0) S.out[idx] = h;
 		}
 		if (lane == 0) VS[c].closed = 1;
+#ifdef FDBXXH_TIMES
+		if (lane == 0 && lw < 4096) {
+			g_lt[lw][0] = lt0;
+			g_lt[lw][1] = lt1;
+			g_lt[lw][2] = __builtin_amdgcn_s_memrealtime();
+			g_lt[lw][3] = lcnt;
+		}
+#endif
 		return;
 	}
 
@@ -242,7 +274,7 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 		for (uint32_t u = 0; u < 2 * kLChains; ++u) {
 			const uint32_t c = (pref + u) % kLChains;
 			{
-				const uint64_t cw = *(volatile uint64_t*)&L.slot[c].claimed;
+				const uint64_t cw = *(lds_vu64*)&VS[c].claimed;
 				const uint32_t cl = (uint32_t)cw, gb = (uint32_t)(cw >> 32);
 				// lim is read after {claimed, gbase}: if the slot changed buffers in
 				// between, gbase differs and the swap below fails
@@ -266,18 +298,25 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 			}
 		}
 	};
+	// The loads are unconditional -- an idle step reads the first long buffer's
+	// first KiB and discards it -- so the in-order vmcnt waits count exactly
+	// one step's loads behind each step: skipped loads on one path made every
+	// wait vmcnt(0) (one step in flight per wave).
+	const uint64_t idle_p = rdf64(S.ents[0].p);
 	auto load = [&](PStep& St) __attribute__((always_inline)) {
-		if (St.nrows == 0) return;
+		const bool on = St.nrows != 0;
 		const uint32_t rr = (uint32_t)r < St.nrows ? (uint32_t)r : 0u;  // rows past the buffer: row 0's block
-		const uint64_t blk = 4ull * St.t + rr;
-		const uint64_t nfull = (St.len - 1) >> 10;
-		const uint32_t ns = (uint32_t)(((St.len - 1) - (nfull << 10)) >> 6);
+		const uint64_t blk = on ? 4ull * St.t + rr : 0;
+		const uint64_t len = on ? St.len : 1024;
+		const uint64_t p = on ? St.p : idle_p;
+		const uint64_t nfull = (len - 1) >> 10;
+		const uint32_t ns = (uint32_t)(((len - 1) - (nfull << 10)) >> 6);
 		const bool fin = blk == nfull;
 #pragma unroll
 		for (int i = 0; i < 4; ++i) {
 			const uint32_t s = g + 4 * i;
 			const bool tail = fin && (s == 15 || s >= ns);
-			const uint64_t a = tail ? St.p + St.len - 64 + 16 * k : St.p + (blk << 10) + 64 * s + 16 * k;
+			const uint64_t a = tail ? p + len - 64 + 16 * k : p + (blk << 10) + 64 * s + 16 * k;
 			const u64x2u x = __builtin_nontemporal_load((g_u64x2u*)a);
 			St.v[i][0] = x[0];
 			St.v[i][1] = x[1];
@@ -369,6 +408,10 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 		claim(B);
 		publish();
 		load(B);
+#ifdef FDBXXH_TIMES
+		lcnt += (A.nrows != 0) + (B.nrows != 0);
+		if (A.nrows == 0 && B.nrows == 0 && lt1 == 0) lt1 = __builtin_amdgcn_s_memrealtime();
+#endif
 		if (A.nrows == 0 && B.nrows == 0) {
 			if (all_closed()) break;
 			if (++idle >= kLSpinMax) break;  // (never: see the chain's bound)
@@ -377,6 +420,14 @@ __global__ __launch_bounds__(1024) void k_xlong(XLong S) {
 			idle = 0;
 		}
 	}
+#ifdef FDBXXH_TIMES
+	if (lane == 0 && lw < 4096) {
+		g_lt[lw][0] = lt0;
+		g_lt[lw][1] = lt1;
+		g_lt[lw][2] = __builtin_amdgcn_s_memrealtime();
+		g_lt[lw][3] = lcnt;
+	}
+#endif
 }
 
 
@@ -389,3 +440,9 @@ int launch_xxh3_long(const XLong& S, int num_cus, bool seeds, hipStream_t stream
 }
 
 }  // namespace fdbxxh
+
+#ifdef FDBXXH_TIMES
+extern "C" int fdbxxh_debug_ltimes(void* host, uint64_t nwave) {
+	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbxxh::g_lt), nwave * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif
