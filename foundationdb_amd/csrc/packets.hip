@@ -17,7 +17,7 @@
 //                 serial chain, each header's length locating the next --
 //                 reading the header bytes only (a 64-byte register window),
 //                 and appends every complete, well-sized frame to a frame list
-//                 (one atomic per step of a wave)
+//                 (staged in registers, one atomic per wave every 8 steps)
 //   XXH3 varlen   the frame payloads through the XXH3 engine
 //                 (xxh3_kernels.hip / xxh3_split.hip), batch size read on the
 //                 device from the walk's frame counter
@@ -65,8 +65,9 @@ struct WalkP {
 // inside the window costs no load: runs of small frames share lines).  The
 // first design staged every buffer whole in LDS (one wave per buffer), which
 // read the batch's bytes a second time: the walk was HBM-bound (257 us on the
-// bench's 1 GiB of Zipf packets).  Per step of the walk, the wave's frames
-// are reserved in the frame list with one atomic.
+// bench's 1 GiB of Zipf packets).
+constexpr int kWalkStage = 8;  // walk steps per list flush
+
 __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
 	const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t lane = threadIdx.x & 63;
@@ -104,58 +105,83 @@ __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
 	int32_t status = FDB_PACKET_OK;
 	bool live = in, overflow = false;
 	uint64_t* const fcount = P.w.hdr;
-	while (__ballot(live) != 0) {
-		bool frame = false;
-		uint32_t fl = 0;
-		uint64_t ck = 0, a = 0;
-		if (live) {
-			a = B0 + p;
-			if (len - p < 4) {                                   // FlowTransport.cpp:1285-1286
-				live = false;
-			} else if (P.hdr == 12 && len - p - 4 < 8) {         // :1293-1294
-				live = false;
-			} else {
-				if (a < wbeg || a + P.hdr > wbeg + 64) restage(a);
-				fl = rd32(a);
-				if (fl > P.limit) {                                // :1299-1304 (before the frame is complete)
-					status = FDB_PACKET_LIMIT_EXCEEDED;
-					live = false;
-				} else if (len - p - P.hdr < fl) {                 // :1306-1307
-					live = false;
-				} else if (fl < 16) {                              // :1309-1319 (sizeof(UID))
-					status = FDB_PACKET_TOO_SMALL;
-					live = false;
-				} else {
-					if (P.hdr == 12) ck = ((uint64_t)rd32(a + 8) << 32) | rd32(a + 4);
-					frame = true;
-				}
-			}
+	// The frames of kWalkStage steps are held in the lane's registers (slot s
+	// of the unrolled group: the step index is wave-uniform) and leave together:
+	// one reservation atomic per wave and group, the lane's frames contiguous
+	// in the list.  Per-step reservations and stores put an atomic and a store
+	// acknowledgement on the walk's chain (vmcnt counts stores and loads in
+	// issue order: the next header load's wait waited for them).
+	uint64_t s_off[kWalkStage], s_ck[kWalkStage];
+	uint32_t s_len[kWalkStage];
+	uint32_t smask = 0;
+	auto step = [&](int slot) __attribute__((always_inline)) {
+		if (!live) return;
+		const uint64_t a = B0 + p;
+		if (len - p < 4) {                                   // FlowTransport.cpp:1285-1286
+			live = false;
+			return;
 		}
-		// this step's frames: one reservation for the wave (reserving a step
-		// ahead, so that the atomic's return is off the walk's chain, measured
-		// the same: the header loads are the chain)
-		const uint64_t m = __ballot(frame);
-		if (m != 0) {
-			const uint32_t lead = (uint32_t)__builtin_ctzll(m);
-			uint64_t at = 0;
-			if (lane == lead) at = atomicAdd((unsigned long long*)fcount, (unsigned long long)__builtin_popcountll(m));
-			at = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), (int)lead) << 32) |
-			     (uint64_t)(uint32_t)__shfl((int)(uint32_t)at, (int)lead);
-			if (frame) {
-				const uint64_t f = at + (uint64_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+		if (P.hdr == 12 && len - p - 4 < 8) {                // :1293-1294
+			live = false;
+			return;
+		}
+		if (a < wbeg || a + P.hdr > wbeg + 64) restage(a);
+		const uint32_t fl = rd32(a);
+		if (fl > P.limit) {                                  // :1299-1304 (before the frame is complete)
+			status = FDB_PACKET_LIMIT_EXCEEDED;
+			live = false;
+		} else if (len - p - P.hdr < fl) {                   // :1306-1307
+			live = false;
+		} else if (fl < 16) {                                // :1309-1319 (sizeof(UID))
+			status = FDB_PACKET_TOO_SMALL;
+			live = false;
+		} else {
+			s_ck[slot] = P.hdr == 12 ? ((uint64_t)rd32(a + 8) << 32) | rd32(a + 4) : 0;
+			s_off[slot] = a + P.hdr - reinterpret_cast<uint64_t>(P.base);
+			s_len[slot] = fl;
+			smask |= 1u << slot;
+			p += P.hdr + fl;
+			++ord;
+		}
+	};
+	auto flush = [&]() __attribute__((always_inline)) {
+		const uint32_t n = (uint32_t)__builtin_popcount(smask);
+		// the wave's exclusive prefix of n, and its total
+		uint32_t incl = n;
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
+			incl += lane >= (uint32_t)d ? v : 0u;
+		}
+		const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+		if (total == 0) return;
+		uint64_t at = 0;
+		if (lane == 0) at = atomicAdd((unsigned long long*)fcount, (unsigned long long)total);
+		at = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), 0) << 32) | (uint64_t)(uint32_t)__shfl((int)(uint32_t)at, 0);
+		uint64_t f = at + (incl - n);
+		uint32_t o = ord - n;
+#pragma unroll
+		for (int s = 0; s < kWalkStage; ++s) {
+			if (smask & (1u << s)) {
 				if (f < P.w.cap) {
-					P.w.foff[f] = a + P.hdr - reinterpret_cast<uint64_t>(P.base);
-					P.w.flen[f] = fl;
-					P.w.fexp[f] = ck;
+					P.w.foff[f] = s_off[s];
+					P.w.flen[f] = s_len[s];
+					P.w.fexp[f] = s_ck[s];
 					P.w.fbuf[f] = (uint32_t)b;
-					P.w.ford[f] = ord;
+					P.w.ford[f] = o;
 				} else {
 					overflow = true;
 				}
-				p += P.hdr + fl;
-				++ord;
+				++f;
+				++o;
 			}
 		}
+		smask = 0;
+	};
+	while (__ballot(live) != 0) {
+#pragma unroll
+		for (int s = 0; s < kWalkStage; ++s) step(s);
+		flush();
 	}
 	if (in) {
 		P.w.walked[b] = ord;
