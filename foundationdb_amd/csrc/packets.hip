@@ -15,7 +15,7 @@
 // balanced over the whole GPU instead of one buffer per thread:
 //   k_pkt_walk    one lane per receive buffer walks its frame headers -- a
 //                 serial chain, each header's length locating the next --
-//                 reading the header bytes only (a 64-byte register window),
+//                 reading the header bytes only (one 16-byte load per header),
 //                 and appends every complete, well-sized frame to a frame list
 //                 (staged in registers, one atomic per wave every 8 steps)
 //   XXH3 varlen   the frame payloads through the XXH3 engine
@@ -60,12 +60,15 @@ struct WalkP {
 };
 
 // One LANE per receive buffer: each lane walks its buffer's frame headers --
-// a serial chain, each header's length locating the next -- with loads of the
-// header bytes only, through a 64-byte window held in its registers (a header
-// inside the window costs no load: runs of small frames share lines).  The
-// first design staged every buffer whole in LDS (one wave per buffer), which
-// read the batch's bytes a second time: the walk was HBM-bound (257 us on the
-// bench's 1 GiB of Zipf packets).
+// a serial chain, each header's length locating the next -- with one 16-byte
+// load per header, at the header's own address (a following header inside it
+// costs no load).  The walk's time is its longest chain times a load round
+// trip, and the round trip grows with the requests in flight: on the bench's
+// 1 GiB of Zipf packets, a 64-byte window of four aligned loads took 93 us,
+// two aligned loads 73 us, one load 63 us; and 64-thread workgroups (one wave
+// on each of 256 CUs, not four waves on 64) 110 -> 90 us.  The first design
+// staged every buffer whole in LDS (one wave per buffer), which read the
+// batch's bytes a second time: the walk was HBM-bound (257 us).
 constexpr int kWalkStage = 8;  // walk steps per list flush
 
 __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
@@ -76,24 +79,40 @@ __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
 	const uint64_t len = in ? *((g_u64*)reinterpret_cast<uintptr_t>(P.blen + b)) : 0;
 	const uint64_t E = B0 + len;
 	const uint64_t last_chunk = len ? (E - 1) & ~uint64_t(15) : 0;
-	uint64_t wbeg = ~uint64_t(0);  // window: bytes [wbeg, wbeg + 64), wbeg 16-byte aligned
-	u32x4 win[4];
+#ifndef FDBPKT_WIN_CHUNKS
+#define FDBPKT_WIN_CHUNKS 1
+#endif
+	// window chunks of 16 bytes: >= 2 aligned ones (a header fits in two), or
+	// one at the header's own address
+	constexpr int kWinC = FDBPKT_WIN_CHUNKS;
+	uint64_t wbeg = ~uint64_t(0);  // window: bytes [wbeg, wbeg + 16 kWinC)
+	u32x4 win[kWinC];
+	typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+	typedef __attribute__((address_space(1))) const u32x4u g_u32x4u;
+	const uint64_t hi16 = (E + 15) & ~uint64_t(15);  // the end of the buffer's last 16-byte chunk
 	auto restage = [&](uint64_t a) {
+		if (kWinC == 1) {
+			// one 16-byte load at the header itself (unaligned), moved back to end
+			// at hi16 near the buffer's end: the 12-byte header stays inside it
+			wbeg = a + 16 <= hi16 ? a : hi16 - 16;
+			win[0] = *((g_u32x4u*)reinterpret_cast<uintptr_t>(wbeg));
+			return;
+		}
 		wbeg = a & ~uint64_t(15);
 #pragma unroll
-		for (int i = 0; i < 4; ++i) {
+		for (int i = 0; i < kWinC; ++i) {
 			// chunks past the buffer re-read its last one (never used: the walk
 			// checks every length against the buffer's end)
 			const uint64_t c = wbeg + 16ull * i;
 			win[i] = *((g_u32x4*)reinterpret_cast<uintptr_t>(c <= last_chunk ? c : last_chunk));
 		}
 	};
-	// little-endian u32 at absolute address a inside the window (a - wbeg <= 60)
+	// little-endian u32 at absolute address a inside the window (a - wbeg <= 16 kWinC - 4)
 	auto rd32 = [&](uint64_t a) -> uint32_t {
 		const uint32_t o = (uint32_t)(a - wbeg), wi = o >> 2;
 		uint32_t w0 = 0, w1 = 0;
 #pragma unroll
-		for (uint32_t k = 0; k < 16; ++k) {
+		for (uint32_t k = 0; k < 4 * kWinC; ++k) {
 			const uint32_t v = win[k >> 2][k & 3];
 			w0 = wi == k ? v : w0;
 			w1 = wi + 1 == k ? v : w1;
@@ -125,7 +144,7 @@ __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
 			live = false;
 			return;
 		}
-		if (a < wbeg || a + P.hdr > wbeg + 64) restage(a);
+		if (a < wbeg || a + P.hdr > wbeg + 16 * kWinC) restage(a);
 		const uint32_t fl = rd32(a);
 		if (fl > P.limit) {                                  // :1299-1304 (before the frame is complete)
 			status = FDB_PACKET_LIMIT_EXCEEDED;
@@ -303,7 +322,10 @@ int launch_verify(const uint8_t* base, const uint64_t* boff, const uint64_t* ble
 	W.hdr = checksum ? 12u : 4u;
 	W.limit = limit;
 	W.w = w;
-	k_pkt_walk<<<(unsigned)((nbuf + 255) / 256), 256, 0, s>>>(W);
+#ifndef FDBPKT_WALK_BLOCK
+#define FDBPKT_WALK_BLOCK 64
+#endif
+	k_pkt_walk<<<(unsigned)((nbuf + FDBPKT_WALK_BLOCK - 1) / FDBPKT_WALK_BLOCK), FDBPKT_WALK_BLOCK, 0, s>>>(W);
 	CheckP C{};
 	C.base = base;
 	C.boff = boff;
