@@ -237,3 +237,40 @@ def test_gpu_packets_one_shot_matches(cuda):
     assert np.array_equal(got["consumed"], want[0])
     assert np.array_equal(got["frames"], want[1])
     assert np.array_equal(got["status"], want[2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("checksum", [True, False])
+def test_gpu_packets_many_small_frames(cuda, checksum):
+    """Buffers of up to ~150 minimum-size frames (many 8-step flush groups of
+    the walk per lane, every lane of a wave ending at a different step), at
+    random alignments, with the batch's last buffer -- a frame cut inside its
+    header -- ending at the device array's last byte: the walk's one 16-byte
+    header load is moved back near a buffer's end and must stay inside it."""
+    import foundationdb_amd.packets as PK
+    rng = np.random.default_rng(41 + checksum)
+    bufs = []
+    for i in range(300):
+        n = int(rng.integers(0, 150))
+        body = b"".join(frame(rng.integers(0, 256, int(rng.integers(16, 40)), dtype=np.uint8).tobytes(), checksum)
+                        for _ in range(n))
+        if i % 7 == 3:  # a cut frame after the run: its length word or checksum incomplete
+            nxt = frame(rng.integers(0, 256, 20, dtype=np.uint8).tobytes(), checksum)
+            body += nxt[: int(rng.integers(1, 12 if checksum else 4))]
+        bufs.append(body)
+    last = frame(rng.integers(0, 256, 30, dtype=np.uint8).tobytes(), checksum)
+    bufs.append(b"".join(frame(rng.integers(0, 256, 17, dtype=np.uint8).tobytes(), checksum) for _ in range(9))
+                + last[:7])
+    mem, offs, lens = pack(bufs, rng)
+    mem = mem[: int(offs[-1] + lens[-1])].copy()  # no bytes after the last buffer
+    want_c, want_f, want_s = O.packets_verify(mem, offs, lens, checksum=checksum)
+    total = int(lens.sum())
+    V = PK.PacketVerifier(cuda, len(bufs), total // 20 + len(bufs), total)
+    V.verify(_dev(mem, cuda), _dev(offs, cuda), _dev(lens, cuda), checksum=checksum)
+    got = V.results_numpy()
+    assert int(want_f.max()) > 100
+    assert np.array_equal(got["frames"], want_f)
+    assert np.array_equal(got["status"], want_s)
+    assert np.array_equal(got["consumed"], want_c)
+    fr = V.frames_numpy()
+    assert fr.size == int(want_f.sum())
