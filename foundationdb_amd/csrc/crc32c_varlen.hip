@@ -517,11 +517,12 @@ __global__ __launch_bounds__(256) void k_xcount(V7Params P) {
 	const uint64_t i = (uint64_t)blockIdx.x * kTileW + threadIdx.x;
 	const uint32_t lane = threadIdx.x & 63;
 	const bool in = i < P.count;
-	uint64_t off = 0, len = 0;
-	if (in) v7_buffer(P, i, off, len);
-	uint64_t on = __shfl_down(off, 1), ln = __shfl_down(len, 1);
-	if (lane == 63 && i + 1 < P.count) v7_buffer(P, i + 1, on, ln);
+	uint64_t off = 0, len = 0, on = 0, ln = 0;
 	const bool has_next = i + 1 < P.count;
+	// the next buffer's metadata loaded directly (beside this one's, one round
+	// trip) rather than shuffled down, which left lane 63's own load behind it
+	if (in) v7_buffer(P, i, off, len);
+	if (has_next) v7_buffer(P, i + 1, on, ln);
 	const uint64_t e = off + len;
 	const bool bad = in && has_next && !(on >= e && on - e < 4096 && on - e <= (len > 256 ? len : 256));
 	if (__ballot(bad) && lane == 0) P.xhdr[0] = P.epoch;
