@@ -442,6 +442,11 @@ struct RowData {
 #define FDBXXH_G3W1 37
 #endif
 constexpr uint64_t kRowsG3W0 = FDBXXH_G3W0, kRowsG3W1 = FDBXXH_G3W1;  // k_xxh3_rows, three generations (32nds)
+#ifndef FDBXXH_ROWS_XE
+#define FDBXXH_ROWS_XE 33
+#define FDBXXH_ROWS_XO 31
+#endif
+constexpr uint64_t kRowsXE = FDBXXH_ROWS_XE, kRowsXO = FDBXXH_ROWS_XO;  // k_xxh3_rows, even / odd XCDs (32nds)
 #ifdef FDBXXH_TIMES
 // development: per-wave timestamps of the row kernels (start, rows done, end; s_memrealtime, 100 MHz)
 __device__ uint64_t g_vt[16384][4];
@@ -463,18 +468,30 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 	// 573 / 613 / 669 us median for equal ranges), so their ranges are longer
 	// -- 42 : 37 : 32 (633 / 619 / 614 us; 37 : 35 : 32 left 584 / 612 / 642;
 	// two generations: 42 : 32) -- and the generations end together.
+	// Within a generation, workgroup b runs on XCD b % 8 and the odd XCDs
+	// stream ~6 % slower (as in k_pages4k, crc32c_device.h: xcd_range): an even
+	// workgroup's waves take kRowsXE / kRowsXO of an odd one's.  Same box,
+	// bench protocol: xxh3-pages4k 674 -> 668 us, SQLite's list 499 -> 495 us;
+	// the 8-byte-aligned form (DiskQueue's 4092 B at +4) ran 557 -> 570 us with
+	// them, so it keeps equal weights.
+	const uint64_t kXE = A16 ? kRowsXE : 32, kXO = A16 ? kRowsXO : 32;
 	uint64_t begin, end;
 	if (P.ngen == 2 || P.ngen == 3) {
 		const uint64_t wpg = nwave / P.ngen;
 		const uint64_t gsel = w / wpg;
 		const uint64_t W0 = P.ngen == 3 ? kRowsG3W0 : 42, W1 = P.ngen == 3 ? kRowsG3W1 : 32, W2 = 32;
 		const uint64_t sumW = P.ngen == 3 ? W0 + W1 + W2 : W0 + W1;
-		const uint64_t unit = (P.count * 32 + wpg * sumW - 1) / (wpg * sumW);  // pages per wave at weight 32
-		auto per_of = [&](uint64_t Wg) { return ((unit * Wg + 31) / 32 + 3) & ~uint64_t(3); };
-		const uint64_t p0 = per_of(W0), p1 = per_of(W1), p2 = per_of(W2);
-		const uint64_t pg = gsel == 0 ? p0 : (gsel == 1 ? p1 : p2);
-		const uint64_t start = gsel == 0 ? 0 : (gsel == 1 ? wpg * p0 : wpg * (p0 + p1));
-		begin = start + (w - gsel * wpg) * pg;
+		const uint64_t bpg = wpg / wpb, ne = (bpg + 1) / 2, no = bpg / 2;  // workgroups per generation, even / odd
+		const uint64_t den = sumW * wpb * (ne * kXE + no * kXO);
+		const uint64_t unit = (P.count * 1024 + den - 1) / den;  // pages per wave at weight 32 x 32
+		auto per_of = [&](uint64_t Wg, uint64_t Wx) { return ((unit * Wg * Wx + 1023) / 1024 + 3) & ~uint64_t(3); };
+		auto gen_pages = [&](uint64_t Wg) { return wpb * (ne * per_of(Wg, kXE) + no * per_of(Wg, kXO)); };
+		const uint64_t Wg = gsel == 0 ? W0 : (gsel == 1 ? W1 : W2);
+		const uint64_t start = gsel == 0 ? 0 : (gsel == 1 ? gen_pages(W0) : gen_pages(W0) + gen_pages(W1));
+		const uint64_t wi = w - gsel * wpg, bi = wi / wpb;
+		const uint64_t pe = per_of(Wg, kXE), po = per_of(Wg, kXO);
+		begin = start + wpb * (((bi + 1) / 2) * pe + (bi / 2) * po) + (wi % wpb) * ((bi & 1) ? po : pe);
+		const uint64_t pg = (bi & 1) ? po : pe;
 		end = begin + pg < P.count ? begin + pg : P.count;
 	} else {
 		uint64_t per = (P.count + nwave - 1) / nwave;
