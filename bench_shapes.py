@@ -88,6 +88,26 @@ def xxh3_seeds(n):
     return (i * np.uint64(0x9E3779B97F4A7C15)) ^ np.uint64(0xFDBEEFDB)
 
 
+def array_sha256(a, dtype):
+    """sha256 of the whole result array as little-endian words: any single
+    wrong value (or two that cancel in xor and sum) changes it."""
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=dtype).tobytes()).hexdigest()
+
+
 def digest(crcs):
+    """xor, sum and sha256 of a CRC-32C result array (the full-size golden pins)."""
     crcs = np.asarray(crcs, dtype=np.uint32)
-    return {"xor": int(np.bitwise_xor.reduce(crcs)) if crcs.size else 0, "sum": int(crcs.astype(np.uint64).sum())}
+    return {"xor": int(np.bitwise_xor.reduce(crcs)) if crcs.size else 0, "sum": int(crcs.astype(np.uint64).sum()),
+            "sha256": array_sha256(crcs, "<u4")}
+
+
+def pinned(entry):
+    """The digest fields of a golden entry (every full-size entry carries all three)."""
+    return {k: entry[k] for k in ("xor", "sum", "sha256")}
+
+
+def digest64(h):
+    """The same for XXH3-64 result arrays (hex strings, as xxh3_golden.json holds them)."""
+    h = np.asarray(h, dtype=np.uint64)
+    return {"xor": "%016x" % (int(np.bitwise_xor.reduce(h)) if h.size else 0), "sum": "%016x" % int(h.sum(dtype=np.uint64)),
+            "sha256": array_sha256(h, "<u8")}

@@ -121,8 +121,8 @@ class Pages:
     def verify(self):
         got = self.out.cpu().numpy()
         d = shard_digest(self.page_bytes, self.count, self.seed, self.state)
-        if d is not None:  # the reference's own digest of this exact shard
-            return int(np.bitwise_xor.reduce(got)) == d["xor"] and int(got.astype(np.uint64).sum()) == d["sum"]
+        if d is not None:  # the reference's own digest of this exact shard (xor, sum, sha256 of every checksum)
+            return S.digest(got) == S.pinned(d)
         return _spot_check(self.buf, np.arange(self.count, dtype=np.uint64) * self.page_bytes,
                            np.full(self.count, self.page_bytes, np.uint64), self.seed, got)
 
@@ -136,7 +136,7 @@ class Pages:
 
 
 def shard_digest(page_bytes, count, seed, state):
-    """{xor, sum} the reference produced for this page batch (tests/golden:
+    """{xor, sum, sha256} the reference produced for this page batch (tests/golden:
     pages_full for the state 0x5EED batch, pages_shards for rank shards), or None."""
     g = _golden()
     full = g["pages_full"]
@@ -155,14 +155,14 @@ def shard_digest(page_bytes, count, seed, state):
 
 
 def _varlen_digest(shape, lengths, seed):
-    """{xor, sum} the reference produced for this exact batch (tests/golden,
+    """{xor, sum, sha256} the reference produced for this exact batch (tests/golden,
     make_golden.py --varlen), or None if the batch is not a pinned one."""
     ent = _golden().get("varlen_full", {}).get(shape) if shape else None
     if ent is None or ent["lengths_sha256"] != S.lengths_digest(lengths):
         return None
     for d in ent["digests"]:
         if d["seed"] == seed:
-            return {"xor": d["xor"], "sum": d["sum"]}
+            return S.pinned(d)
     return None
 
 
@@ -310,7 +310,7 @@ class HostPages(HostChunks):
         got = self.out
         if self.count == 1 << 20:
             d = [d for d in _golden()["pages_full"]["digests"] if d["seed"] == self.seed][0]
-            return int(np.bitwise_xor.reduce(got)) == d["xor"] and int(got.astype(np.uint64).sum()) == d["sum"]
+            return S.digest(got) == S.pinned(d)
         host = self.buf.numpy()
         rng = np.random.default_rng(0)
         return all(F.crc32c_append(self.seed, host[i * 4096:(i + 1) * 4096]) == int(got[i])
@@ -376,8 +376,7 @@ class Xxh3Pages:
         with open(os.path.join(ROOT, "tests", "golden", "xxh3_golden.json")) as fh:
             g = json.load(fh)["pages_full"]
         a = self.out.cpu().numpy().view(np.uint64)
-        return ("%016x" % int(np.bitwise_xor.reduce(a)) == g["xor"] and
-                "%016x" % int(a.sum(dtype=np.uint64)) == g["sum"])
+        return S.digest64(a) == S.pinned(g)
 
     def cpu_sample(self):
         from oracle import oracle as O

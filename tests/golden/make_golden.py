@@ -22,6 +22,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
+import bench_shapes as S  # noqa: E402  (digest: xor, sum and sha256 of a whole result array)
 
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "crc32c_golden.json")
 
@@ -36,9 +37,8 @@ def sm_bytes(nbytes, state):
 def varlen_full(g):
     """BASELINE configs[2] (Zipf packets) and configs[4] (backup chunks) at their
     exact bench shapes (bench_shapes.py): the reference's crc32c_append over
-    every buffer of each ~1 GiB batch, as xor/sum digests plus the first 64
+    every buffer of each ~1 GiB batch, as xor/sum/sha256 digests plus the first 64
     checksums, for seeds 0 and 0xFDBEEFDB."""
-    import bench_shapes as S
     ref = O.reference()
     out = {}
     for name in ("zipf", "chunks"):
@@ -65,9 +65,10 @@ def pages_shards(g, nshard=8, threads=8):
     GPUs -- rank r checksums bytes [r*4 GiB, (r+1)*4 GiB) of one splitmix64
     file.  The reference's crc32c_append over every page of every shard, as 8 KiB
     pages with the SQLite seed (pages8k) and as 4 KiB pages with seed 0
-    (pages4k), xor/sum digests per shard."""
+    (pages4k), xor/sum/sha256 digests per shard."""
     from concurrent.futures import ThreadPoolExecutor
     from bench_shapes import GOLDEN_GAMMA, SHARD_BYTES, shard_state
+    import bench_shapes as S
     out = {"state": 0x5EED, "shard_bytes": SHARD_BYTES, "gamma": GOLDEN_GAMMA, "pages8k": [], "pages4k": []}
     for r in range(nshard):
         data = O.splitmix64(SHARD_BYTES // 8, shard_state(r)).view(np.uint8)
@@ -78,8 +79,7 @@ def pages_shards(g, nshard=8, threads=8):
                 parts = list(pool.map(lambda k: O.reference_batch_fixed(data[cuts[k] * pb:], pb, pb, cuts[k + 1] - cuts[k],
                                                                          seed=seed), range(threads)))
             c = np.concatenate(parts)
-            out[name].append({"rank": r, "state": shard_state(r), "count": n, "page_bytes": pb, "seed": seed,
-                              "xor": int(np.bitwise_xor.reduce(c)), "sum": int(c.astype(np.uint64).sum())})
+            out[name].append(dict(S.digest(c), rank=r, state=shard_state(r), count=n, page_bytes=pb, seed=seed))
             print(name, r, hex(out[name][-1]["xor"]), flush=True)
         del data
     g["pages_shards"] = out
@@ -168,17 +168,15 @@ def main():
     pb = {"state": 0x5EED, "page_bytes": 4096, "count": 65536, "digests": []}
     for s in (0, 0xFDBEEFDB, 0xAB12FD93):
         c = np.array([crc(s, pages[4096 * i:4096 * (i + 1)]) for i in range(65536)], dtype=np.uint32)
-        pb["digests"].append({"seed": s, "xor": int(np.bitwise_xor.reduce(c)), "sum": int(c.astype(np.uint64).sum()),
-                              "first64": [int(x) for x in c[:64]]})
+        pb["digests"].append(dict(S.digest(c), seed=s, first64=[int(x) for x in c[:64]]))
     # 8 KiB sqlite-sized pages over the same bytes
     c8 = np.array([crc(0xFDBEEFDB, pages[8192 * i:8192 * (i + 1)]) for i in range(32768)], dtype=np.uint32)
-    pb["digest_8k_fdbeefdb"] = {"xor": int(np.bitwise_xor.reduce(c8)), "sum": int(c8.astype(np.uint64).sum())}
+    pb["digest_8k_fdbeefdb"] = S.digest(c8)
     # 4088 / 4092 B sub-page regions (SQLite legacy codec, DiskQueue V1)
     c4088 = np.array([crc(0xFDBEEFDB, pages[4096 * i:4096 * i + 4088]) for i in range(65536)], dtype=np.uint32)
     c4092 = np.array([crc(0xFDBEEFDB, pages[4096 * i + 4:4096 * (i + 1)]) for i in range(65536)], dtype=np.uint32)
-    pb["digest_4088_fdbeefdb"] = {"xor": int(np.bitwise_xor.reduce(c4088)), "sum": int(c4088.astype(np.uint64).sum())}
-    pb["digest_4092_at4_fdbeefdb"] = {"xor": int(np.bitwise_xor.reduce(c4092)),
-                                      "sum": int(c4092.astype(np.uint64).sum())}
+    pb["digest_4088_fdbeefdb"] = S.digest(c4088)
+    pb["digest_4092_at4_fdbeefdb"] = S.digest(c4092)
     g["pages"] = pb
 
     # --- BASELINE configs[1] at full size: 1 Mi x 4 KiB (4 GiB), same stream
@@ -186,10 +184,9 @@ def main():
     full = {"state": 0x5EED, "page_bytes": 4096, "count": 1 << 20, "digests": []}
     for s in (0, 0xFDBEEFDB):
         c = O.reference_batch_fixed(big, 4096, 4096, 1 << 20, seed=s)
-        full["digests"].append({"seed": s, "xor": int(np.bitwise_xor.reduce(c)), "sum": int(c.astype(np.uint64).sum())})
+        full["digests"].append(dict(S.digest(c), seed=s))
     c = O.reference_batch_fixed(big, 8192, 8192, 1 << 19, seed=0xFDBEEFDB)
-    full["digest_8k_fdbeefdb"] = {"count": 1 << 19, "xor": int(np.bitwise_xor.reduce(c)),
-                                  "sum": int(c.astype(np.uint64).sum())}
+    full["digest_8k_fdbeefdb"] = dict(S.digest(c), count=1 << 19)
     del big
     g["pages_full"] = full
 

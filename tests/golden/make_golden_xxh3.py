@@ -19,6 +19,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
+import bench_shapes as S  # noqa: E402  (digest64: xor, sum and sha256 of a whole result array)
 
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "xxh3_golden.json")
 SEEDS = [0, 0xFDBEEFDB, 0x8000000000000005, 0x0123456789ABCDEF]
@@ -35,10 +36,9 @@ def varlen_full(g):
     """BASELINE configs[2] (Zipf packets) and configs[4] (backup chunks) at the
     exact bench shapes (bench_shapes.py), the bytes bench.py hashes (splitmix64,
     bench_shapes.STATE): the reference's XXH3_64bits over every buffer, and
-    XXH3_64bits_withSeed with per-buffer seeds (bench_shapes.xxh3_seeds), as xor/sum digests
+    XXH3_64bits_withSeed with per-buffer seeds (bench_shapes.xxh3_seeds), as xor/sum/sha256 digests
     plus the first 64 digests."""
     import ctypes
-    import bench_shapes as S
     L = O.xxh3_reference()
     f = L.XXH3_64bits_withSeed
     out = {}
@@ -53,9 +53,7 @@ def varlen_full(g):
         seeded = np.array([f(ctypes.c_void_p(base + int(o)), int(n), int(s))
                            for o, n, s in zip(offsets, lengths, sd)], dtype=np.uint64)
         for kind, h in (("seed0", plain), ("seeds", seeded)):
-            ent["digests"].append({"kind": kind, "xor": "%016x" % int(np.bitwise_xor.reduce(h)),
-                                   "sum": "%016x" % int(h.sum(dtype=np.uint64)),
-                                   "first64": ["%016x" % int(v) for v in h[:64]]})
+            ent["digests"].append(dict(S.digest64(h), kind=kind, first64=["%016x" % int(v) for v in h[:64]]))
         out[name] = ent
         del data
     g["varlen_full"] = out
@@ -90,8 +88,7 @@ def main():
     L = O.xxh3_reference()
     rw = np.array([L.XXH3_64bits_withSeed(pages.ctypes.data + 4096 * i, 4096, i) for i in range(0, npg, 16)],
                   dtype=np.uint64)
-    def digest(a):
-        return {"xor": "%016x" % int(np.bitwise_xor.reduce(a)), "sum": "%016x" % (int(a.sum(dtype=np.uint64)))}
+    digest = S.digest64
     g["pages"] = {"count": npg, "state": 0x5EED,
                   "sqlite_4088": dict(digest(sq), first=["%016x" % v for v in sq[:4]]),
                   "diskqueue_4088_at8": dict(digest(dq), count=npg - 1),

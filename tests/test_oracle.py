@@ -5,6 +5,7 @@ import os
 import numpy as np
 import pytest
 
+import bench_shapes as S
 from oracle import oracle as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -75,19 +76,38 @@ def test_page_batch_digests(golden, oracle_mod):
     pages = O.splitmix64(512 * pb["count"], pb["state"]).view(np.uint8)
     for d in pb["digests"]:
         c = O.batch_fixed(pages, 4096, 4096, pb["count"], seed=d["seed"])
-        assert int(np.bitwise_xor.reduce(c)) == d["xor"]
-        assert int(c.astype(np.uint64).sum()) == d["sum"]
+        assert S.digest(c) == S.pinned(d)
         assert [int(x) for x in c[:64]] == d["first64"]
     # SURVEY §8c / BASELINE.md published digest of this batch at seed 0
     d0 = [d for d in pb["digests"] if d["seed"] == 0][0]
     assert d0["xor"] == 0xC18E0D85 and d0["sum"] == 0x0000807AFF89425D
     assert d0["first64"][0] == 0x076DE509 and d0["first64"][1] == 0x808DD38F
     c8 = O.batch_fixed(pages, 8192, 8192, pb["count"] // 2, seed=0xFDBEEFDB)
-    assert int(np.bitwise_xor.reduce(c8)) == pb["digest_8k_fdbeefdb"]["xor"]
+    assert S.digest(c8) == S.pinned(pb["digest_8k_fdbeefdb"])
     c4088 = O.batch_fixed(pages, 4096, 4088, pb["count"], seed=0xFDBEEFDB)
-    assert int(c4088.astype(np.uint64).sum()) == pb["digest_4088_fdbeefdb"]["sum"]
+    assert S.digest(c4088) == S.pinned(pb["digest_4088_fdbeefdb"])
     c4092 = O.batch_fixed(pages[4:], 4096, 4092, pb["count"], seed=0xFDBEEFDB)
-    assert int(c4092.astype(np.uint64).sum()) == pb["digest_4092_at4_fdbeefdb"]["sum"]
+    assert S.digest(c4092) == S.pinned(pb["digest_4092_at4_fdbeefdb"])
+
+
+def test_digest_pins_catch_compensating_errors(golden, oracle_mod):
+    """The full-size pins hold a sha256 of the whole result array: two swapped
+    checksums (xor and sum unchanged) or a pair of errors that cancel in both
+    still fail the comparison."""
+    pb = golden["pages"]
+    pages = O.splitmix64(512 * pb["count"], pb["state"]).view(np.uint8)
+    d = pb["digests"][0]
+    c = O.batch_fixed(pages, 4096, 4096, pb["count"], seed=d["seed"])
+    assert S.digest(c) == S.pinned(d)
+    swapped = c.copy()
+    swapped[[10, 20]] = swapped[[20, 10]]
+    assert S.digest(swapped)["xor"] == d["xor"] and S.digest(swapped)["sum"] == d["sum"]
+    assert S.digest(swapped) != S.pinned(d)
+    # every full-size entry carries the array hash
+    for e in (golden["pages_full"]["digests"] + [golden["pages_full"]["digest_8k_fdbeefdb"]] +
+              golden["pages_shards"]["pages4k"] + golden["pages_shards"]["pages8k"] +
+              golden["varlen_full"]["zipf"]["digests"] + golden["varlen_full"]["chunks"]["digests"]):
+        assert len(e["sha256"]) == 64
 
 
 def test_chained_equals_oneshot(golden, oracle_mod):
@@ -127,7 +147,6 @@ def test_oracle_matches_compiled_reference_random():
 def test_oracle_varlen_configs_exact_batches(oracle_mod, golden, name):
     """The oracle reproduces the reference's digests of the exact configs[2] /
     configs[4] batches (and the shape generator still yields the pinned list)."""
-    import bench_shapes as S
     O = oracle_mod
     ent = golden["varlen_full"][name]
     lengths, offsets, extent = S.shape(name)
@@ -135,7 +154,7 @@ def test_oracle_varlen_configs_exact_batches(oracle_mod, golden, name):
     data = O.splitmix64(extent // 8, ent["state"]).view(np.uint8)
     d = ent["digests"][1]
     got = O.batch_varlen(data, offsets, lengths, seed=d["seed"])
-    assert S.digest(got) == {"xor": d["xor"], "sum": d["sum"]}
+    assert S.digest(got) == S.pinned(d)
     assert [int(x) for x in got[:64]] == d["first64"]
 
 
@@ -156,7 +175,6 @@ def test_shard_generator_jump_and_shard_digests():
     is exact (checked at small word offsets against the continuous stream), and
     shard 0 of the reference-generated shard digests is the full-size page batch
     (tests/golden pages_shards vs pages_full)."""
-    import bench_shapes as S
     whole = O.splitmix64(4096, S.STATE)
     for w in (1, 7, 512, 3000):
         st = (S.STATE + w * S.GOLDEN_GAMMA) & 0xFFFFFFFFFFFFFFFF
@@ -168,7 +186,6 @@ def test_shard_generator_jump_and_shard_digests():
     assert len(sh["pages8k"]) == 8 and len(sh["pages4k"]) == 8
     assert [d["state"] for d in sh["pages8k"]] == [S.shard_state(r) for r in range(8)]
     d0 = [d for d in full["digests"] if d["seed"] == 0][0]
-    assert (sh["pages4k"][0]["xor"], sh["pages4k"][0]["sum"]) == (d0["xor"], d0["sum"])
-    assert (sh["pages8k"][0]["xor"], sh["pages8k"][0]["sum"]) == (full["digest_8k_fdbeefdb"]["xor"],
-                                                                  full["digest_8k_fdbeefdb"]["sum"])
+    assert S.pinned(sh["pages4k"][0]) == S.pinned(d0)
+    assert S.pinned(sh["pages8k"][0]) == S.pinned(full["digest_8k_fdbeefdb"])
     assert len({d["xor"] for d in sh["pages8k"]}) == 8  # the shards differ

@@ -33,8 +33,14 @@ def hexs(a):
 
 
 def digest(a):
-    a = np.asarray(a, dtype=np.uint64)
-    return {"xor": "%016x" % int(np.bitwise_xor.reduce(a)), "sum": "%016x" % int(a.sum(dtype=np.uint64))}
+    """xor, sum and sha256 of a whole XXH3 result array (bench_shapes.digest64)."""
+    import bench_shapes as S
+    return S.digest64(a)
+
+
+def pin(entry):
+    import bench_shapes as S
+    return S.pinned(entry)
 
 
 # ------------------------------------------------------------------ CPU (oracle)
@@ -52,12 +58,12 @@ def test_oracle_pages_match_reference_fixtures(xg):
     pages = sm_bytes(p["count"] * 4096, p["state"])
     sq = O.xxh3_batch_fixed(pages, 4096, 4088, p["count"])
     assert hexs(sq[:4]) == p["sqlite_4088"]["first"]
-    assert digest(sq) == {k: p["sqlite_4088"][k] for k in ("xor", "sum")}
+    assert digest(sq) == pin(p["sqlite_4088"])
     dq = O.xxh3_batch_fixed(pages[8:], 4096, 4088, p["count"] - 1)
-    assert digest(dq) == {k: p["diskqueue_4088_at8"][k] for k in ("xor", "sum")}
+    assert digest(dq) == pin(p["diskqueue_4088_at8"])
     idx = np.arange(0, p["count"], 16, dtype=np.uint64)
     rw = O.xxh3_batch_varlen(pages, idx * 4096, np.full(idx.size, 4096, np.uint64), seeds=idx)
-    assert digest(rw) == p["redwood_seeded_4096_every16"]
+    assert digest(rw) == pin(p["redwood_seeded_4096_every16"])
 
 
 def test_hashlittle2_known_answers(xg):
@@ -92,7 +98,7 @@ def test_oracle_varlen_configs_exact_batches(xg, name):
         seeds = S.xxh3_seeds(lengths.size) if d["kind"] == "seeds" else None
         got = O.xxh3_batch_varlen(data, offsets, lengths, seeds=seeds, threads=8)
         assert hexs(got[:64]) == d["first64"]
-        assert digest(got) == {"xor": d["xor"], "sum": d["sum"]}
+        assert digest(got) == pin(d)
 
 
 def test_oracle_against_reference_random():
@@ -142,13 +148,13 @@ def test_gpu_pages_golden(xg, cuda):
     d = dev_bytes(pages, cuda)
     sq = host(X.batch_fixed(d, 4096, 4088, p["count"]))
     assert hexs(sq[:4]) == p["sqlite_4088"]["first"]
-    assert digest(sq) == {k: p["sqlite_4088"][k] for k in ("xor", "sum")}
+    assert digest(sq) == pin(p["sqlite_4088"])
     dq = host(X.batch_fixed(d, 4096, 4088, p["count"] - 1, byte_offset=8))
-    assert digest(dq) == {k: p["diskqueue_4088_at8"][k] for k in ("xor", "sum")}
+    assert digest(dq) == pin(p["diskqueue_4088_at8"])
     idx = np.arange(0, p["count"], 16, dtype=np.int64)
     seeds = torch.tensor(idx, device=cuda)
     rw = host(X.batch_fixed(d, 4096 * 16, 4096, idx.size, seeds=seeds))
-    assert digest(rw) == p["redwood_seeded_4096_every16"]
+    assert digest(rw) == pin(p["redwood_seeded_4096_every16"])
 
 
 @pytest.mark.gpu
@@ -208,7 +214,7 @@ def test_gpu_varlen_configs_exact_batches(xg, cuda, name):
         seeds = torch.tensor(S.xxh3_seeds(lengths.size).view(np.int64), device=cuda) if d["kind"] == "seeds" else None
         got = host(X.batch_varlen(buf, d_off, d_len, seeds=seeds))
         assert hexs(got[:64]) == d["first64"], (name, d["kind"])
-        assert digest(got) == {"xor": d["xor"], "sum": d["sum"]}, (name, d["kind"])
+        assert digest(got) == pin(d), (name, d["kind"])
     del buf
 
 
