@@ -756,6 +756,63 @@ int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok
 	return fdb_diskqueue_check_pages_ws(d_pages, count, d_ok, d_bad, ws, have, stream);
 }
 
+// ---- the write side: sealing pages in place ----------------------------------
+int fdb_sqlite_seal_pages_ws(void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno, void* d_workspace,
+                             uint64_t workspace_bytes, void* stream) {
+	if (count == 0) return 0;
+	if (int rc = pages_ok(d_pages, page_size, count, d_pages, "fdb_sqlite_seal_pages: null pointer")) return rc;
+	if (!d_workspace || workspace_bytes < fdbpc::workspace_bytes(count) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_sqlite_seal_pages: workspace too small or misaligned");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	if (fdbpc::sqlite_seal(static_cast<uint8_t*>(d_pages), page_size, count, first_pgno, st->num_cus, d_workspace,
+	                       reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "fdb_sqlite_seal_pages: launch setup failed");
+	return check_launch("fdb_sqlite_seal_pages launch");
+}
+
+int fdb_sqlite_seal_pages(void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno, void* stream) {
+	if (count == 0) return 0;
+	if (int rc = pages_ok(d_pages, page_size, count, d_pages, "fdb_sqlite_seal_pages: null pointer")) return rc;
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have,
+	                              &hold))
+		return rc;
+	return fdb_sqlite_seal_pages_ws(d_pages, page_size, count, first_pgno, ws, have, stream);
+}
+
+int fdb_diskqueue_seal_pages_ws(void* d_pages, uint64_t count, void* d_workspace, uint64_t workspace_bytes,
+                                void* stream) {
+	if (count == 0) return 0;
+	if (int rc = pages_ok(d_pages, 4096, count, d_pages, "fdb_diskqueue_seal_pages: null pointer")) return rc;
+	if (!d_workspace || workspace_bytes < fdbpc::workspace_bytes(count) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_diskqueue_seal_pages: workspace too small or misaligned");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	if (fdbpc::diskqueue_seal(static_cast<uint8_t*>(d_pages), count, st->tables, st->num_cus, d_workspace,
+	                          reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "fdb_diskqueue_seal_pages: launch setup failed");
+	return check_launch("fdb_diskqueue_seal_pages launch");
+}
+
+int fdb_diskqueue_seal_pages(void* d_pages, uint64_t count, void* stream) {
+	if (count == 0) return 0;
+	if (int rc = pages_ok(d_pages, 4096, count, d_pages, "fdb_diskqueue_seal_pages: null pointer")) return rc;
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have,
+	                              &hold))
+		return rc;
+	return fdb_diskqueue_seal_pages_ws(d_pages, count, ws, have, stream);
+}
+
 // ---- FlowTransport receive verification (include/fdb_packets.h) ------------
 
 uint64_t fdb_packets_workspace_bytes(uint64_t nbuf, uint64_t max_frames, uint64_t total_bytes) {

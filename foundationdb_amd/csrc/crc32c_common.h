@@ -36,11 +36,12 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // order -- one thread writing a table word's 32 replicas -- puts all lanes of
 // a write on the same banks and cost ~15 us per launch.  The loads of a round
 // are all issued before its writes.
-__device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t) {
+// (s4: the four 256-entry word-step tables, ln: the 64 lanes' nibble tables --
+// slice4 / lane for the contiguous 64-byte lane spans, stride4 / lane_s for
+// the strided page layout)
+__device__ inline void fill_lds_src(uint32_t* lds, const uint32_t* __restrict__ s4, const uint32_t* __restrict__ ln) {
 	typedef __attribute__((address_space(1))) const uint32_t g_u32;
 	auto gl = [](const uint32_t* p) -> uint32_t { return *((g_u32*)reinterpret_cast<uintptr_t>(p)); };
-	const uint32_t* s4 = &t->slice4[0][0];
-	const uint32_t* ln = &t->lane[0][0][0];
 	constexpr uint32_t kSliceQ = 0x20000 / 16;  // quads of the two slicing regions
 	constexpr uint32_t kLaneQ = 0x8000 / 16;    // quads of the lane tables
 	constexpr uint32_t kPer = 8;
@@ -80,6 +81,9 @@ __device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t
 		}
 	}
 	__syncthreads();
+}
+__device__ inline void fill_lds_b(uint32_t* lds, const DevTables* __restrict__ t) {
+	fill_lds_src(lds, &t->slice4[0][0], &t->lane[0][0][0]);
 }
 
 // The same fill split in two for 1024-thread workgroups, so a kernel can put

@@ -32,6 +32,9 @@ struct DevTables {
 	uint32_t xinv64[65][8][16];      // x^(-8*64*j): a prefix positioned at the block end -> back to lane span j before it
 	uint32_t pow64[64][8][16];       // x^(8*64*c)
 	uint32_t pow1[64][8][16];        // x^(8*d)   (with pow64 and bpow: x^(8*len) for any len < 2^40)
+	// strided page layout (k_pages4k<..., STRIDED>): lane l's chain over the page's dwords at 4l + 256k
+	uint32_t stride4[4][256];        // [k]: byte k of a register word times x^(8*256) (one 256-byte stride)
+	uint32_t lane_s[64][8][16];      // x^(-8*4l): lane l's chain end (4l + 4096) back to the page end
 };
 
 // Build the tables on the host (crc32c_tables.cpp).

@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "crc32c_common.h"
 
 #ifndef FDBCRC_PU
@@ -81,6 +83,57 @@ __device__ __forceinline__ void unit_crc_b(const uint32_t* lds, int lane, uint32
 	}
 }
 
+// Strided page layout (STRIDED): lane l reads dword k of a page at byte
+// 4l + 256k -- 16 global_load_dword per page, each 256 contiguous bytes -- and
+// runs ONE register chain over its 16 words at a 256-byte stride:
+//     r' = (r ^ w) * x^(8*256)
+// four lookups per word from the stride4 tables, exactly as the contiguous
+// chain's x^32 step, and no permlane swizzle.  The chain ends at 4l + 4096;
+// the lane multiplies by x^(-8*4l) (lane_s) before the wave XOR.
+struct BlockS {
+	uint32_t w[16];
+};
+typedef __attribute__((address_space(1))) const uint32_t g_u32k;
+__device__ __forceinline__ void load_block_s(BlockS& b, const uint8_t* page, uint32_t lane4) {
+	const uint8_t* p = page + lane4;
+#pragma unroll
+	for (int k = 0; k < 16; ++k) b.w[k] = __builtin_nontemporal_load((g_u32k*)reinterpret_cast<uintptr_t>(p + 256 * k));
+}
+template <int U, bool WINDOW, bool RAW = WINDOW>
+__device__ __forceinline__ void unit_crc_s(const uint32_t* lds, int lane, uint32_t c4, uint32_t c_lane,
+                                           BlockS (&u)[U], const uint32_t (&s)[U], uint32_t (&crc)[U],
+                                           uint32_t h, uint32_t t) {
+	uint32_t x[U];
+	if (WINDOW) {
+		// word 0 of lane l holds bytes [4l, 4l + 4): keep those >= h and XOR in
+		// ~seed at byte h (it reaches lane h/4 and, past a word boundary, the
+		// next lane); word 15 holds [3840 + 4l, +4): keep those < 4096 - t
+		const int d = (int)h - 4 * lane;  // ~seed's byte offset inside the word
+		const uint32_t keep0 = d <= 0 ? ~0u : (d >= 4 ? 0u : ~0u << (8 * d));
+		const int cut = 256 - (int)t - 4 * lane;
+		const uint32_t keep15 = cut >= 4 ? ~0u : (cut <= 0 ? 0u : ~0u >> (8 * (4 - cut)));
+#pragma unroll
+		for (int j = 0; j < U; ++j) {
+			const uint32_t sd = ~s[j];
+			const uint32_t inj = (d > -4 && d < 4) ? (d >= 0 ? sd << (8 * d) : sd >> (-8 * d)) : 0u;
+			x[j] = (u[j].w[0] & keep0) ^ inj;
+			u[j].w[15] &= keep15;
+		}
+	} else {
+#pragma unroll
+		for (int j = 0; j < U; ++j) x[j] = (lane == 0 ? ~s[j] : 0u) ^ u[j].w[0];
+	}
+#pragma unroll
+	for (int w = 0; w < 16; ++w)
+#pragma unroll
+		for (int j = 0; j < U; ++j) x[j] = word_step4_next(lds, x[j], w < 15 ? u[j].w[w + 1] : 0u, c4);
+#pragma unroll
+	for (int j = 0; j < U; ++j) {
+		const uint32_t r = wave_xor(mul_nibbles(lds, x[j], c_lane));
+		crc[j] = RAW ? r : ~r;
+	}
+}
+
 // Lane-parallel multiply of a per-lane value by a constant whose nibble tables
 // live in global memory (8 gathers, L2-resident).
 __device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t v) {
@@ -117,7 +170,10 @@ __device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t
 // development: per-wave start / end timestamps of k_pages4k and k_bigblocks (s_memrealtime, 100 MHz)
 __device__ uint64_t g_bt[16384][4];
 #endif
-template <int U, bool WINDOW = false, bool LIST = false, bool PAIR = false>
+#ifndef FDBCRC_STRIDED
+#define FDBCRC_STRIDED 0
+#endif
+template <int U, bool WINDOW = false, bool LIST = false, bool PAIR = false, bool STRIDED = FDBCRC_STRIDED>
 __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ base, uint64_t stride, uint64_t count,
                                                   uint32_t seed, const uint32_t* __restrict__ seeds,
                                                   uint32_t* __restrict__ out, const DevTables* __restrict__ tabs,
@@ -155,9 +211,22 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		if (PAIR) return base + (j >> 1) * stride + (j & 1) * 4096;
 		return base + (LIST ? (uint64_t)idx[j] : j) * stride;
 	};
-	auto load_u = [&](Block (&u)[U], uint64_t i0) {
+	typedef typename std::conditional<STRIDED, BlockS, Block>::type Blk;
+	const uint32_t lane4 = 4u * (uint32_t)c.lane;
+	auto load_u = [&](Blk (&u)[U], uint64_t i0) {
 #pragma unroll
-		for (int j = 0; j < U; ++j) load_block(u[j], page(i0 + j), c.ld_off);
+		for (int j = 0; j < U; ++j) {
+			if constexpr (STRIDED)
+				load_block_s(u[j], page(i0 + j), lane4);
+			else
+				load_block(u[j], page(i0 + j), c.ld_off);
+		}
+	};
+	auto unit = [&](Blk (&u)[U], const uint32_t (&sd)[U], uint32_t (&crc)[U]) {
+		if constexpr (STRIDED)
+			unit_crc_s<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u, sd, crc, h, t);
+		else
+			unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u, sd, crc, h, t);
 	};
 	auto clampg = [&](uint64_t g) { return g < g1 ? g : ngrab; };  // ngrab: nothing left
 	auto request = [&]() -> uint32_t {
@@ -177,9 +246,12 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 	uint64_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
 	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
 	uint32_t sdA = seed_of(gA), sdB = seed_of(gB);
-	Block u0[U], u1[U];
+	Blk u0[U], u1[U];
 	load_u(u0, gA * C);  // in flight during the LDS fill
-	fill_lds_b(lds, tabs);
+	if constexpr (STRIDED)
+		fill_lds_src(lds, &tabs->stride4[0][0], &tabs->lane_s[0][0][0]);
+	else
+		fill_lds_b(lds, tabs);
 	uint32_t mine = 0;     // lane 2U*f + j: checksum of page j of the group's f-th grab
 	uint64_t myi = ~0ull;  // ... and its index in the batch (~0: none)
 	uint32_t f = 0;        // grabs in the current store group
@@ -233,7 +305,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int j = 0; j < U; ++j) sd[j] = rdlane(sdA, j);
-		unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u0, sd, crc, h, t);
+		unit(u0, sd, crc);
 #pragma unroll
 		for (int j = 0; j < U; ++j) mine = (uint32_t)c.lane == l0 + j ? crc[j] : mine;
 		__builtin_amdgcn_sched_barrier(0);
@@ -241,7 +313,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int j = 0; j < U; ++j) sd[j] = rdlane(sdA, U + j);
-		unit_crc_b<U, WINDOW, WINDOW || PAIR>(lds, c.lane, c4, c_lane, u1, sd, crc, h, t);
+		unit(u1, sd, crc);
 #pragma unroll
 		for (int j = 0; j < U; ++j) mine = (uint32_t)c.lane == l0 + U + j ? crc[j] : mine;
 		__builtin_amdgcn_sched_barrier(0);

@@ -41,6 +41,8 @@ void build_dev_tables(DevTables* t) {
 		mul_tables_nibble(xpow8(64u * c), t->pow64[c]);
 		mul_tables_nibble(xpow8(c), t->pow1[c]);
 	}
+	mul_tables_byte(xpow8(256), t->stride4);
+	for (int l = 0; l < 64; ++l) mul_tables_nibble(xpow8_inv(4u * l), t->lane_s[l]);
 	for (int m = 0; m < 64; ++m) {
 		// x^(8*2^m) by repeated squaring of x^8
 		uint32_t c = kOne >> 8;

@@ -515,6 +515,76 @@ __global__ __launch_bounds__(256) void k_dq_final(const uint8_t* __restrict__ pa
 }
 
 // ---------------------------------------------------------------------------
+// Write side: sealing pages in place
+// ---------------------------------------------------------------------------
+// SQLite checksum(write = true) (KeyValueStoreSQLite.cpp:107-116): the trailer
+// of page i = XXH3 split part1 = (h >> 32) & 0xffffff, part2 = (uint32_t)h, as
+// one little-endian u64 at [ps - 8, ps) (8-byte aligned: pages 16-byte aligned).
+__global__ __launch_bounds__(256) void k_sq_seal(uint8_t* __restrict__ pages, uint64_t ps, uint64_t count,
+                                                 const uint64_t* __restrict__ xxh_out) {
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t h = xxh_out[i];
+		*reinterpret_cast<uint64_t*>(pages + i * ps + ps - 8) = ((h >> 32) & 0x00ffffffull) | (h << 32);
+	}
+}
+
+// DiskQueue Page::updateHash (DiskQueue.cpp:1089-1105) by implementationVersion:
+// V1 -> list a (CRC-32C of [4, 4096) into hash32), V0 -> list c (hashlittle2
+// UID), V2 and every other version -> list b (the switch's default: XXH3 of
+// [8, 4096) into hash64).
+__global__ __launch_bounds__(kCB) void k_dq_seal_classify(const uint8_t* __restrict__ pages, uint64_t count,
+                                                          uint32_t* v1_l, uint32_t* v2_l, uint32_t* v0_l,
+                                                          unsigned long long* __restrict__ ctr) {
+	__shared__ Stage<3> S;
+	stage_init(S);
+	const uint64_t i0 = (uint64_t)blockIdx.x * kSpan;
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; ++k) {
+		const uint64_t i = i0 + k * kCB + threadIdx.x;
+		const bool in = i < count;
+		const uint32_t ver = in ? (ld32(pages + i * 4096 + 8) >> 16) : 0xFFFFu;
+		stage_push(S, 0, in && ver == 1, (uint32_t)i);
+		stage_push(S, 1, in && ver != 0 && ver != 1, (uint32_t)i);
+		stage_push(S, 2, in && ver == 0, (uint32_t)i);
+	}
+	uint32_t* const lists[3] = {v1_l, v2_l, v0_l};
+	stage_flush(S, lists, ctr);
+}
+
+__global__ __launch_bounds__(kCB) void k_dq_seal_write(uint8_t* __restrict__ pages, const uint32_t* __restrict__ v1_l,
+                                                       const uint32_t* __restrict__ v2_l,
+                                                       const unsigned long long* __restrict__ ctr,
+                                                       const uint32_t* __restrict__ crc_out,
+                                                       const uint64_t* __restrict__ xxh_out) {
+	const uint64_t n1 = ctr[0], n2 = ctr[1];
+	for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < (n1 > n2 ? n1 : n2);
+	     j += (uint64_t)gridDim.x * blockDim.x) {
+		if (j < n1) *reinterpret_cast<uint32_t*>(pages + (uint64_t)v1_l[j] * 4096) = crc_out[j];
+		if (j < n2) *reinterpret_cast<uint64_t*>(pages + (uint64_t)v2_l[j] * 4096) = xxh_out[j];
+	}
+}
+
+// V0 pages: hash = UID(c << 32 | b, 0xFDB) from hashlittle2 over [16, 4096)
+// (checksum_hashlittle2, DiskQueue.cpp:1077-1082); bytes 8..15 become 0xFDB
+// (magic 0x0FDB, implementationVersion 0: the UID overlays them).
+__global__ __launch_bounds__(256) void k_dq_seal_v0(uint8_t* __restrict__ pages, const uint32_t* __restrict__ v0_l,
+                                                    const unsigned long long* __restrict__ ctr) {
+	const uint64_t n = ctr[2];
+	if ((uint64_t)blockIdx.x * 4 * kL3PerWave >= n) return;
+	__shared__ uint32_t lw[4][64 * kStW];
+	const uint32_t lane = threadIdx.x & 63;
+	const uint64_t j0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kL3PerWave;
+	const uint64_t j = j0 + lane % kL3PerWave;
+	if (j0 < n) {  // wave-uniform (see k_sq_final)
+		const uint64_t i = v0_l[j < n ? j : n - 1];
+		uint8_t* p = pages + i * 4096;
+		uint32_t c = 0x12345678u, b = 0xbeefabcdu;
+		hashlittle2_core<true>(p + 16, 4080, &c, &b, lw[threadIdx.x >> 6]);
+		if (j < n && lane < kL3PerWave) *reinterpret_cast<u32x4*>(p) = u32x4{b, c, 0xFDBu, 0u};
+	}
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 uint64_t workspace_bytes(uint64_t count) {
@@ -613,6 +683,60 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	                                           w.trl);
 	k_dq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ok, w.ctr);
 	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
+	return 0;
+}
+
+// Seal every page of the batch in place (codec op 6 / 7, KeyValueStoreSQLite.cpp:203-244).
+int sqlite_seal(uint8_t* pages, uint64_t ps, uint64_t count, uint32_t first_pgno, int num_cus, void* ws,
+                hipStream_t s) {
+	const Ws w = carve(ws, count);
+	const unsigned g = blocks(count) < 4096 ? blocks(count) : 4096;
+	// page 1 of a database with pages over SQLITE_DEFAULT_PAGE_SIZE is first
+	// sealed as a 1024-byte page (:221-224); its trailer at [1016, 1024) lies in
+	// the full page's hashed bytes, so this goes first (stream order)
+	const uint64_t i1 = (uint32_t)(1u - first_pgno);
+	if (i1 < count && ps > 1024) {
+		uint64_t* h1 = reinterpret_cast<uint64_t*>(w.ctr);  // (the counters are unused here)
+		fdbxxh::XxhParams P{};
+		P.base = pages + i1 * ps;
+		P.stride = 1024;
+		P.length = 1016;
+		P.count = 1;
+		P.out = h1;
+		if (fdbxxh::launch_xxh3(P, num_cus, nullptr, s)) return -1;
+		k_sq_seal<<<1, 64, 0, s>>>(pages + i1 * ps, 1024, 1, h1);
+	}
+	fdbxxh::XxhParams P{};
+	P.base = pages;
+	P.stride = ps;
+	P.length = ps - 8;
+	P.count = count;
+	P.out = w.xxh_out;
+	if (fdbxxh::launch_xxh3(P, num_cus, nullptr, s)) return -1;
+	k_sq_seal<<<g, 256, 0, s>>>(pages, ps, count, w.xxh_out);
+	return 0;
+}
+
+int diskqueue_seal(uint8_t* pages, uint64_t count, const fdbcrc::DevTables* tabs, int num_cus, void* ws,
+                   hipStream_t s) {
+	const Ws w = carve(ws, count);
+	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
+	k_dq_seal_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, w.list_a, w.list_b, w.list_c, w.ctr);
+	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
+	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
+	if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n1, count, 4, 0, 0xFDBEEFDBu, w.crc_out, tabs, num_cus, s))
+		return -1;
+	fdbxxh::XxhParams P{};
+	P.base = pages + 8;
+	P.stride = 4096;
+	P.length = 4088;
+	P.count = count;
+	P.out = w.xxh_out;
+	P.idx = w.list_b;
+	P.d_count = n2;
+	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
+	k_dq_seal_write<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out);
+	k_dq_seal_v0<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, w.ctr);
 	return 0;
 }
 

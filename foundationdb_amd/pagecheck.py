@@ -1,9 +1,10 @@
-"""Python host mirror of the batched page verifiers (include/fdb_pagecheck.h).
+"""Python host mirror of the batched page verifiers and sealers (include/fdb_pagecheck.h).
 
 Reference interfaces: PageChecksumCodec::checksum(pgno, page, pageLen,
-write=false) (fdbserver/kvstore/KeyValueStoreSQLite.cpp:100-201) and
-DiskQueue Page::checkHash (fdbserver/kvstore/DiskQueue.cpp:1047-1120), run
-over whole batches of device-resident pages.  No CPU fallback.
+write=false/true) (fdbserver/kvstore/KeyValueStoreSQLite.cpp:100-201, the
+codec's page writes :203-244) and DiskQueue Page::checkHash / updateHash
+(fdbserver/kvstore/DiskQueue.cpp:1047-1120), run over whole batches of
+device-resident pages.  No CPU fallback.
 """
 import ctypes
 
@@ -27,6 +28,10 @@ def _lib():
         L.fdb_diskqueue_check_pages.argtypes = [vp, u64, vp, vp, vp]
         L.fdb_pagecheck_workspace_bytes.restype = u64
         L.fdb_pagecheck_workspace_bytes.argtypes = [u64]
+        L.fdb_sqlite_seal_pages.restype = ctypes.c_int
+        L.fdb_sqlite_seal_pages.argtypes = [vp, u64, u64, u32, vp]
+        L.fdb_diskqueue_seal_pages.restype = ctypes.c_int
+        L.fdb_diskqueue_seal_pages.argtypes = [vp, u64, vp]
         _bound = True
     return L
 
@@ -78,3 +83,33 @@ def diskqueue_check_pages(pages, count=None, stream=None, ok=None, bad=None):
         rc = _lib().fdb_diskqueue_check_pages(_vp(pages), count, _vp(ok), _vp(bad), _stream_handle(stream))
     _check(rc, "fdb_diskqueue_check_pages")
     return ok, bad
+
+
+def _page_count(pages, page_size, count, who):
+    _require_device(pages, "pages")
+    nbytes = pages.numel() * pages.element_size()
+    count = nbytes // page_size if count is None else int(count)
+    if count * page_size > nbytes:
+        raise CRC32CError(f"{who}: pages extend past the tensor")
+    return count
+
+
+def sqlite_seal_pages(pages, page_size, count=None, first_pgno=1, stream=None):
+    """Seals a batch of SQLite pages in place as the codec's page writes do
+    (checksum(write = true): the XXH3 trailer; page 1 also at 1024 bytes when
+    page_size > 1024).  Asynchronous on `stream`."""
+    count = _page_count(pages, page_size, count, "sqlite_seal_pages")
+    with torch.cuda.device(pages.device):
+        rc = _lib().fdb_sqlite_seal_pages(_vp(pages), page_size, count, first_pgno, _stream_handle(stream))
+    _check(rc, "fdb_sqlite_seal_pages")
+    return pages
+
+
+def diskqueue_seal_pages(pages, count=None, stream=None):
+    """Page::updateHash over a batch of 4 KiB DiskQueue pages, in place, by
+    each page's implementationVersion.  Asynchronous on `stream`."""
+    count = _page_count(pages, 4096, count, "diskqueue_seal_pages")
+    with torch.cuda.device(pages.device):
+        rc = _lib().fdb_diskqueue_seal_pages(_vp(pages), count, _stream_handle(stream))
+    _check(rc, "fdb_diskqueue_seal_pages")
+    return pages

@@ -49,6 +49,29 @@ int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t
 int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad,
                                  void* d_workspace, uint64_t workspace_bytes, void* stream);
 
+/* The write side, in place.  fdb_sqlite_seal_pages replaces the codec's page
+ * writes (op 6 db page / op 7 journal page, KeyValueStoreSQLite.cpp:203-244)
+ * over a batch: every page's trailer [page_size-8, page_size) becomes
+ * PageChecksumCodec::checksum(write = true) (:107-116), XXH3_64bits of
+ * [0, page_size-8) split part1 = (h >> 32) & 0xffffff, part2 = (uint32_t)h;
+ * the page numbered 1 (first_pgno + i == 1) is first sealed as a 1024-byte
+ * page when page_size > 1024 (SQLITE_DEFAULT_PAGE_SIZE, :221-224), exactly as
+ * the codec does, so it verifies at both sizes.
+ * fdb_diskqueue_seal_pages replaces Page::updateHash (DiskQueue.cpp:1089-1105,
+ * called at commit, :955-965) over 4096-byte pages by implementationVersion:
+ * V0 the hashlittle2 UID (bytes 8..15 become 0xFDB), V1 hash32 =
+ * crc32c_append(0xfdbeefdb, page + 4, 4092), V2 -- and, as the reference's
+ * switch default, every other version -- hash64 = XXH3_64bits(page + 8, 4088).
+ * (checkHash then rejects versions above 2, as the reference does.)
+ * Same page constraints as the verifiers; the _ws forms take a workspace of
+ * fdb_pagecheck_workspace_bytes(count). */
+int fdb_sqlite_seal_pages(void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno, void* stream);
+int fdb_sqlite_seal_pages_ws(void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno, void* d_workspace,
+                             uint64_t workspace_bytes, void* stream);
+int fdb_diskqueue_seal_pages(void* d_pages, uint64_t count, void* stream);
+int fdb_diskqueue_seal_pages_ws(void* d_pages, uint64_t count, void* d_workspace, uint64_t workspace_bytes,
+                                void* stream);
+
 /* Host-resident pages (a file scan reading pages from disk, as
  * checkAllPageChecksums does, KeyValueStoreSQLite.cpp:1378-1470, or a DiskQueue
  * recovery reading page runs, DiskQueue.cpp:1230-1290): the same verification

@@ -342,6 +342,10 @@ def pagecheck_reference():
         L.ref_sqlite_verify_pages.argtypes = [vp, u64, u64, ctypes.c_uint32, vp]
         L.ref_diskqueue_check_pages.restype = u64
         L.ref_diskqueue_check_pages.argtypes = [vp, u64, vp]
+        L.ref_sqlite_seal_pages.restype = None
+        L.ref_sqlite_seal_pages.argtypes = [vp, u64, u64, ctypes.c_uint32]
+        L.ref_diskqueue_seal_pages.restype = None
+        L.ref_diskqueue_seal_pages.argtypes = [vp, u64]
         _pcref = L
     return _pcref
 
@@ -362,6 +366,23 @@ def ref_diskqueue_check_pages(pages, count):
     ok = np.zeros(count, np.uint8)
     bad = pagecheck_reference().ref_diskqueue_check_pages(pages.ctypes.data, count, ok.ctypes.data)
     return ok, int(bad)
+
+
+def ref_sqlite_seal_pages(pages, page_size, count, first_pgno=1):
+    """A sealed copy of `pages`: the codec's page writes (op 6 / 7) composed from
+    the reference's XXH3_64bits (oracle/ref_pagecheck.c)."""
+    out = np.array(np.ascontiguousarray(pages).view(np.uint8).reshape(-1), copy=True)
+    assert count * page_size <= out.nbytes
+    pagecheck_reference().ref_sqlite_seal_pages(out.ctypes.data, page_size, count, first_pgno)
+    return out
+
+
+def ref_diskqueue_seal_pages(pages, count):
+    """A sealed copy of `pages`: Page::updateHash by version from the reference primitives."""
+    out = np.array(np.ascontiguousarray(pages).view(np.uint8).reshape(-1), copy=True)
+    assert count * 4096 <= out.nbytes
+    pagecheck_reference().ref_diskqueue_seal_pages(out.ctypes.data, count)
+    return out
 
 
 # ---------------------------------------------------------------- page formats
@@ -409,6 +430,31 @@ def diskqueue_hash(page, version):
     if version == 1:
         return crc32c(0xFDBEEFDB, page[4:]).to_bytes(4, "little") + page[4:16]
     return xxh3_64(page[8:]).to_bytes(8, "little") + page[8:16]
+
+
+def sqlite_seal_pages(pages, page_size, count, first_pgno=1):
+    """The codec's page writes (KeyValueStoreSQLite.cpp:203-244) on a copy of
+    `pages`, from our XXH3 restatement: page 1 with page_size > 1024
+    (SQLITE_DEFAULT_PAGE_SIZE) first sealed as a 1024-byte page (:221-224),
+    then every page's trailer = sqlite_trailer_xxh3 (checksum(write = true), :107-116)."""
+    out = np.array(np.ascontiguousarray(pages).view(np.uint8).reshape(-1)[:count * page_size], copy=True)
+    for i in range(count):
+        pg = out[i * page_size:(i + 1) * page_size]
+        if first_pgno + i == 1 and page_size > 1024:
+            pg[1016:1024] = np.frombuffer(sqlite_trailer_xxh3(pg[:1024]), np.uint8)
+        pg[-8:] = np.frombuffer(sqlite_trailer_xxh3(pg), np.uint8)
+    return out
+
+
+def diskqueue_seal_pages(pages, count):
+    """Page::updateHash (DiskQueue.cpp:1089-1105) on a copy of `pages` by
+    implementationVersion; versions other than 0 and 1 take XXH3 (the switch's default)."""
+    out = np.array(np.ascontiguousarray(pages).view(np.uint8).reshape(-1)[:count * 4096], copy=True)
+    for i in range(count):
+        pg = out[i * 4096:(i + 1) * 4096]
+        ver = int.from_bytes(bytes(pg[10:12]), "little")
+        pg[:16] = np.frombuffer(diskqueue_hash(pg, ver if ver <= 1 else 2), np.uint8)
+    return out
 
 
 def diskqueue_check_page(page):

@@ -15,6 +15,16 @@
  * (fdbserver/kvstore/DiskQueue.cpp:1077-1120) by implementationVersion.
  * Both return the number of bad pages (SQLiteDB::checkAllPageChecksums,
  * KeyValueStoreSQLite.cpp:1378-1470, counts them).
+ *
+ * The write side, in place: ref_sqlite_seal_pages restates the codec's page
+ * writes (op 6 / 7, KeyValueStoreSQLite.cpp:203-244): page 1 of a database
+ * whose page size exceeds SQLITE_DEFAULT_PAGE_SIZE (1024) is first sealed as
+ * a 1024-byte page (:221-224), then every page gets checksum(write = true)
+ * (:107-116): XXH3_64bits of [0, pageLen - 8), part1 = (h >> 32) & 0xffffff,
+ * part2 = (uint32_t)h.  ref_diskqueue_seal_pages restates Page::updateHash
+ * (DiskQueue.cpp:1089-1105) by implementationVersion: V0 the hashlittle2 UID,
+ * V1 hash32 = crc32c_append(0xfdbeefdb, &_unused, 4092), V2 and every other
+ * version hash64 = XXH3_64bits(&magic, 4088).
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -33,6 +43,42 @@ static uint64_t rd64(const uint8_t* p) {
 	uint64_t v;
 	memcpy(&v, p, 8);
 	return v;
+}
+
+static void wr32(uint8_t* p, uint32_t v) { memcpy(p, &v, 4); }
+static void wr64(uint8_t* p, uint64_t v) { memcpy(p, &v, 8); }
+
+static void sqlite_seal(uint8_t* page, uint64_t page_len) {
+	const size_t n = (size_t)page_len - 8;
+	const uint64_t h = XXH3_64bits(page, n);
+	wr32(page + n, (uint32_t)((h >> 32) & 0x00ffffffu));
+	wr32(page + n + 4, (uint32_t)h);
+}
+
+void ref_sqlite_seal_pages(uint8_t* pages, uint64_t page_size, uint64_t count, uint32_t first_pgno) {
+	for (uint64_t i = 0; i < count; ++i) {
+		uint8_t* page = pages + i * page_size;
+		if (first_pgno + (uint32_t)i == 1 && page_size > 1024) sqlite_seal(page, 1024);
+		sqlite_seal(page, page_size);
+	}
+}
+
+void ref_diskqueue_seal_pages(uint8_t* pages, uint64_t count) {
+	for (uint64_t i = 0; i < count; ++i) {
+		uint8_t* page = pages + 4096 * i;
+		uint16_t ver;
+		memcpy(&ver, page + 10, 2);
+		if (ver == 0) {
+			uint32_t part[2] = {0x12345678u, 0xbeefabcdu};
+			hashlittle2(page + 16, 4096 - 16, &part[0], &part[1]);
+			wr64(page, ((uint64_t)part[0] << 32) | part[1]);
+			wr64(page + 8, 0xFDBull);
+		} else if (ver == 1) {
+			wr32(page, crc32c_append(0xfdbeefdbu, page + 4, 4096 - 4));
+		} else {
+			wr64(page, XXH3_64bits(page + 8, 4096 - 8));
+		}
+	}
 }
 
 static int sqlite_check(const uint8_t* page, uint64_t page_size, uint32_t pgno) {

@@ -182,3 +182,94 @@ def test_gpu_host_resident_verifiers(cuda, pinned):
     s0, b0 = pipe.sqlite_verify_pages(hp, 4096, count=0)
     assert s0.size == 0 and int(b0[0]) == 0
     pipe.close()
+
+
+# ------------------------------------------------------------------ write side
+
+def _dq_versions(n, seed):
+    """4 KiB pages with implementationVersion 0 / 1 / 2 and a few unknown ones."""
+    rng = np.random.default_rng(seed)
+    pages = sm_bytes(n * 4096, seed).reshape(n, 4096)
+    vers = rng.choice([0, 1, 2, 2, 3, 0xFFFF], n)
+    for i in range(n):
+        pages[i, 10:12] = np.frombuffer(int(vers[i]).to_bytes(2, "little"), np.uint8)
+    return pages, vers
+
+
+@pytest.mark.skipif(not O.pagecheck_reference_available(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("page_size", [512, 1024, 4096, 8192])
+def test_oracle_seal_matches_reference_composition(page_size):
+    """The seal restatements (oracle.sqlite_seal_pages / diskqueue_seal_pages)
+    write the same bytes as the codec's page writes and Page::updateHash
+    composed from the reference's own primitives (oracle/ref_pagecheck.c), and
+    the sealed pages verify (status 2 for SQLite; DiskQueue V0-V2 ok, unknown
+    versions rejected by checkHash although updateHash sealed them, as in the
+    reference).  Batches starting at page 0, 1 and 2 cover page 1's extra
+    1024-byte seal."""
+    n = 24
+    pages = sm_bytes(n * page_size, page_size + 3)
+    for first in (0, 1, 2):
+        want = O.ref_sqlite_seal_pages(pages, page_size, n, first)
+        assert np.array_equal(O.sqlite_seal_pages(pages, page_size, n, first), want)
+        st, bad = O.ref_sqlite_verify_pages(want, page_size, n, first)
+        assert bad == 0 and (st == 2).all()
+        i1 = 1 - first
+        if 0 <= i1 < n and page_size > 1024:  # page 1 also verifies as a 1024-byte page
+            p1 = want[i1 * page_size:i1 * page_size + 1024]
+            assert O.sqlite_verify_page(p1, 1) == 2
+    dq, vers = _dq_versions(64, page_size)
+    want = O.ref_diskqueue_seal_pages(dq, 64)
+    assert np.array_equal(O.diskqueue_seal_pages(dq, 64), want)
+    ok, _ = O.ref_diskqueue_check_pages(want, 64)
+    assert np.array_equal(ok, (vers <= 2).astype(np.uint8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("page_size", [512, 4096, 8192, 65536])
+def test_gpu_sqlite_seal_pages(cuda, page_size):
+    """fdb_sqlite_seal_pages writes exactly the bytes the reference's codec
+    composition writes (byte for byte, every page, first_pgno 0 / 1 / 5), and
+    the verifier then accepts every page as XXH3-sealed."""
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    n = {512: 3000, 4096: 2000, 8192: 700, 65536: 40}[page_size]
+    pages = sm_bytes(n * page_size, page_size + 17)
+    for first in (0, 1, 5):
+        want = O.ref_sqlite_seal_pages(pages, page_size, n, first) if O.pagecheck_reference_available() else \
+            O.sqlite_seal_pages(pages, page_size, n, first)
+        d = torch.from_numpy(pages.copy()).to(cuda)
+        PC.sqlite_seal_pages(d, page_size, first_pgno=first)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy()
+        assert np.array_equal(got, want), (page_size, first, int(np.flatnonzero(got != want)[0]))
+        status, bad = PC.sqlite_verify_pages(d, page_size, first_pgno=first)
+        assert (status.cpu().numpy() == 2).all() and int(bad.cpu().numpy().view(np.uint64)[0]) == 0
+        PC.sqlite_seal_pages(d, page_size, first_pgno=first)  # sealing again changes nothing
+        assert np.array_equal(d.cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+def test_gpu_diskqueue_seal_pages(cuda):
+    """fdb_diskqueue_seal_pages = Page::updateHash per page (V0 / V1 / V2 and
+    unknown versions, which take XXH3), byte for byte against the reference
+    composition; seal-then-check accepts every V0-V2 page."""
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    n = 3000
+    dq, vers = _dq_versions(n, 21)
+    want = O.ref_diskqueue_seal_pages(dq, n) if O.pagecheck_reference_available() else O.diskqueue_seal_pages(dq, n)
+    d = torch.from_numpy(dq.reshape(-1).copy()).to(cuda)
+    PC.diskqueue_seal_pages(d)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    assert np.array_equal(got, want.reshape(-1))
+    ok, bad = PC.diskqueue_check_pages(d)
+    assert np.array_equal(ok.cpu().numpy(), (vers <= 2).astype(np.uint8))
+    assert int(bad.cpu().numpy().view(np.uint64)[0]) == int((vers > 2).sum())
+    # one kind only, and a single page
+    for v in (0, 1, 2):
+        one = dq[:5].copy()
+        one[:, 10:12] = np.frombuffer(v.to_bytes(2, "little"), np.uint8)
+        d1 = torch.from_numpy(one.reshape(-1).copy()).to(cuda)
+        PC.diskqueue_seal_pages(d1)
+        assert np.array_equal(d1.cpu().numpy(), O.diskqueue_seal_pages(one, 5))

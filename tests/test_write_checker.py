@@ -5,6 +5,7 @@ and lost-write data, syncs, truncates, an exhausted history budget."""
 import numpy as np
 import pytest
 
+from oracle import oracle as O
 from oracle import write_checker_model as M
 
 FILE_PAGES = 96
@@ -124,6 +125,97 @@ def test_sweep_order_and_batched_verification():
     assert st["fail"] == 1 and st["succeed"] == 18
     assert c.sweep_pages(100)[0] == 7  # the lost write stays in the history
     c.close()
+
+
+class _LRU2:
+    """The reference test's second LRU (fdbrpc/AsyncFileWriteChecker.cpp:31-161):
+    most recent at the head, truncate(n) drops pages [n, maxFullPagePlusOne)."""
+
+    def __init__(self):
+        from collections import OrderedDict
+        self.m = OrderedDict()  # least recently used first
+        self.max_plus_one = 0
+
+    def update(self, page, info):
+        self.m.pop(page, None)
+        self.m[page] = info
+        self.max_plus_one = max(self.max_plus_one, page + 1)
+
+    def remove(self, page):
+        self.m.pop(page, None)
+
+    def truncate(self, n):
+        for i in range(n, self.max_plus_one):
+            self.remove(i)
+        self.max_plus_one = min(self.max_plus_one, n)
+
+    def least_recently_used(self):
+        return next(iter(self.m)) if self.m else 0
+
+
+def test_reference_lru_sequence():
+    """The reference's own LRU test (/fdbrpc/AsyncFileWriteChecker/LRU,
+    fdbrpc/AsyncFileWriteChecker.cpp:164-229) replayed through the checker's
+    C ABI and the line-by-line model: 1000 steps, each an update (p > 0.5 or
+    empty history), a removal (p < 0.45) or a truncate, pages in [1, 1000).
+    update(page, info) is a write of 8192 bytes at (page - 1) * 4096 (it
+    records exactly that page: updateChecksumHistory's pageEnd leaves out the
+    last full page), with fresh random bytes so the checksum changes each
+    time; remove(page) is a sync followed by a read of the page's bytes (a
+    synced page that verifies leaves the history, verifyChecksum :244-275);
+    truncate(page) is truncate(page * 4096) (maxFullPage = size / 4096,
+    :76-84).  After every step: existence and (checksum, timestamp) of the
+    pages touched, and the least recently used page (fdb_wc_sweep_pages) with
+    its entry, as the reference compares them against LRU2."""
+    import foundationdb_amd.write_checker as W
+    rng = np.random.default_rng(20240518)
+    W.reset_budget()
+    M.Budget.value = None
+    nat = W.WriteChecker(1 << 20, gpu_threshold=0)
+    model = M.WriteCheckerModel(1 << 20)
+    lru2 = _LRU2()
+    content = {}  # the bytes each recorded page holds on "disk"
+    limit, t = 1000, 1
+    for _ in range(1000):
+        t += 1
+        r = rng.random()
+        if not lru2.m or r > 0.5:  # add / update
+            page = int(rng.integers(1, limit))
+            if page in lru2.m:
+                assert nat.history_entry(page) == lru2.m[page]
+            data = rng.integers(0, 256, 8192, dtype=np.uint8)
+            off = (page - 1) * 4096
+            assert nat.write(data, off, t) == [page]
+            nat.write_done([page])
+            model.write_done(model.write(data, off, t))
+            content[page] = data
+            lru2.update(page, (O.crc32c(M.SEED, data[:4096].tobytes()), t))
+            assert nat.history_entry(page) == lru2.m[page] == model.history()[page]
+        elif r < 0.45:  # remove
+            page = list(lru2.m)[int(rng.integers(0, len(lru2.m)))]
+            assert nat.history_entry(page) == lru2.m[page]
+            nat.sync(t)
+            model.sync(t)
+            t += 1
+            assert nat.read(content[page], (page - 1) * 4096) == 0
+            model.read(content[page], (page - 1) * 4096)
+            lru2.remove(page)
+            assert nat.history_entry(page) is None and page not in model.history()
+        else:  # truncate
+            keys = list(lru2.m)
+            page, page2 = (keys[int(rng.integers(0, len(keys)))] for _ in range(2))
+            nat.truncate(page * 4096)
+            model.truncate(page * 4096)
+            lru2.truncate(page)
+            if page2 >= page:
+                assert nat.history_entry(page2) is None and page2 not in lru2.m
+        assert nat.stats()["history"] == len(lru2.m) == model.lru.size()
+        if lru2.m:
+            lru_page = lru2.least_recently_used()
+            assert nat.sweep_pages(1) == [lru_page] == model.sweep_pages(1)
+            assert nat.history_entry(lru_page) == lru2.m[lru_page]
+    nat.close()
+    model.close()
 
 
 @pytest.mark.gpu
