@@ -865,7 +865,7 @@ int fdb_packets_frames(const void* d_workspace, uint64_t nbuf, uint64_t max_fram
 	void* xws = nullptr;
 	uint64_t xb = 0;
 	const fdbpkt::Ws w = fdbpkt::carve(const_cast<void*>(d_workspace), nbuf, max_frames, ~0ull >> 1, &xws, &xb);
-	if (fdbpkt::launch_frames(w, d_frames, capacity, d_nframes, reinterpret_cast<hipStream_t>(stream)))
+	if (fdbpkt::launch_frames(w, nbuf, d_frames, capacity, d_nframes, reinterpret_cast<hipStream_t>(stream)))
 		return fail(FDB_CRC32C_EHIP, "fdb_packets_frames: launch setup failed");
 	return check_launch("fdb_packets_frames launch");
 }

@@ -10,7 +10,8 @@ namespace fdbpkt {
 // Workspace: [0] the frame counter, then per buffer the walk's results and the
 // first failing frame, per frame slot the list the walk appends to.
 struct Ws {
-	uint64_t* hdr;       // [0]: frames appended (may exceed cap: then some were not recorded)
+	uint64_t* hdr;       // [0]: frames appended (may exceed cap: then some were not recorded);
+	                     // [1], [2]: nbuf and max_frames of the batch (k_pkt_walk)
 	uint32_t* walked;    // per buffer: frames walked
 	int32_t* wstat;      // ... why the walk stopped
 	uint32_t* bad_ord;   // ... first frame whose checksum failed (~0: none)
@@ -37,6 +38,6 @@ Ws carve(void* ws, uint64_t nbuf, uint64_t max_frames, uint64_t ws_bytes, void**
 int launch_verify(const uint8_t* base, const uint64_t* boff, const uint64_t* blen, uint64_t nbuf, int checksum,
                   uint32_t limit, uint64_t max_frames, fdb_packet_result* out, void* ws, uint64_t ws_bytes,
                   int num_cus, hipStream_t s);
-int launch_frames(const Ws& w, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n, hipStream_t s);
+int launch_frames(const Ws& w, uint64_t nbuf, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n, hipStream_t s);
 
 }  // namespace fdbpkt

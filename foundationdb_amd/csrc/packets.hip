@@ -202,6 +202,10 @@ __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
 		for (int s = 0; s < kWalkStage; ++s) step(s);
 		flush();
 	}
+	if (b == 0) {  // the batch's shape, for fdb_packets_frames' check of its arguments
+		P.w.hdr[1] = P.nbuf;
+		P.w.hdr[2] = P.w.cap;
+	}
 	if (in) {
 		P.w.walked[b] = ord;
 		P.w.wstat[b] = overflow ? FDB_PACKET_ECAPACITY : status;
@@ -243,7 +247,12 @@ __global__ __launch_bounds__(256) void k_pkt_final(CheckP P) {
 	P.out[b] = r;
 }
 
-__global__ __launch_bounds__(256) void k_pkt_frames(Ws w, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n) {
+__global__ __launch_bounds__(256) void k_pkt_frames(Ws w, uint64_t nbuf, fdb_packet_frame* out, uint64_t capacity,
+                                                    uint64_t* d_n) {
+	if (w.hdr[1] != nbuf || w.hdr[2] != w.cap) {  // not the shape of the last verify in this workspace
+		if (blockIdx.x == 0 && threadIdx.x == 0 && d_n) *d_n = ~0ull;
+		return;
+	}
 	const uint64_t n0 = *w.hdr < w.cap ? *w.hdr : w.cap;
 	const uint64_t n = n0 < capacity ? n0 : capacity;
 	if (blockIdx.x == 0 && threadIdx.x == 0 && d_n) *d_n = n0;
@@ -258,9 +267,9 @@ __global__ __launch_bounds__(256) void k_pkt_frames(Ws w, fdb_packet_frame* out,
 	}
 }
 
-int launch_frames(const Ws& w, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n, hipStream_t s) {
+int launch_frames(const Ws& w, uint64_t nbuf, fdb_packet_frame* out, uint64_t capacity, uint64_t* d_n, hipStream_t s) {
 	const uint64_t g = (w.cap < capacity ? w.cap : capacity) / 256 + 1;
-	k_pkt_frames<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, s>>>(w, out, capacity, d_n);
+	k_pkt_frames<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, s>>>(w, nbuf, out, capacity, d_n);
 	return 0;
 }
 

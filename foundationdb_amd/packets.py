@@ -63,6 +63,7 @@ class PacketVerifier:
         self.ws = torch.empty(n, dtype=torch.uint8, device=self.device)
         self.results = torch.empty(self.nbuf * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
         self._n = 0
+        self._stream = None
 
     def verify(self, data, buf_offsets, buf_lengths, checksum=True, packet_limit=PACKET_LIMIT, stream=None):
         """Starts the verification of receive buffers [data + off, + len) on
@@ -75,6 +76,7 @@ class PacketVerifier:
         if n > self.nbuf or buf_lengths.numel() != n:
             raise CRC32CError("packets: more buffers than the verifier was sized for, or mismatched arrays")
         self._n = n
+        self._stream = stream  # frames_numpy() reads the frame list on the same stream
         with torch.cuda.device(data.device):
             rc = _lib().fdb_packets_verify_ws(_vp(data), _vp(buf_offsets), _vp(buf_lengths), n, self.total_bytes,
                                               1 if checksum else 0, packet_limit, self.max_frames,
@@ -88,7 +90,10 @@ class PacketVerifier:
         return self.results[: self._n * RESULT_DTYPE.itemsize].cpu().numpy().view(RESULT_DTYPE)
 
     def frames_numpy(self, stream=None):
-        """The last batch's frame list (FRAME_DTYPE records, in no particular order)."""
+        """The last batch's frame list (FRAME_DTYPE records, in no particular
+        order), read on the stream verify() ran on unless `stream` is given."""
+        if stream is None:
+            stream = self._stream
         out = torch.empty(max(self.max_frames, 1) * FRAME_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
         cnt = torch.zeros(1, dtype=torch.uint64, device=self.device)
         with torch.cuda.device(self.device):
@@ -96,7 +101,10 @@ class PacketVerifier:
                                            _vp(cnt), _stream_handle(stream))
         _check(rc, "fdb_packets_frames")
         torch.cuda.synchronize(self.device)
-        k = min(int(cnt.cpu().numpy()[0]), self.max_frames)
+        k = int(cnt.cpu().numpy().view(np.uint64)[0])
+        if k == (1 << 64) - 1:
+            raise CRC32CError("fdb_packets_frames: the workspace does not hold a batch of this shape")
+        k = min(k, self.max_frames)
         return out[: k * FRAME_DTYPE.itemsize].cpu().numpy().view(FRAME_DTYPE)
 
 

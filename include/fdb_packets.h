@@ -86,7 +86,10 @@ int fdb_packets_verify(const void* d_base, const uint64_t* d_buf_offsets, const 
                        uint64_t max_frames, fdb_packet_result* d_results, void* stream);
 /* The frame list of the last fdb_packets_verify_ws in d_workspace: copies up
  * to `capacity` frames into d_frames and their count (<= max_frames) into
- * *d_nframes (device u64).  Asynchronous on `stream`. */
+ * *d_nframes (device u64).  nbuf and max_frames must be the ones that call
+ * was given (they place the frame arrays in the workspace); with any other
+ * values nothing is copied and *d_nframes is set to UINT64_MAX.  Asynchronous
+ * on `stream`: launch it on the verify call's stream, or after it. */
 int fdb_packets_frames(const void* d_workspace, uint64_t nbuf, uint64_t max_frames, fdb_packet_frame* d_frames,
                        uint64_t capacity, uint64_t* d_nframes, void* stream);
 

@@ -227,6 +227,54 @@ def test_gpu_packets_capacity_and_empty(cuda):
     V.verify(_dev(mem, cuda), e, e)
 
 
+def walk_model(buf, checksum, limit):
+    """The frames the walk finds in one buffer: scan_model without the checksum
+    check (k_pkt_walk records every complete, well-sized frame)."""
+    p, n, e = 0, 0, len(buf)
+    hdr = 12 if checksum else 4
+    while e - p >= hdr:
+        L = int.from_bytes(buf[p:p + 4], "little")
+        if L > limit or e - p - hdr < L or L < 16:
+            break
+        p += hdr + L
+        n += 1
+    return n
+
+
+@pytest.mark.gpu
+def test_gpu_packets_capacity_with_corrupt_frames(cuda):
+    """A frame list too small for a batch that also holds corrupted frames:
+    the buffers whose frames all fit get the oracle's outcome; a buffer that
+    overflowed (fewer frames recorded than its walk found -- the recorded ones
+    are always an ordinal prefix, the list being reserved in walk order) reports
+    CHECKSUM_FAILED when a recorded frame failed (the oracle's frame count and
+    consumed bytes), FDB_PACKET_ECAPACITY otherwise.  Every buffer checked."""
+    import foundationdb_amd.packets as PK
+    bufs, kinds = build_buffers(57, nbuf=400)
+    mem, offs, lens = pack(bufs, np.random.default_rng(5))
+    want = O.packets_verify(mem, offs, lens)
+    assert (want[2] == PK.CHECKSUM_FAILED).sum() >= 20  # corrupted frames throughout the batch
+    walked = np.array([walk_model(b, True, PACKET_LIMIT) for b in bufs])
+    for cap in (1, 64, int(walked.sum()) // 2, int(walked.sum()) - 1):
+        V = PK.PacketVerifier(cuda, len(bufs), cap, int(lens.sum()))
+        V.verify(_dev(mem, cuda), _dev(offs, cuda), _dev(lens, cuda))
+        got = V.results_numpy()
+        fr = V.frames_numpy()
+        assert fr.size == min(cap, int(walked.sum()))
+        rec = np.bincount(fr["buffer"].astype(np.int64), minlength=len(bufs))
+        for b in range(len(bufs)):
+            ords = sorted(int(r["ordinal"]) for r in fr[fr["buffer"] == b])
+            assert ords == list(range(rec[b]))  # an ordinal prefix
+        over = rec < walked
+        assert over.any() or cap >= walked.sum()
+        for b in range(len(bufs)):
+            if not over[b] or (want[2][b] == PK.CHECKSUM_FAILED and want[1][b] < rec[b]):
+                assert (got["consumed"][b], got["frames"][b], got["status"][b]) == \
+                    (want[0][b], want[1][b], want[2][b]), (cap, b)
+            else:
+                assert got["status"][b] == PK.ECAPACITY, (cap, b)
+
+
 @pytest.mark.gpu
 def test_gpu_packets_one_shot_matches(cuda):
     import foundationdb_amd.packets as PK

@@ -9,6 +9,10 @@
 //   dword: 16 global_load_dword per page, lane l reading bytes 4l + 256k
 //          (256 contiguous bytes per instruction)
 //   dx2:   8 global_load_dwordx2 per page, lane l reading 8l + 512k
+//   u8/u1: coal's shape shifted by 8 / 1 bytes (unaligned dwordx4; the
+//          DiskQueue V2 XXH3 region at +8, packet payloads at any offset)
+//   dq2:   coal's shape at +8 as two dwordx2 per 16 bytes (the current
+//          8-byte-aligned XXH3 row form)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/membench3.hip -o tools/membench3
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -73,7 +77,9 @@ __global__ __launch_bounds__(1024) void rdw(const unsigned char* __restrict__ sr
   if (x == 0x12345678u) out[w] = x;
 }
 
-template <int HALF>
+typedef __attribute__((ext_vector_type(4), aligned(1))) unsigned int u32x4u;
+typedef __attribute__((address_space(1))) const u32x4u g4u;
+template <int HALF, int SHIFT = 0>
 __global__ __launch_bounds__(1024) void rd(const unsigned char* __restrict__ src, size_t npages, u32* __restrict__ out) {
   __shared__ u32 lds[160 * 256];
   const u32 lane = threadIdx.x & 63;
@@ -82,7 +88,7 @@ __global__ __launch_bounds__(1024) void rd(const unsigned char* __restrict__ src
   u32 off[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    if (HALF) {  // k = 2A + B: bytes 2048A + 128r + 64B + 16(lane & 3), r = lane >> 2
+    if (HALF == 1) {  // k = 2A + B: bytes 2048A + 128r + 64B + 16(lane & 3), r = lane >> 2
       off[k] = 2048u * (k >> 1) + 128u * (lane >> 2) + 64u * (k & 1) + 16u * (lane & 3);
     } else {
       off[k] = 1024u * k + 16u * lane;
@@ -99,7 +105,18 @@ __global__ __launch_bounds__(1024) void rd(const unsigned char* __restrict__ src
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) u[4 * j + k] = ld(src + (p + j) * 4096 + off[k]);
+      for (int k = 0; k < 4; ++k) {
+        const unsigned char* a = src + (p + j) * 4096 + off[k] + SHIFT;
+        if (SHIFT == 0) {
+          u[4 * j + k] = ld(a);
+        } else if (HALF == 2) {  // two dwordx2 per 16 B (8-byte aligned)
+          const u32x2 x = __builtin_nontemporal_load((g2*)(uintptr_t)a), y = __builtin_nontemporal_load((g2*)(uintptr_t)(a + 8));
+          u[4 * j + k] = u32x4{x.x, x.y, y.x, y.y};
+        } else {
+          const u32x4u v = __builtin_nontemporal_load((g4u*)(uintptr_t)a);
+          u[4 * j + k] = u32x4{v.x, v.y, v.z, v.w};
+        }
+      }
   };
   u32x4 acc = {0, 0, 0, 0};
   load(a, p0);
@@ -142,8 +159,11 @@ int main() {
     float h = timeit([&] { rd<1><<<cus, 1024>>>(d, npages, o); }, 30);
     float w1 = timeit([&] { rdw<2><<<cus, 1024>>>(d, npages, o); }, 30);
     float w2 = timeit([&] { rdw<3><<<cus, 1024>>>(d, npages, o); }, 30);
-    printf("coal %.4f ms %.1f GB/s   half %.4f ms %.1f GB/s   dword %.4f ms %.1f GB/s   dx2 %.4f ms %.1f GB/s\n", c,
-           bytes / c / 1e6, h, bytes / h / 1e6, w1, bytes / w1 / 1e6, w2, bytes / w2 / 1e6);
+    float u8 = timeit([&] { rd<0, 8><<<cus, 1024>>>(d, npages - 2, o); }, 30);
+    float u1 = timeit([&] { rd<0, 1><<<cus, 1024>>>(d, npages - 2, o); }, 30);
+    float q2 = timeit([&] { rd<2, 8><<<cus, 1024>>>(d, npages - 2, o); }, 30);
+    printf("coal %.1f  half %.1f  dword %.1f  dx2 %.1f  u8 %.1f  u1 %.1f  dq2 %.1f GB/s\n", bytes / c / 1e6,
+           bytes / h / 1e6, bytes / w1 / 1e6, bytes / w2 / 1e6, bytes / u8 / 1e6, bytes / u1 / 1e6, bytes / q2 / 1e6);
   }
   CHECK(hipFree(d)); CHECK(hipFree(o));
   return 0;
