@@ -708,6 +708,48 @@ __device__ __forceinline__ uint64_t short_fin(const ShortLd& S, uint64_t len, ui
 	return xxh3_aval(acc);
 }
 
+// The same from a key table in LDS (uniform seed): key pair q = (secret at
+// soff_q + 8 bytes) + seed, (secret at soff_q + 8, + 8) - seed, for the 16
+// secret offsets the 17-240 B forms use -- 16j (j < 8), 16j + 3 (j < 7) and
+// 119 -- so that slot q is chunk q on the 129-240 B path and chunks i, 4 + i
+// take slots 2i, 2i + 1 on the 17-128 B one.  (As constants + seed the 32
+// keys sat in SGPRs across the row loop and spilled.)
+__device__ __forceinline__ void short_keys(uint64_t* keys, int t, uint64_t seed) {
+	if (t < 32) {
+		const int q = t >> 1, soff = q < 8 ? 16 * q : (q < 15 ? 16 * (q - 8) + 3 : 119);
+		keys[t] = (t & 1) ? ksec(soff + 8) - seed : ksec(soff) + seed;
+	}
+}
+// SEEDED: the table holds the seed-0 keys and each lane adds its own seed.
+template <bool SEEDED>
+__device__ __forceinline__ uint64_t short_fin_k(const ShortLd& S, uint64_t len, const uint64_t* keys, uint64_t seed) {
+	typedef uint64_t u64x2k __attribute__((ext_vector_type(2)));
+	const u64x2k* kp = reinterpret_cast<const u64x2k*>(keys);
+	const bool big = len > 128;
+	const int pairs = (int)((len - 1) >> 5);
+	const int rounds = (int)len >> 4;
+	auto mix = [&](int k, int q) __attribute__((always_inline)) {
+		const u64x2k kk = kp[q];
+		return mulfold(S.x[k][0] ^ (SEEDED ? kk[0] + seed : kk[0]), S.x[k][1] ^ (SEEDED ? kk[1] - seed : kk[1]));
+	};
+	uint64_t acc = len * P64_1;
+	if (!big) {
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint64_t t = mix(i, 2 * i) + mix(4 + i, 2 * i + 1);
+			acc += i <= pairs ? t : 0;
+		}
+		return xxh3_aval(acc);
+	}
+#pragma unroll
+	for (int i = 0; i < 8; ++i) acc += mix(i, i);
+	acc = xxh3_aval(acc);
+#pragma unroll
+	for (int i = 8; i < 15; ++i) acc += i < rounds ? mix(i, i) : 0;
+	acc += mix(15, 15);
+	return xxh3_aval(acc);
+}
+
 // XXH3 of 241 B - 1 KiB (one partial block, xxhash.h:3641-3718: no scramble)
 // on a lane quad: lane k keeps accumulator pair k over the (len-1)/64 stripes
 // and the last one, the four merge terms add over the quad.  Every data load
@@ -817,11 +859,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 	const int lane = threadIdx.x & 63;
 	const int r = lane >> 4, l = lane & 15, k = l & 3, g = l >> 2;
 	__shared__ uint64_t ksl[24];  // the default secret (the quad path's keys)
+	__shared__ __attribute__((aligned(16))) uint64_t skey[32];  // the short path's keys (short_keys)
 	// per wave: the tail's short (from the front) and quad (from the back) lists
 	__shared__ uint64_t tlen[4][kTailCap], toff[4][kTailCap];
 	__shared__ uint32_t tidx[4][kTailCap];
 	__shared__ uint64_t tsd[SEEDS ? 4 : 1][SEEDS ? kTailCap : 1];
 	if (threadIdx.x < 24) ksl[threadIdx.x] = SEEDS ? kSec[threadIdx.x] : sec_word((int)threadIdx.x, P.seed);
+	short_keys(skey, (int)threadIdx.x, SEEDS ? 0 : P.seed);
 	__syncthreads();
 	const uint64_t wpb = blockDim.x >> 6;
 	const uint64_t w = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1232,7 +1276,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 			ShortLd SL;
 			short_load(SL, base + off, len, on);
 			flushp();
-			put(on, short_fin(SL, len, sd), idx);
+			put(on, short_fin_k<SEEDS>(SL, len, skey, sd), idx);
 		}
 		for (uint32_t t0 = 0; t0 < nq; t0 += 16) {  // full passes of sixteen quads
 			const uint32_t e = t0 + ((uint32_t)lane >> 2);
