@@ -391,26 +391,25 @@ def _sqlite_pages_on_device(dev, count, kinds_per=16):
     """1 Mi SQLite pages of 4 KiB in HBM, the mix a database written by several
     FoundationDB versions holds: trailers from the current writer (XXH3,
     KeyValueStoreSQLite.cpp:106-116) on 12 of every 16 pages, from the legacy
-    writer (CRC-32C, :119-128) on 3, and a corrupt trailer on 1.  The trailers
-    are built with the engine's own batch kernels; verify() re-checks a sample
-    with the CPU oracle, so nothing here is circular."""
-    import foundationdb_amd.xxh3 as X
+    writer (CRC-32C, :119-128) on 3, and a corrupt trailer on 1.  Every page is
+    first sealed by the engine's own write side (fdb_sqlite_seal_pages, page 1
+    also at 1024 B), then the legacy CRC trailers come from the CRC batch kernel;
+    verify() re-checks a sample with the CPU oracle, so nothing here is circular."""
+    import foundationdb_amd.pagecheck as PC
     buf = torch.empty(count * 4096, dtype=torch.uint8, device=dev)
     F.fill_splitmix64(buf, STATE)
     pages = buf.view(count, 4096)
-    h = X.batch_fixed(buf, 4096, 4088, count)
+    PC.sqlite_seal_pages(buf, 4096, count, first_pgno=1)
     c = F.batch_fixed(buf, 4096, 4088, count, seed=0xFDBEEFDB)
     kind = torch.arange(count, device=dev) % kinds_per
-    hv = h.view(torch.int64)
-    p1x = ((hv >> 32) & 0x00FFFFFF).to(torch.int32)
-    p2x = (hv & 0xFFFFFFFF).to(torch.int64).to(torch.int32)
-    tr = torch.zeros(count, 2, dtype=torch.int32, device=dev)
-    xx = kind < 12
+    tr = pages[:, 4088:4096].contiguous().view(torch.int32).view(count, 2)
     cr = (kind >= 12) & (kind < 15)
-    tr[:, 0] = torch.where(xx, p1x, torch.where(cr, torch.zeros_like(p1x), torch.full_like(p1x, 0x7E000001)))
-    tr[:, 1] = torch.where(xx, p2x, torch.where(cr, c.view(torch.int32), p2x ^ 0x5A5A5A5A))
+    bad = kind == 15
+    tr[:, 0] = torch.where(cr, torch.zeros_like(tr[:, 0]), torch.where(bad, torch.full_like(tr[:, 0], 0x7E000001),
+                                                                          tr[:, 0]))
+    tr[:, 1] = torch.where(cr, c.view(torch.int32), torch.where(bad, tr[:, 1] ^ 0x5A5A5A5A, tr[:, 1]))
     pages[:, 4088:4096] = tr.view(torch.uint8).view(count, 8)
-    expect = torch.where(xx, 2, torch.where(cr, 1, 0)).to(torch.uint8)
+    expect = torch.where(kind < 12, 2, torch.where(cr, 1, 0)).to(torch.uint8)
     return buf, expect
 
 
@@ -487,36 +486,36 @@ class SqliteVerifyHost(SqliteVerify):
         self.status, self.bad = torch.from_numpy(st), torch.from_numpy(bad.view(np.int64))
 
 
-def _diskqueue_pages_on_device(dev, count):
-    """1 Mi DiskQueue pages of 4 KiB in HBM (fdbserver/kvstore/DiskQueue.cpp:1047-1120):
-    implementationVersion V2 (XXH3-64 of bytes [8, 4096), the current TLog
-    format) on 12 of every 16 pages, V1 (CRC-32C of [4, 4096), TLogVersion V3..V6)
-    on 3, and a V2 page with a wrong hash on 1; a few V0 (hashlittle2) pages
-    built on the host.  The hashes are written with the engine's own batch
-    kernels; verify() re-checks a sample with the reference composition."""
-    import foundationdb_amd.xxh3 as X
-    from oracle import oracle as O
+def _diskqueue_headers(dev, count, state):
+    """Unsealed DiskQueue pages (fdbserver/kvstore/DiskQueue.cpp:1047-1120):
+    splitmix64 bytes with magic + implementationVersion V2 (XXH3-64 of [8, 4096),
+    the current TLog format) on 13 of every 16 pages, V1 (CRC-32C of [4, 4096),
+    TLogVersion V3..V6) on 3, and V0 (hashlittle2) on every 4099th page."""
     buf = torch.empty(count * 4096, dtype=torch.uint8, device=dev)
-    F.fill_splitmix64(buf, STATE ^ 0xD15C)
+    F.fill_splitmix64(buf, state)
     pages = buf.view(count, 4096)
     kind = torch.arange(count, device=dev) % 16
     ver = torch.where((kind >= 12) & (kind < 15), 1, 2).to(torch.int16)
+    v0 = torch.arange(7, count, 4099, device=dev)
+    ver[v0] = 0
     hdr = torch.stack([torch.full_like(ver, 0x4D51), ver], 1)  # magic, implementationVersion
     pages[:, 8:12] = hdr.view(torch.uint8).view(count, 4)
-    h64 = X.batch_fixed(buf, 4096, 4088, count, byte_offset=8)
-    c32 = F.batch_fixed(buf, 4096, 4092, count, seed=0xFDBEEFDB, byte_offset=4)
-    h64 = h64.view(torch.int64)
-    h64 = torch.where(kind == 15, h64 ^ 0x5A5A, h64)
-    pages[:, 0:8] = torch.where((ver == 2)[:, None], h64.view(torch.uint8).view(count, 8), pages[:, 0:8])
-    pages[:, 0:4] = torch.where((ver == 1)[:, None], c32.view(torch.uint8).view(count, 4), pages[:, 0:4])
-    v0 = np.arange(7, count, 4099)  # V0 pages: hashlittle2 of [16, 4096), built on the host
-    for i in v0:
-        pg = pages[int(i)].cpu().numpy()
-        pg[8:12] = np.frombuffer((0x0FDB).to_bytes(2, "little") + (0).to_bytes(2, "little"), np.uint8)
-        pg[:16] = np.frombuffer(O.diskqueue_hash(pg, 0), np.uint8)
-        pages[int(i)] = torch.from_numpy(pg).to(dev)
-    expect = torch.where(kind == 15, 0, 1).to(torch.uint8)
-    expect[torch.from_numpy(v0).to(dev)] = 1
+    return buf, kind, ver
+
+
+def _diskqueue_pages_on_device(dev, count):
+    """1 Mi DiskQueue pages of 4 KiB in HBM, sealed by the engine's own write side
+    (fdb_diskqueue_seal_pages, Page::updateHash by version), then one V2 page of
+    every 16 given a wrong hash.  verify() re-checks a sample with the reference
+    composition."""
+    import foundationdb_amd.pagecheck as PC
+    buf, kind, ver = _diskqueue_headers(dev, count, STATE ^ 0xD15C)
+    PC.diskqueue_seal_pages(buf, count)
+    pages = buf.view(count, 4096)
+    bad = (kind == 15) & (ver == 2)
+    h64 = pages[:, 0:8].contiguous().view(torch.int64).view(count)
+    pages[:, 0:8] = torch.where(bad[:, None], (h64 ^ 0x5A5A).view(torch.uint8).view(count, 8), pages[:, 0:8])
+    expect = torch.where(bad, 0, 1).to(torch.uint8)
     return buf, expect
 
 
@@ -562,6 +561,100 @@ class DiskQueueVerify:
                          ref_available=lambda O_: O_.pagecheck_reference_available(),
                          port=lambda O_: [O_.diskqueue_check_page(host[4096 * i:4096 * (i + 1)])
                                           for i in range(n)])
+
+
+class SqliteSeal:
+    """SQLite page writes (the codec's op 6 / op 7, KeyValueStoreSQLite.cpp:203-244
+    -> PageChecksumCodec::checksum(write=true), :107-116) over a batch: 1 Mi
+    4 KiB pages sealed in place each step (fdb_sqlite_seal_pages)."""
+    metric = "device-resident SQLite page sealing GiB/s (1 Mi 4 KiB pages, XXH3 trailers); % of HBM-read peak"
+    kernel_name = "fdb_sqlite_seal_pages (k_xxh3_rows over the pages + k_sq_seal trailer write)"
+
+    def __init__(self, dev, rank, count=1 << 20):
+        import foundationdb_amd.pagecheck as PC
+        self.PC, self.count = PC, count
+        self.buf = torch.empty(count * 4096, dtype=torch.uint8, device=dev)
+        F.fill_splitmix64(self.buf, STATE ^ 0x5EA1)
+        self.sample = np.concatenate([[0], np.random.default_rng(1).choice(np.arange(1, count), 63, replace=False)])
+        self.orig = self.buf.view(count, 4096)[torch.from_numpy(self.sample).to(dev)].cpu().numpy()
+        self.bytes_per_step = count * 4096
+        # each page: 4088 B hashed + the 8-byte trailer written (page 1's 1024 B pass aside)
+        self.algorithmic_bytes_per_step = count * 4096
+        self.data_desc = f"synthetic: splitmix64 pages (state 0x{STATE ^ 0x5EA1:X}) in HBM, sealed in place"
+        self.config = {"workload": f"{count} x 4 KiB SQLite pages sealed in place (page 1 also at 1024 B), "
+                                   "device-resident", "pages": count}
+
+    def step(self, stream):
+        self.PC.sqlite_seal_pages(self.buf, 4096, self.count, first_pgno=1, stream=stream)
+
+    def verify(self):
+        from oracle import oracle as O
+        st, bad = self.PC.sqlite_verify_pages(self.buf, 4096, self.count, first_pgno=1)
+        if not bool((st == 2).all()) or int(bad.cpu().numpy().view(np.uint64)[0]) != 0:
+            return False
+        # page 1 also verifies as a 1024-byte page, as the codec guarantees
+        st1, _ = self.PC.sqlite_verify_pages(self.buf[:1024], 1024, 1, first_pgno=1)
+        if int(st1.cpu()[0]) != 2:
+            return False
+        got = self.buf.view(self.count, 4096)[torch.from_numpy(self.sample).to(self.buf.device)].cpu().numpy()
+        seal = O.ref_sqlite_seal_pages if O.pagecheck_reference_available() else O.sqlite_seal_pages
+        for j, i in enumerate(self.sample):
+            want = seal(self.orig[j], 4096, 1, first_pgno=int(i) + 1)
+            if not np.array_equal(got[j], want):
+                return False
+        return True
+
+    def cpu_sample(self):
+        from oracle import oracle as O
+        n = 65536
+        host = O.splitmix64(n * 4096 // 8, STATE ^ 0x5EA1).view(np.uint8)
+        return CpuSample(f"{n} pages sealed in place by the codec's checksum(write=true) composed from the "
+                         "reference's own XXH3_64bits compiled unmodified (oracle/ref_pagecheck.c)",
+                         n * 4096, host, ref=lambda O_: O_.ref_sqlite_seal_pages(host, 4096, n, 1, inplace=True),
+                         ref_available=lambda O_: O_.pagecheck_reference_available(),
+                         port=lambda O_: O_.sqlite_seal_pages(host, 4096, n, 1))
+
+
+class DiskQueueSeal:
+    """DiskQueue commit-time hashing (Page::updateHash, DiskQueue.cpp:1089-1105,
+    called for every page of a commit, :955-965): 1 Mi 4 KiB pages of mixed
+    implementationVersion sealed in place each step (fdb_diskqueue_seal_pages)."""
+    metric = ("device-resident DiskQueue page sealing GiB/s (1 Mi 4 KiB pages, V2 / V1 / V0 by version); "
+              "% of HBM-read peak")
+    kernel_name = "fdb_diskqueue_seal_pages (classify + k_xxh3_rows list + k_pages4k list + hash write)"
+
+    def __init__(self, dev, rank, count=1 << 20):
+        import foundationdb_amd.pagecheck as PC
+        self.PC, self.count = PC, count
+        self.buf, _, _ = _diskqueue_headers(dev, count, STATE ^ 0x5EA2)
+        self.sample = np.concatenate([[7, 4106], np.random.default_rng(2).choice(count, 62, replace=False)])
+        self.orig = self.buf.view(count, 4096)[torch.from_numpy(self.sample).to(dev)].cpu().numpy()
+        self.bytes_per_step = count * 4096
+        self.algorithmic_bytes_per_step = count * 4096
+        self.data_desc = "synthetic: splitmix64 pages in HBM, implementationVersion V2 / V1 13:3 plus V0 pages"
+        self.config = {"workload": f"{count} x 4 KiB DiskQueue pages sealed in place by implementationVersion, "
+                                   "device-resident", "pages": count}
+
+    def step(self, stream):
+        self.PC.diskqueue_seal_pages(self.buf, self.count, stream=stream)
+
+    def verify(self):
+        from oracle import oracle as O
+        ok, bad = self.PC.diskqueue_check_pages(self.buf, self.count)
+        if not bool((ok == 1).all()) or int(bad.cpu().numpy().view(np.uint64)[0]) != 0:
+            return False
+        got = self.buf.view(self.count, 4096)[torch.from_numpy(self.sample).to(self.buf.device)].cpu().numpy()
+        seal = O.ref_diskqueue_seal_pages if O.pagecheck_reference_available() else O.diskqueue_seal_pages
+        return all(np.array_equal(got[j], seal(self.orig[j], 1)) for j in range(self.sample.size))
+
+    def cpu_sample(self):
+        n = 65536
+        host = self.buf[:n * 4096].cpu().numpy()
+        return CpuSample(f"first {n} pages through Page::updateHash (DiskQueue.cpp:1089-1105) composed from the "
+                         "reference's own crc32c_append / XXH3_64bits / hashlittle2 (oracle/ref_pagecheck.c), in place",
+                         n * 4096, host, ref=lambda O_: O_.ref_diskqueue_seal_pages(host, n, inplace=True),
+                         ref_available=lambda O_: O_.pagecheck_reference_available(),
+                         port=lambda O_: O_.diskqueue_seal_pages(host, n))
 
 
 class Xxh3Zipf(VarLen):
@@ -722,5 +815,7 @@ WORKLOADS = {
     "sqlite-verify": lambda dev, rank: SqliteVerify(dev, rank),
     "sqlite-verify-host": lambda dev, rank: SqliteVerifyHost(dev, rank),
     "diskqueue-verify": lambda dev, rank: DiskQueueVerify(dev, rank),
+    "sqlite-seal": lambda dev, rank: SqliteSeal(dev, rank),
+    "diskqueue-seal": lambda dev, rank: DiskQueueSeal(dev, rank),
     "packets-verify": lambda dev, rank: PacketsVerify(dev, rank),
 }

@@ -63,6 +63,7 @@ __device__ __forceinline__ void push(bool want, uint32_t i, uint32_t* list, unsi
 // reference's tail mix (same values as its masked reads).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 // Wave-cooperative main loop (STAGED): the wave's 64 pages (one per lane, all
 // of one length) are read in stages of kSt = 192 bytes (16 rounds) per page,
 // coalesced -- load t of a stage covers chunks u = 64t + lane, i.e. chunk u % 12
@@ -520,12 +521,18 @@ __global__ __launch_bounds__(256) void k_dq_final(const uint8_t* __restrict__ pa
 // SQLite checksum(write = true) (KeyValueStoreSQLite.cpp:107-116): the trailer
 // of page i = XXH3 split part1 = (h >> 32) & 0xffffff, part2 = (uint32_t)h, as
 // one little-endian u64 at [ps - 8, ps) (8-byte aligned: pages 16-byte aligned).
+// The seal stores are nontemporal: a plain 8-byte store leaves a partially
+// written line in the last-level cache that costs the NEXT pass over the pages
+// ~120 us per 1 Mi 4 KiB pages (its read-modify-write on the way to HBM lands
+// in that pass); rewriting the whole 64-byte line instead (read 56 B + write
+// 64 B) recovered nothing, the nontemporal 8-byte store all of it (same box:
+// sqlite-seal 0.830 -> 0.722 ms, its XXH3 pass 778 -> 667 us = the pass on
+// untouched pages; diskqueue-seal 0.873 -> 0.802 ms; tools/seal_probe.py).
+__device__ __forceinline__ uint64_t sq_trailer(uint64_t h) { return ((h >> 32) & 0x00ffffffull) | (h << 32); }
 __global__ __launch_bounds__(256) void k_sq_seal(uint8_t* __restrict__ pages, uint64_t ps, uint64_t count,
                                                  const uint64_t* __restrict__ xxh_out) {
-	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t h = xxh_out[i];
-		*reinterpret_cast<uint64_t*>(pages + i * ps + ps - 8) = ((h >> 32) & 0x00ffffffull) | (h << 32);
-	}
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
+		__builtin_nontemporal_store(sq_trailer(xxh_out[i]), reinterpret_cast<uint64_t*>(pages + i * ps + ps - 8));
 }
 
 // DiskQueue Page::updateHash (DiskQueue.cpp:1089-1105) by implementationVersion:
@@ -551,22 +558,28 @@ __global__ __launch_bounds__(kCB) void k_dq_seal_classify(const uint8_t* __restr
 	stage_flush(S, lists, ctr);
 }
 
+// The hash stores of V1 / V2 pages (nontemporal, see k_sq_seal).
 __global__ __launch_bounds__(kCB) void k_dq_seal_write(uint8_t* __restrict__ pages, const uint32_t* __restrict__ v1_l,
                                                        const uint32_t* __restrict__ v2_l,
                                                        const unsigned long long* __restrict__ ctr,
                                                        const uint32_t* __restrict__ crc_out,
                                                        const uint64_t* __restrict__ xxh_out) {
 	const uint64_t n1 = ctr[0], n2 = ctr[1];
-	for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < (n1 > n2 ? n1 : n2);
-	     j += (uint64_t)gridDim.x * blockDim.x) {
-		if (j < n1) *reinterpret_cast<uint32_t*>(pages + (uint64_t)v1_l[j] * 4096) = crc_out[j];
-		if (j < n2) *reinterpret_cast<uint64_t*>(pages + (uint64_t)v2_l[j] * 4096) = xxh_out[j];
+	for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < (n1 > n2 ? n1 : n2);
+	     t += (uint64_t)gridDim.x * blockDim.x) {
+		if (t < n1) __builtin_nontemporal_store(crc_out[t], reinterpret_cast<uint32_t*>(pages + (uint64_t)v1_l[t] * 4096));
+		if (t < n2) __builtin_nontemporal_store(xxh_out[t], reinterpret_cast<uint64_t*>(pages + (uint64_t)v2_l[t] * 4096));
 	}
 }
 
 // V0 pages: hash = UID(c << 32 | b, 0xFDB) from hashlittle2 over [16, 4096)
 // (checksum_hashlittle2, DiskQueue.cpp:1077-1082); bytes 8..15 become 0xFDB
-// (magic 0x0FDB, implementationVersion 0: the UID overlays them).
+// (magic 0x0FDB, implementationVersion 0: the UID overlays them).  One serial
+// lookup3 chain per page: ~30 us for any number of V0 pages up to a few
+// thousand, a latency the stores' launch cannot hide (run in the same launch,
+// under the stores' memory traffic, the chain's 21 dependent load stages took
+// the launch from 50 to 84 us; a grid capped at 64 workgroups with a stride
+// loop ran 44 us against this form's 30).
 __global__ __launch_bounds__(256) void k_dq_seal_v0(uint8_t* __restrict__ pages, const uint32_t* __restrict__ v0_l,
                                                     const unsigned long long* __restrict__ ctr) {
 	const uint64_t n = ctr[2];

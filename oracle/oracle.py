@@ -368,18 +368,26 @@ def ref_diskqueue_check_pages(pages, count):
     return ok, int(bad)
 
 
-def ref_sqlite_seal_pages(pages, page_size, count, first_pgno=1):
-    """A sealed copy of `pages`: the codec's page writes (op 6 / 7) composed from
-    the reference's XXH3_64bits (oracle/ref_pagecheck.c)."""
-    out = np.array(np.ascontiguousarray(pages).view(np.uint8).reshape(-1), copy=True)
+def _seal_target(pages, inplace):
+    if inplace:
+        assert isinstance(pages, np.ndarray) and pages.dtype == np.uint8 and pages.flags.c_contiguous
+        return pages.reshape(-1)
+    return np.array(np.ascontiguousarray(pages).view(np.uint8).reshape(-1), copy=True)
+
+
+def ref_sqlite_seal_pages(pages, page_size, count, first_pgno=1, inplace=False):
+    """A sealed copy of `pages` (or `pages` itself with inplace): the codec's page
+    writes (op 6 / 7) composed from the reference's XXH3_64bits (oracle/ref_pagecheck.c)."""
+    out = _seal_target(pages, inplace)
     assert count * page_size <= out.nbytes
     pagecheck_reference().ref_sqlite_seal_pages(out.ctypes.data, page_size, count, first_pgno)
     return out
 
 
-def ref_diskqueue_seal_pages(pages, count):
-    """A sealed copy of `pages`: Page::updateHash by version from the reference primitives."""
-    out = np.array(np.ascontiguousarray(pages).view(np.uint8).reshape(-1), copy=True)
+def ref_diskqueue_seal_pages(pages, count, inplace=False):
+    """A sealed copy of `pages` (or `pages` itself with inplace): Page::updateHash
+    by version from the reference primitives."""
+    out = _seal_target(pages, inplace)
     assert count * 4096 <= out.nbytes
     pagecheck_reference().ref_diskqueue_seal_pages(out.ctypes.data, count)
     return out

@@ -234,10 +234,13 @@ def test_gpu_sqlite_seal_pages(cuda, page_size):
     import foundationdb_amd.pagecheck as PC
     n = {512: 3000, 4096: 2000, 8192: 700, 65536: 40}[page_size]
     pages = sm_bytes(n * page_size, page_size + 17)
-    for first in (0, 1, 5):
+    for first, shift in ((0, 0), (1, 0), (5, 0), (1, 16)):
+        # shift 16: pages off the 64-byte line grid (the trailer-only store form)
         want = O.ref_sqlite_seal_pages(pages, page_size, n, first) if O.pagecheck_reference_available() else \
             O.sqlite_seal_pages(pages, page_size, n, first)
-        d = torch.from_numpy(pages.copy()).to(cuda)
+        whole = torch.zeros(pages.size + shift, dtype=torch.uint8, device=cuda)
+        d = whole[shift:]
+        d.copy_(torch.from_numpy(pages))
         PC.sqlite_seal_pages(d, page_size, first_pgno=first)
         torch.cuda.synchronize()
         got = d.cpu().numpy()
@@ -258,11 +261,14 @@ def test_gpu_diskqueue_seal_pages(cuda):
     n = 3000
     dq, vers = _dq_versions(n, 21)
     want = O.ref_diskqueue_seal_pages(dq, n) if O.pagecheck_reference_available() else O.diskqueue_seal_pages(dq, n)
-    d = torch.from_numpy(dq.reshape(-1).copy()).to(cuda)
-    PC.diskqueue_seal_pages(d)
-    torch.cuda.synchronize()
-    got = d.cpu().numpy()
-    assert np.array_equal(got, want.reshape(-1))
+    for shift in (16, 0):  # 16: off the 64-byte line grid (the hash-only store form)
+        whole = torch.zeros(dq.size + shift, dtype=torch.uint8, device=cuda)
+        d = whole[shift:]
+        d.copy_(torch.from_numpy(dq.reshape(-1)))
+        PC.diskqueue_seal_pages(d)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy()
+        assert np.array_equal(got, want.reshape(-1)), shift
     ok, bad = PC.diskqueue_check_pages(d)
     assert np.array_equal(ok.cpu().numpy(), (vers <= 2).astype(np.uint8))
     assert int(bad.cpu().numpy().view(np.uint64)[0]) == int((vers > 2).sum())
