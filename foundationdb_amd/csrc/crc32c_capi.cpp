@@ -36,6 +36,7 @@ struct StreamState {
 	uint64_t ws_bytes = 0;
 	uint32_t* ctr = nullptr;  // page-kernel grab counters
 	uint64_t ctr_bytes = 0;
+	uint64_t* aux = nullptr;  // the verifiers' counters (stream_aux)
 	uint64_t* hst_h = nullptr;  // varlen route statistics of the stream's last batch (host-mapped)
 	uint64_t* hst_d = nullptr;  // ... its device address
 	// extent route state (crc32c_extent.hip): grown to the batches seen
@@ -255,6 +256,33 @@ int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr) {
 	return 0;
 }
 
+// The stream's counter words of the page verifiers, the seal passes and the
+// packet verifier (kAux* in crc32c_device.h): zeroed once here, on `stream`
+// ahead of their first use, and put back to zero by the last kernel of every
+// call that uses them, so no call starts with a memset (and a captured graph
+// of a call replays correctly: it ends with them at zero too).  Per stream,
+// not in the workspace: the convenience entry points share one workspace per
+// stream between every API, and a caller's workspace is not ours to keep.
+int stream_aux(hipStream_t stream, uint64_t** aux) {
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	StreamState* ss = stream_state(st, stream);
+	std::lock_guard<std::mutex> lock(g_mu);
+	if (!ss->aux) {
+		uint64_t* q = nullptr;
+		hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), kAuxBytes);
+		if (e != hipSuccess) return fail(FDB_CRC32C_ENOMEM, "hipMalloc(stream counters)", e);
+		e = hipMemsetAsync(q, 0, kAuxBytes, stream);
+		if (e != hipSuccess) {
+			(void)hipFree(q);
+			return fail(FDB_CRC32C_EHIP, "hipMemsetAsync(stream counters)", e);
+		}
+		ss->aux = q;
+	}
+	*aux = ss->aux;
+	return 0;
+}
+
 // Frees what the library holds for `stream` on the current device.
 int release_stream(hipStream_t stream) {
 	DeviceState* st = nullptr;
@@ -271,6 +299,7 @@ int release_stream(hipStream_t stream) {
 	hipError_t e = hipStreamSynchronize(stream);
 	if (ss->ws) (void)hipFree(ss->ws);
 	if (ss->ctr) (void)hipFree(ss->ctr);
+	if (ss->aux) (void)hipFree(ss->aux);
 	if (ss->hst_h) (void)hipHostFree(ss->hst_h);
 	if (ss->xmem) (void)hipFree(ss->xmem);
 	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "hipStreamSynchronize(release)", e);
@@ -703,8 +732,12 @@ int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t
 		return fail(FDB_CRC32C_EINVAL, "fdb_sqlite_verify_pages: workspace too small or misaligned");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
+	uint64_t* aux = nullptr;
+	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux)) return rc;
 	if (fdbpc::sqlite_verify(static_cast<const uint8_t*>(d_pages), page_size, count, first_pgno, d_status, d_bad,
-	                         st->tables, st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream)))
+	                         st->tables, st->num_cus, d_workspace,
+	                         reinterpret_cast<unsigned long long*>(aux + kAuxPageCtr),
+	                         reinterpret_cast<hipStream_t>(stream)))
 		return fail(FDB_CRC32C_EHIP, "fdb_sqlite_verify_pages: launch setup failed");
 	return check_launch("fdb_sqlite_verify_pages launch");
 }
@@ -736,8 +769,11 @@ int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d
 		return fail(FDB_CRC32C_EINVAL, "fdb_diskqueue_check_pages: workspace too small or misaligned");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
+	uint64_t* aux = nullptr;
+	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux)) return rc;
 	if (fdbpc::diskqueue_check(static_cast<const uint8_t*>(d_pages), count, d_ok, d_bad, st->tables, st->num_cus,
-	                           d_workspace, reinterpret_cast<hipStream_t>(stream)))
+	                           d_workspace, reinterpret_cast<unsigned long long*>(aux + kAuxPageCtr),
+	                           reinterpret_cast<hipStream_t>(stream)))
 		return fail(FDB_CRC32C_EHIP, "fdb_diskqueue_check_pages: launch setup failed");
 	return check_launch("fdb_diskqueue_check_pages launch");
 }
@@ -793,7 +829,10 @@ int fdb_diskqueue_seal_pages_ws(void* d_pages, uint64_t count, void* d_workspace
 		return fail(FDB_CRC32C_EINVAL, "fdb_diskqueue_seal_pages: workspace too small or misaligned");
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
+	uint64_t* aux = nullptr;
+	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux)) return rc;
 	if (fdbpc::diskqueue_seal(static_cast<uint8_t*>(d_pages), count, st->tables, st->num_cus, d_workspace,
+	                          reinterpret_cast<unsigned long long*>(aux + kAuxPageCtr),
 	                          reinterpret_cast<hipStream_t>(stream)))
 		return fail(FDB_CRC32C_EHIP, "fdb_diskqueue_seal_pages: launch setup failed");
 	return check_launch("fdb_diskqueue_seal_pages launch");
@@ -835,9 +874,25 @@ int fdb_packets_verify_ws(const void* d_base, const uint64_t* d_buf_offsets, con
 	const uint64_t need = fdbpkt::workspace_bytes(nbuf, max_frames, total_bytes, st->num_cus);
 	if (!d_workspace || workspace_bytes < need || reinterpret_cast<uintptr_t>(d_workspace) % 16)
 		return fail(FDB_CRC32C_EINVAL, "fdb_packets_verify: workspace too small or misaligned");
+	const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+	uint64_t* aux = nullptr;
+	if (int rc = stream_aux(s, &aux)) return rc;
+	// the split route's room from the long frames the stream's last batch
+	// needed (host-mapped, no synchronisation; a stale hint costs speed only:
+	// long frames past the room are hashed by the row kernel, and the next call
+	// grows the room)
+	StreamState* ss = stream_state(st, s);
+	bool mapped;
+	{
+		std::lock_guard<std::mutex> lock(g_mu);
+		mapped = stream_mapped(ss);
+	}
+	const uint64_t last = mapped ? *reinterpret_cast<volatile uint64_t*>(ss->hst_h + kHstatXxhNeed) : ~0ull;
+	const uint64_t room = mapped ? last + last / 4 : ~0ull;
 	if (fdbpkt::launch_verify(static_cast<const uint8_t*>(d_base), d_buf_offsets, d_buf_lengths, nbuf,
 	                          checksum_enabled ? 1 : 0, packet_limit, max_frames, d_results, d_workspace,
-	                          workspace_bytes, st->num_cus, reinterpret_cast<hipStream_t>(stream)))
+	                          workspace_bytes, st->num_cus, aux + kAuxPktFrames, room,
+	                          mapped ? ss->hst_d + kHstatXxhNeed : nullptr, s))
 		return fail(FDB_CRC32C_EHIP, "fdb_packets_verify: launch setup failed");
 	return check_launch("fdb_packets_verify launch");
 }

@@ -68,6 +68,11 @@ __device__ __forceinline__ void xcd_range(uint64_t n, uint64_t b, uint64_t G, ui
 	g1 = e0 < n ? e0 : n;
 }
 int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr);  // crc32c_capi.cpp
+// per-stream counter words (crc32c_capi.cpp: stream_aux), zero between calls
+constexpr uint64_t kAuxBytes = 256;
+constexpr int kAuxPktFrames = 0;  // u64: the packet verifier's frame counter
+constexpr int kAuxPageCtr = 8;    // u64[8]: the page verifiers' list counters and failures
+int stream_aux(hipStream_t stream, uint64_t** aux);
 
 int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream);

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
 	uint32_t ord = 0;  // frames walked
 	int32_t status = FDB_PACKET_OK;
 	bool live = in, overflow = false;
-	uint64_t* const fcount = P.w.hdr;
+	uint64_t* const fcount = P.w.fcount;
 	// The frames of kWalkStage steps are held in the lane's registers (slot s
 	// of the unrolled group: the step index is wave-uniform) and leave together:
 	// one reservation atomic per wave and group, the lane's frames contiguous
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void k_pkt_walk(WalkP P) {
 
 // Per frame: the digest against the header's checksum.
 __global__ __launch_bounds__(256) void k_pkt_check(CheckP P) {
-	const uint64_t n = *P.w.hdr < P.w.cap ? *P.w.hdr : P.w.cap;
+	const uint64_t n = *P.w.fcount < P.w.cap ? *P.w.fcount : P.w.cap;
 	for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n; f += (uint64_t)gridDim.x * blockDim.x) {
 		if (P.w.fh[f] != P.w.fexp[f]) {
 			const uint32_t b = P.w.fbuf[f];
@@ -230,8 +230,16 @@ __global__ __launch_bounds__(256) void k_pkt_check(CheckP P) {
 	}
 }
 
+// Per buffer: the reference's outcome.  Thread 0 also moves the frame count
+// into the workspace (fdb_packets_frames reads it there) and puts the
+// stream's counter back to zero for the next call (no kernel of this launch
+// reads it).
 __global__ __launch_bounds__(256) void k_pkt_final(CheckP P) {
 	const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (b == 0) {
+		P.w.hdr[0] = *P.w.fcount;
+		*P.w.fcount = 0;
+	}
 	if (b >= P.nbuf) return;
 	const uint32_t n = P.w.walked[b], bo = P.w.bad_ord[b];
 	fdb_packet_result r;
@@ -318,11 +326,11 @@ Ws carve(void* ws, uint64_t nbuf, uint64_t max_frames, uint64_t ws_bytes, void**
 
 int launch_verify(const uint8_t* base, const uint64_t* boff, const uint64_t* blen, uint64_t nbuf, int checksum,
                   uint32_t limit, uint64_t max_frames, fdb_packet_result* out, void* ws, uint64_t ws_bytes,
-                  int num_cus, hipStream_t s) {
+                  int num_cus, uint64_t* fcount, uint64_t room_blocks, uint64_t* hneed, hipStream_t s) {
 	void* xws = nullptr;
 	uint64_t xws_bytes = 0;
-	const Ws w = carve(ws, nbuf, max_frames, ws_bytes, &xws, &xws_bytes);
-	if (hipMemsetAsync(w.hdr, 0, 8, s) != hipSuccess) return -1;
+	Ws w = carve(ws, nbuf, max_frames, ws_bytes, &xws, &xws_bytes);
+	w.fcount = fcount;
 	WalkP W{};
 	W.base = base;
 	W.boff = boff;
@@ -348,9 +356,21 @@ int launch_verify(const uint8_t* base, const uint64_t* boff, const uint64_t* ble
 		X.offsets = w.foff;
 		X.lengths = w.flen;
 		X.count = max_frames;
-		X.d_count = w.hdr;
+		X.d_count = w.fcount;
 		X.out = w.fh;
-		X.ws_bytes = xws_bytes;
+		// the split route's room: none when the limit keeps every frame within
+		// 16 KiB (its launch would be empty), else what the caller asks for
+		const uint64_t nw = fdbxxh::xxh3_nwave(num_cus);
+		uint64_t xb = xws_bytes;
+		if (limit <= fdbxxh::kXSplitMin) {
+			const uint64_t b0 = fdbxxh::xxh3_workspace_bytes(max_frames, nw);
+			xb = xb < b0 ? xb : b0;
+		} else if (room_blocks != ~0ull) {
+			const uint64_t b1 = fdbxxh::xxh3_workspace_bytes_for(max_frames, nw, room_blocks);
+			xb = xb < b1 ? xb : b1;
+		}
+		X.ws_bytes = xb;
+		X.hneed = hneed;
 		if (fdbxxh::launch_xxh3(X, num_cus, xws, s)) return -1;
 		const uint64_t g = (max_frames + 255) / 256;
 		k_pkt_check<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, s>>>(C);

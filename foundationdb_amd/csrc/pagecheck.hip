@@ -404,8 +404,14 @@ __global__ __launch_bounds__(256) void k_sq_final(const uint8_t* __restrict__ pa
 	count_bad(bad, &s_bad, &ctr[3]);
 }
 
-__global__ void k_store_bad(const unsigned long long* __restrict__ ctr, uint64_t* __restrict__ d_bad) {
-	*d_bad = ctr[3];
+// The last kernel of a verify or seal call: the failure count out, and the
+// stream's counters (crc32c_capi.cpp: stream_aux) back to zero for the next
+// call -- no memset ahead of any call.
+__global__ void k_pc_done(unsigned long long* __restrict__ ctr, uint64_t* __restrict__ d_bad) {
+	const unsigned long long bad = ctr[3];
+	__syncthreads();
+	if (threadIdx.x == 0 && d_bad) *d_bad = bad;
+	if (threadIdx.x < 8) ctr[threadIdx.x] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -638,23 +644,23 @@ static Ws carve(void* ws, uint64_t count) {
 static unsigned blocks(uint64_t n, uint64_t per = 256) { return (unsigned)((n + per - 1) / per); }
 
 int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t first_pgno, uint8_t* status,
-                  uint64_t* d_bad, const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s) {
+                  uint64_t* d_bad, const fdbcrc::DevTables* tabs, int num_cus, void* ws, unsigned long long* ctr,
+                  hipStream_t s) {
 	const Ws w = carve(ws, count);
-	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
-	k_sq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, count, status, w.list_a, w.list_b, w.list_c, w.ctr,
+	k_sq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, count, status, w.list_a, w.list_b, w.list_c, ctr,
 	                                                  w.trl);
-	const uint64_t* n_crc = reinterpret_cast<const uint64_t*>(&w.ctr[L_CRC]);
-	const uint64_t* n_xxh = reinterpret_cast<const uint64_t*>(&w.ctr[L_XXH]);
+	const uint64_t* n_crc = reinterpret_cast<const uint64_t*>(&ctr[L_CRC]);
+	const uint64_t* n_xxh = reinterpret_cast<const uint64_t*>(&ctr[L_XXH]);
 	if (ps == 4096) {
 		if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n_crc, count, 0, 8, 0xFDBEEFDBu, w.crc_out, tabs,
 		                                     num_cus, s))
 			return -1;
-		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, false, status, w.list_b, w.ctr,
+		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, false, status, w.list_b, ctr,
 		                                                   w.trl);
 	} else {
 		// other page sizes: every page through the general fixed-stride engine
 		fdbcrc::launch_fixed_general(pages, ps, ps - 8, count, 0xFDBEEFDBu, nullptr, w.crc_out, tabs, num_cus, w.eng, s);
-		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, true, status, w.list_b, w.ctr,
+		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, true, status, w.list_b, ctr,
 		                                                   w.trl);
 	}
 	fdbxxh::XxhParams P{};
@@ -666,19 +672,18 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 	P.idx = w.list_b;
 	P.d_count = n_xxh;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_sq_after_xxh<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_b, w.xxh_out, status, w.list_c, w.ctr, w.trl);
-	k_sq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, w.ctr, w.trl);
-	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
+	k_sq_after_xxh<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_b, w.xxh_out, status, w.list_c, ctr, w.trl);
+	k_sq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, ctr, w.trl);
+	k_pc_done<<<1, 64, 0, s>>>(ctr, d_bad);
 	return 0;
 }
 
 int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t* d_bad,
-                    const fdbcrc::DevTables* tabs, int num_cus, void* ws, hipStream_t s) {
+                    const fdbcrc::DevTables* tabs, int num_cus, void* ws, unsigned long long* ctr, hipStream_t s) {
 	const Ws w = carve(ws, count);
-	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
-	k_dq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, ok, w.list_a, w.list_b, w.list_c, w.ctr, w.trl);
-	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
-	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
+	k_dq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, ok, w.list_a, w.list_b, w.list_c, ctr, w.trl);
+	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&ctr[0]);
+	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&ctr[1]);
 	// V1: crc32c(0xfdbeefdb, bytes [4, 4096))
 	if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n1, count, 4, 0, 0xFDBEEFDBu, w.crc_out, tabs, num_cus, s))
 		return -1;
@@ -692,10 +697,10 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	P.idx = w.list_b;
 	P.d_count = n2;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_dq_compare<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out, ok, &w.ctr[3],
+	k_dq_compare<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, ctr, w.crc_out, w.xxh_out, ok, &ctr[3],
 	                                           w.trl);
-	k_dq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ok, w.ctr);
-	if (d_bad) k_store_bad<<<1, 1, 0, s>>>(w.ctr, d_bad);
+	k_dq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ok, ctr);
+	k_pc_done<<<1, 64, 0, s>>>(ctr, d_bad);
 	return 0;
 }
 
@@ -709,7 +714,7 @@ int sqlite_seal(uint8_t* pages, uint64_t ps, uint64_t count, uint32_t first_pgno
 	// the full page's hashed bytes, so this goes first (stream order)
 	const uint64_t i1 = (uint32_t)(1u - first_pgno);
 	if (i1 < count && ps > 1024) {
-		uint64_t* h1 = reinterpret_cast<uint64_t*>(w.ctr);  // (the counters are unused here)
+		uint64_t* h1 = w.trl;  // (scratch: the saved trailers are not used here)
 		fdbxxh::XxhParams P{};
 		P.base = pages + i1 * ps;
 		P.stride = 1024;
@@ -731,12 +736,11 @@ int sqlite_seal(uint8_t* pages, uint64_t ps, uint64_t count, uint32_t first_pgno
 }
 
 int diskqueue_seal(uint8_t* pages, uint64_t count, const fdbcrc::DevTables* tabs, int num_cus, void* ws,
-                   hipStream_t s) {
+                   unsigned long long* ctr, hipStream_t s) {
 	const Ws w = carve(ws, count);
-	if (hipMemsetAsync(w.ctr, 0, 64, s) != hipSuccess) return -1;
-	k_dq_seal_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, w.list_a, w.list_b, w.list_c, w.ctr);
-	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&w.ctr[0]);
-	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&w.ctr[1]);
+	k_dq_seal_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, w.list_a, w.list_b, w.list_c, ctr);
+	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&ctr[0]);
+	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&ctr[1]);
 	if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n1, count, 4, 0, 0xFDBEEFDBu, w.crc_out, tabs, num_cus, s))
 		return -1;
 	fdbxxh::XxhParams P{};
@@ -748,8 +752,9 @@ int diskqueue_seal(uint8_t* pages, uint64_t count, const fdbcrc::DevTables* tabs
 	P.idx = w.list_b;
 	P.d_count = n2;
 	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
-	k_dq_seal_write<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, w.ctr, w.crc_out, w.xxh_out);
-	k_dq_seal_v0<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, w.ctr);
+	k_dq_seal_write<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, ctr, w.crc_out, w.xxh_out);
+	k_dq_seal_v0<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ctr);
+	k_pc_done<<<1, 64, 0, s>>>(ctr, nullptr);
 	return 0;
 }
 

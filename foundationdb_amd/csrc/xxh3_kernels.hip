@@ -645,6 +645,7 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 // ---------------------------------------------------------------------------
 typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(1)));
 typedef __attribute__((address_space(1))) const u64x2u g_u64x2u;
+typedef __attribute__((address_space(1))) const uint32_t g_u32a;
 
 // xxh3_short (17-240 B, xxhash.h:2847-2951) for one lane's buffer in two
 // halves, so that a pass issues every data load it has (these and the lane
@@ -847,9 +848,14 @@ struct VStep {
 	uint64_t v[4][2];
 	uint64_t len, buf, seed;  // this row's buffer
 	uint32_t blk;             // block loaded
+	uint32_t ra;              // FDBXXH_ALN: the row's byte shift (0: loaded at the bytes' own address)
+	uint32_t nx;              // ... lane 15: the dword after the block
 	bool act;                 // row has a buffer
 	bool any;                 // some row has one (uniform)
 };
+#ifndef FDBXXH_ALN
+#define FDBXXH_ALN 1
+#endif
 
 constexpr int kTailPasses = 4;                    // buffers listed at once: 64 each
 constexpr uint32_t kTailCap = 64 * kTailPasses;  // list entries per wave
@@ -984,15 +990,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 		const uint64_t nfull = (llen - 1) >> 10;
 		const uint32_t ns = (uint32_t)(((llen - 1) - (nfull << 10)) >> 6);
 		const bool fin = lblk == nfull;
+		// FDBXXH_ALN: a full block of a byte-unaligned buffer loads from the
+		// dword-aligned address below its bytes (a byte-unaligned dwordx4 streams
+		// ~23 % slower, a dword-aligned one at full rate: tools/membench3.hip),
+		// and compute() shifts the bytes back (v_alignbyte; the dword after each
+		// lane's chunk from the next lane, DPP; after the block's last chunk, lane
+		// 15's own extra load, issued only by the rows that shift).  A dword
+		// holding a buffer byte never crosses a page, so nothing outside a mapped
+		// page is read.
+		const uint32_t ra = FDBXXH_ALN && !fin ? (uint32_t)lp & 3u : 0u;
+		const uint64_t lpa = lp - ra;
 #pragma unroll
 		for (int i = 0; i < 4; ++i) {
 			const uint32_t s = g + 4 * i;
 			const bool tail = fin && (s == 15 || s >= ns);
-			const uint64_t a = tail ? lp + llen - 64 + 16 * k : lp + ((uint64_t)lblk << 10) + 64 * s + 16 * k;
+			const uint64_t a = tail ? lp + llen - 64 + 16 * k : lpa + ((uint64_t)lblk << 10) + 64 * s + 16 * k;
 			const u64x2u x = __builtin_nontemporal_load((g_u64x2u*)a);
 			S.v[i][0] = x[0];
 			S.v[i][1] = x[1];
 		}
+		if (FDBXXH_ALN && l == 15 && ra != 0) S.nx = __builtin_nontemporal_load((g_u32a*)(lpa + ((uint64_t)(lblk + 1) << 10)));
+		S.ra = ra;
 		S.len = llen;
 		S.buf = lbuf;
 		S.seed = lseed;
@@ -1014,10 +1032,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 	};
 	RowKeys K = row_keys(lane, seed0);
 	uint64_t a0 = 0, a1 = 0;
-	auto compute = [&](const VStep& S) __attribute__((always_inline)) {
+	auto compute = [&](VStep& S) __attribute__((always_inline)) {
 		const uint64_t nfull = (S.len - 1) >> 10;
 		const uint32_t ns = (uint32_t)(((S.len - 1) - (nfull << 10)) >> 6);
 		const bool fin = S.blk == nfull;
+		if (FDBXXH_ALN && __ballot(S.ra != 0) != 0) {  // some row loaded dword-aligned: shift its bytes back
+			uint32_t nxt[4];
+#pragma unroll
+			for (int i = 0; i < 4; ++i)  // lane l <- dword 0 of lane l + 1 (mod 16) of load i
+				nxt[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)S.v[i][0], 0x12F, 0xF, 0xF, false);
+#pragma unroll
+			for (int i = 0; i < 4; ++i) {
+				const uint32_t w0 = (uint32_t)S.v[i][0], w1 = (uint32_t)(S.v[i][0] >> 32);
+				const uint32_t w2 = (uint32_t)S.v[i][1], w3 = (uint32_t)(S.v[i][1] >> 32);
+				const uint32_t w4 = l == 15 ? (i < 3 ? nxt[i + 1] : S.nx) : nxt[i];
+				const uint32_t sh = S.ra;
+				S.v[i][0] = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+				S.v[i][1] = ((uint64_t)__builtin_amdgcn_alignbyte(w4, w3, sh) << 32) | __builtin_amdgcn_alignbyte(w3, w2, sh);
+			}
+		}
 		if (SEEDS && __ballot(S.blk == 0 && S.act) != 0) K = row_keys(lane, S.seed);
 		if (S.blk == 0) {
 			a0 = k == 0 ? P32_3 : (k == 1 ? P64_2 : (k == 2 ? P64_4 : P64_5));
@@ -1173,6 +1206,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 	s0.buf = s1.buf = 0;
 	s0.seed = s1.seed = seed0;
 	s0.blk = s1.blk = 0;
+	s0.ra = s1.ra = 0;
+	s0.nx = s1.nx = 0;
 	s0.act = s1.act = false;
 	s0.any = s1.any = false;
 	for (;;) {

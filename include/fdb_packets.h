@@ -80,7 +80,15 @@ int fdb_packets_verify_ws(const void* d_base, const uint64_t* d_buf_offsets, con
                           uint64_t nbuf, uint64_t total_bytes, int checksum_enabled, uint32_t packet_limit,
                           uint64_t max_frames, fdb_packet_result* d_results, void* d_workspace,
                           uint64_t workspace_bytes, void* stream);
-/* Same with the library's per-stream workspace. */
+/* Same with the library's per-stream workspace.
+ * Both forms keep the walk's frame counter in a word of the stream's own
+ * (zeroed when the stream is first used, put back to zero by each call's last
+ * kernel: no memset per call), so calls on one stream run in stream order, and
+ * a captured graph of a call replays on one stream at a time.  Frames over
+ * 16 KiB take the XXH3 split route only when the packet limit allows them and
+ * the stream's previous batch had some (a host-mapped hint, no
+ * synchronisation); otherwise the row kernel hashes them -- the same digests,
+ * and no empty split-route launch for batches of short frames. */
 int fdb_packets_verify(const void* d_base, const uint64_t* d_buf_offsets, const uint64_t* d_buf_lengths,
                        uint64_t nbuf, uint64_t total_bytes, int checksum_enabled, uint32_t packet_limit,
                        uint64_t max_frames, fdb_packet_result* d_results, void* stream);

@@ -41,7 +41,10 @@ int fdb_sqlite_verify_pages(const void* d_pages, uint64_t page_size, uint64_t co
 int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad, void* stream);
 
 /* Caller-owned workspace variants (no allocation, capture-safe); size from
- * fdb_pagecheck_workspace_bytes(count), 16-byte aligned. */
+ * fdb_pagecheck_workspace_bytes(count), 16-byte aligned.  Every form keeps its
+ * list counters in words of the stream's own (zeroed when the stream is first
+ * used, put back to zero by each call's last kernel: no memset per call), so a
+ * captured graph of a call replays on one stream at a time. */
 uint64_t fdb_pagecheck_workspace_bytes(uint64_t count);
 int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno,
                                uint8_t* d_status, uint64_t* d_bad, void* d_workspace, uint64_t workspace_bytes,

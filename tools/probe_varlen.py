@@ -44,6 +44,8 @@ run("256 x 1M", [256] * (1 << 20), 256)
 run("64 x 1M", [64] * (1 << 20), 64)
 run("4000 x 256K (ragged)", [4000] * (1 << 18), 4096)
 run("zipf", W.zipf_lengths(), 256)
+run("zipf a64", W.zipf_lengths(), 64)
+run("zipf a16", W.zipf_lengths(), 16)
 run("small: 4096 x 1000", [4096] * 1000, 4096, reps=200)
 run("small: 1500 x 10000", [1500] * 10000, 2048, reps=200)
 run("small: 600 x 2000", [600] * 2000, 1024, reps=200)
