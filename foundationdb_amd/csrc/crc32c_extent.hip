@@ -836,6 +836,39 @@ __device__ void x_fallback(const XParams& P, const uint32_t* s4) {
 	}
 }
 
+// A buffer spanning more than kFinLongChain units (grabs) is not chained by
+// its own lane (one dependent table multiply per unit: a 300 MiB buffer on
+// 8-block grabs is 9600 of them, ~1 ms of one lane) but by its whole wave,
+// inside the pass (a uniform loop over the wave's long buffers): lane j
+// chains a 64th of the aggregates, weights its part by C^(units after it) =
+// M^(per * units), and the parts XOR-reduce (the aggregate chain is linear).
+constexpr uint32_t kFinLongChain = 64;
+// The aggregates of units [ws, we) chained by the wave (D = sum of agg[v] *
+// C^(we - 1 - v)): lane j Horner-combines units [ws + j*sl, ws + (j+1)*sl)
+// and carries its part past the units after it, * C^(we - its end) =
+// M^(per * units); the parts XOR-reduce.
+__device__ __forceinline__ uint32_t wave_chain(const uint32_t* agg, const uint32_t* lds, uint32_t cbase,
+                                                        const DevTables* T, uint64_t per, uint64_t ws, uint64_t we,
+                                                        uint32_t lane) {
+	const uint64_t n = we - ws, sl = (n + 63) / 64;
+	const uint64_t v0 = ws + lane * sl < we ? ws + lane * sl : we;
+	const uint64_t v1 = v0 + sl < we ? v0 + sl : we;
+	uint32_t part = 0;
+	for (uint64_t v = v0; v < v1; v += 4) {
+		uint32_t a[4];
+#pragma unroll
+		for (uint32_t t = 0; t < 4; ++t) a[t] = xld32(agg + (v + t < v1 ? v + t : v1 - 1));
+#pragma unroll
+		for (uint32_t t = 0; t < 4; ++t)
+			if (v + t < v1) part = lmul(lds, cbase, part) ^ a[t];
+	}
+	const uint64_t after = we - v1;
+	if (after && v1 > v0) part = xmul_blocks(T, part, (uint32_t)(per * after));
+#pragma unroll
+	for (int d = 32; d >= 1; d >>= 1) part ^= (uint32_t)__shfl_xor((int)part, d);
+	return part;
+}
+
 __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	__shared__ uint32_t lds[kFinWords];
 	const bool packed = x_packed(P);
@@ -885,6 +918,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	struct In {
 		u32x2 cs, ce;
 		uint64_t P0, P1;
+		uint64_t ws, we;  // the units holding its start and end (set by units())
 		uint32_t sd;
 		bool ok;
 	};
@@ -924,17 +958,23 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		}
 		return r;
 	};
-	auto finish = [&](const In& I) -> uint32_t {
+	// A buffer spanning units ws < we: the end point takes the aggregates of
+	// the units from ws to we - 1 (the start point's unit start is the origin)
+	auto units = [&](In& I) {
+		const uint32_t ks = x_blk(I.P0 - G.S), ke = x_blk(I.P1 - G.S);
+		I.ws = lgp < 64 ? ks >> lgp : ks / per;
+		I.we = lgp < 64 ? ke >> lgp : ke / per;
+	};
+	// Dq (long chains): the aggregate chain, computed by the wave
+	auto finish = [&](const In& I, bool queued, uint32_t Dq) -> uint32_t {
 		const uint64_t sp = I.P0 - G.S, ep = I.P1 - G.S;
-		const uint32_t ks = x_blk(sp), ke = x_blk(ep);
+		const uint32_t ke = x_blk(ep);
 		// G(p): the unit-local prefix at p64, positioned at its block's end
 		uint32_t ge = I.ce[0];
-		// A buffer spanning units ws < we: the end point takes the aggregates of
-		// the units from ws to we - 1 (the start point's unit start is the origin)
-		const uint64_t ws = lgp < 64 ? ks >> lgp : ks / per, we = lgp < 64 ? ke >> lgp : ke / per;
+		const uint64_t ws = I.ws, we = I.we;
 		if (ws != we) {
-			uint32_t D = 0;
-			for (uint64_t v = ws; v < we; v += 8) {  // eight aggregates in flight per round trip
+			uint32_t D = Dq;
+			for (uint64_t v = ws; !queued && v < we; v += 8) {  // eight aggregates in flight per round trip
 				uint32_t a[8];
 #pragma unroll
 				for (uint32_t t = 0; t < 8; ++t) a[t] = xld32(agg + (v + t < we ? v + t : we - 1));
@@ -958,13 +998,32 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 			rs = lmul(lds, kFinBp0 + 128 * (uint32_t)nbk, rs);
 		return ~(re ^ rs);
 	};
+	// Long chains (more than kFinLongChain units) are chained by the whole
+	// wave, one buffer at a time (uniform loop over the ballot), and the
+	// owning lane finishes with that D.
+	auto long_chains = [&](In& I, uint32_t& D) -> bool {
+		units(I);
+		const bool lg = I.ok && I.we - I.ws > kFinLongChain;
+		uint64_t m = __ballot(lg);
+		D = 0;
+		while (m) {
+			const int j = __builtin_ctzll(m);
+			m &= m - 1;
+			const uint64_t ws = rdlane64(I.ws, j), we = rdlane64(I.we, j);
+			const uint32_t d = wave_chain(agg, lds, cbase, T, per, ws, we, threadIdx.x & 63);
+			D = (int)(threadIdx.x & 63) == j ? d : D;
+		}
+		return lg;
+	};
 	const uint64_t span = (uint64_t)gridDim.x * blockDim.x;
 	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += 2 * span) {
 		In A, B;
 		load_in(A, i0 + threadIdx.x);
 		load_in(B, i0 + span + threadIdx.x);
-		const uint32_t ra = finish(A);
-		const uint32_t rb = finish(B);
+		uint32_t Da, Db;
+		const bool la = long_chains(A, Da), lb = long_chains(B, Db);
+		const uint32_t ra = finish(A, la, Da);
+		const uint32_t rb = finish(B, lb, Db);
 		if (A.ok) P.out[i0 + threadIdx.x] = ra;
 		if (B.ok) P.out[i0 + span + threadIdx.x] = rb;
 	}
