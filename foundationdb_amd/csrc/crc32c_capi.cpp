@@ -821,6 +821,64 @@ int fdb_sqlite_seal_pages(void* d_pages, uint64_t page_size, uint64_t count, uin
 	return fdb_sqlite_seal_pages_ws(d_pages, page_size, count, first_pgno, ws, have, stream);
 }
 
+// ---- the pager's codec hook over a batch (PageChecksumCodec::codec) ----------
+int fdb_sqlite_codec_pages_ws(void* d_pages, uint64_t page_size, uint32_t reserve_size, uint64_t count,
+                              uint32_t first_pgno, int op, uint8_t* d_status, void* d_workspace,
+                              uint64_t workspace_bytes, void* stream) {
+	// KeyValueStoreSQLite.cpp:206-208: writes are ops 6 (db page) and 7 (journal page); anything else must be 3
+	if (op != 3 && op != 6 && op != 7)
+		return fail(FDB_CRC32C_EINVAL, "fdb_sqlite_codec_pages: op must be 3 (read), 6 or 7 (write)");
+	if (count == 0) return 0;
+	if (int rc = pages_ok(d_pages, page_size, count, d_status, "fdb_sqlite_codec_pages: null pointer")) return rc;
+	if (!d_workspace || workspace_bytes < fdbpc::workspace_bytes(count) || reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_sqlite_codec_pages: workspace too small or misaligned");
+	const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+	const bool write = op != 3;
+	auto seal_status = [&](uint8_t* st, uint64_t n) -> int {  // a sealed page: codec() returns it (XXH3 trailer)
+		hipError_t e = hipMemsetAsync(st, 2, n, s);
+		return e == hipSuccess ? 0 : fail(FDB_CRC32C_EHIP, "fdb_sqlite_codec_pages: hipMemsetAsync", e);
+	};
+	if (reserve_size == 8) {  // sizeof(SumType): every page goes through checksum()
+		if (write) {
+			if (int rc = fdb_sqlite_seal_pages_ws(d_pages, page_size, count, first_pgno, d_workspace, workspace_bytes,
+			                                      stream))
+				return rc;
+			return seal_status(d_status, count);
+		}
+		return fdb_sqlite_verify_pages_ws(d_pages, page_size, count, first_pgno, d_status, nullptr, d_workspace,
+		                                  workspace_bytes, stream);
+	}
+	// any other reserve size: codec() returns nullptr for every page but page 1
+	// and leaves it untouched (:225-237); page 1 is checksummed as usual
+	hipError_t e = hipMemsetAsync(d_status, 0, count, s);
+	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "fdb_sqlite_codec_pages: hipMemsetAsync", e);
+	const uint64_t i1 = (uint32_t)(1u - first_pgno);
+	if (i1 >= count) return 0;
+	uint8_t* p1 = static_cast<uint8_t*>(d_pages) + i1 * page_size;
+	if (write) {
+		if (int rc = fdb_sqlite_seal_pages_ws(p1, page_size, 1, 1, d_workspace, workspace_bytes, stream)) return rc;
+		return seal_status(d_status + i1, 1);
+	}
+	return fdb_sqlite_verify_pages_ws(p1, page_size, 1, 1, d_status + i1, nullptr, d_workspace, workspace_bytes, stream);
+}
+
+int fdb_sqlite_codec_pages(void* d_pages, uint64_t page_size, uint32_t reserve_size, uint64_t count,
+                           uint32_t first_pgno, int op, uint8_t* d_status, void* stream) {
+	if (op != 3 && op != 6 && op != 7)
+		return fail(FDB_CRC32C_EINVAL, "fdb_sqlite_codec_pages: op must be 3 (read), 6 or 7 (write)");
+	if (count == 0) return 0;
+	if (int rc = pages_ok(d_pages, page_size, count, d_status, "fdb_sqlite_codec_pages: null pointer")) return rc;
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream), fdbpc::workspace_bytes(count), &ws, &have,
+	                              &hold))
+		return rc;
+	return fdb_sqlite_codec_pages_ws(d_pages, page_size, reserve_size, count, first_pgno, op, d_status, ws, have, stream);
+}
+
 int fdb_diskqueue_seal_pages_ws(void* d_pages, uint64_t count, void* d_workspace, uint64_t workspace_bytes,
                                 void* stream) {
 	if (count == 0) return 0;

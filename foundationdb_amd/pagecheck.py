@@ -32,6 +32,8 @@ def _lib():
         L.fdb_sqlite_seal_pages.argtypes = [vp, u64, u64, u32, vp]
         L.fdb_diskqueue_seal_pages.restype = ctypes.c_int
         L.fdb_diskqueue_seal_pages.argtypes = [vp, u64, vp]
+        L.fdb_sqlite_codec_pages.restype = ctypes.c_int
+        L.fdb_sqlite_codec_pages.argtypes = [vp, u64, u32, u64, u32, ctypes.c_int, vp, vp]
         _bound = True
     return L
 
@@ -113,3 +115,23 @@ def diskqueue_seal_pages(pages, count=None, stream=None):
         rc = _lib().fdb_diskqueue_seal_pages(_vp(pages), count, _stream_handle(stream))
     _check(rc, "fdb_diskqueue_seal_pages")
     return pages
+
+
+CODEC_READ, CODEC_WRITE_DB, CODEC_WRITE_JOURNAL = 3, 6, 7
+
+
+def sqlite_codec_pages(pages, page_size, op, reserve_size=8, count=None, first_pgno=1, stream=None, status=None):
+    """The pager's codec hook (PageChecksumCodec::codec, KeyValueStoreSQLite.cpp:203-244)
+    over a batch of pages, in place: op 3 verifies, ops 6 / 7 seal.  Returns
+    the status tensor: 0 where codec() returns nullptr, else the check that
+    accepted the page (reads) or 2 (writes).  Other ops raise CRC32CError, as
+    the reference asserts."""
+    count = _page_count(pages, page_size, count, "sqlite_codec_pages")
+    if status is None:
+        status = torch.empty(max(count, 1), dtype=torch.uint8, device=pages.device)
+    _require_device(status, "sqlite_codec_pages: status", pages.device, (torch.uint8,), count)
+    with torch.cuda.device(pages.device):
+        rc = _lib().fdb_sqlite_codec_pages(_vp(pages), page_size, reserve_size, count, first_pgno, op, _vp(status),
+                                           _stream_handle(stream))
+    _check(rc, "fdb_sqlite_codec_pages")
+    return status[:count]

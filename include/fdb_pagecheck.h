@@ -75,6 +75,23 @@ int fdb_diskqueue_seal_pages(void* d_pages, uint64_t count, void* stream);
 int fdb_diskqueue_seal_pages_ws(void* d_pages, uint64_t count, void* d_workspace, uint64_t workspace_bytes,
                                 void* stream);
 
+/* The pager's codec hook (PageChecksumCodec::codec, KeyValueStoreSQLite.cpp:203-244,
+ * registered through SQLite's xCodec, contrib/sqlite/sqlite3.h:3990-3996) over
+ * a batch of pages of one database, in place: op 3 (page read) verifies, ops 6
+ * and 7 (db page / journal page write) seal; any other op is refused with
+ * FDB_CRC32C_EINVAL (the reference asserts).  reserve_size is the codec's
+ * current reserve size (sizeChange): when it is not 8 (sizeof(SumType)) the
+ * hook returns nullptr for every page but page 1 and leaves them untouched
+ * (:225-237).  d_status[i] = 0 where codec() returns nullptr (a failed check,
+ * or that reserve-size rule), else the page is returned: for reads the check
+ * that accepted it (1 CRC-32C, 2 XXH3, 3 hashlittle2, as fdb_sqlite_verify_pages),
+ * for writes 2 (sealed with the XXH3 trailer; page 1 also at 1024 bytes). */
+int fdb_sqlite_codec_pages(void* d_pages, uint64_t page_size, uint32_t reserve_size, uint64_t count,
+                           uint32_t first_pgno, int op, uint8_t* d_status, void* stream);
+int fdb_sqlite_codec_pages_ws(void* d_pages, uint64_t page_size, uint32_t reserve_size, uint64_t count,
+                              uint32_t first_pgno, int op, uint8_t* d_status, void* d_workspace,
+                              uint64_t workspace_bytes, void* stream);
+
 /* Host-resident pages (a file scan reading pages from disk, as
  * checkAllPageChecksums does, KeyValueStoreSQLite.cpp:1378-1470, or a DiskQueue
  * recovery reading page runs, DiskQueue.cpp:1230-1290): the same verification

@@ -429,6 +429,19 @@ def sqlite_verify_page(page, pgno):
     return 3 if (c, b) == (part1, part2) else 0
 
 
+def sqlite_codec_page(page, pgno, reserve_size, op):
+    """PageChecksumCodec::codec (KeyValueStoreSQLite.cpp:203-244) on one page:
+    returns (status, page') -- status 0 where codec() returns nullptr, else
+    the accepting check (op 3) or 2 (ops 6 / 7, the page sealed)."""
+    assert op in (3, 6, 7)
+    page = np.array(np.frombuffer(bytes(page), np.uint8), copy=True)
+    if pgno != 1 and reserve_size != 8:  # :225-237
+        return 0, page
+    if op == 3:
+        return sqlite_verify_page(page, pgno), page
+    return 2, sqlite_seal_pages(page, page.size, 1, first_pgno=pgno)
+
+
 def diskqueue_hash(page, version):
     """Page::updateHash (DiskQueue.cpp:1089-1106): the 16-byte hash field for `version`."""
     page = bytes(page)
