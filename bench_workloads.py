@@ -724,6 +724,79 @@ class Xxh3Chunks(Xxh3Zipf):
                          port=lambda O_: O_.xxh3_batch_varlen(host, offs, lens, threads=1))
 
 
+class Xxh3Chained:
+    """XXH3-64 of packets laid over PacketBuffer chains (fdbrpc/FlowTransport.cpp:2025-2068:
+    XXH3_64bits over one buffer, reset / update per buffer / digest when the
+    packet spans several): the configs[2] Zipf packets serialized back to back
+    into 4 KiB PacketBuffers whose slots lie in HBM in shuffled order, one
+    chain of segments per packet (xxh3_gpu_batch_chained)."""
+    metric = ("device-resident XXH3-64 GiB/s on Zipf packets over shuffled 4 KiB PacketBuffer chains; "
+              "% of HBM-read peak")
+    kernel_name = "xxh3_gpu_batch_chained (segment scan + gather of multi-segment chains + fdbxxh varlen)"
+
+    def __init__(self, dev, rank, seg=4096):
+        from oracle import oracle as O
+        import foundationdb_amd.xxh3 as X
+        self.X = X
+        lens = zipf_lengths().astype(np.int64)
+        pos = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        total = int(lens.sum())
+        nbuf = (total + seg - 1) // seg
+        stream = O.splitmix64((nbuf * seg + 7) // 8, STATE).view(np.uint8)[:nbuf * seg]
+        slot = np.random.default_rng(7).permutation(nbuf).astype(np.int64)
+        host = np.empty(nbuf * seg, np.uint8)
+        host.reshape(nbuf, seg)[slot] = stream.reshape(nbuf, seg)  # buffer k lives at slot[k]
+        # one segment per (packet, buffer) it touches
+        b0, b1 = pos // seg, (pos + lens - 1) // seg
+        nseg = (b1 - b0 + 1)
+        pk = np.repeat(np.arange(lens.size), nseg)
+        bk = np.repeat(b0, nseg) + (np.arange(nseg.sum()) - np.repeat(np.cumsum(nseg) - nseg, nseg))
+        lo = np.maximum(pos[pk], bk * seg)
+        hi = np.minimum(pos[pk] + lens[pk], (bk + 1) * seg)
+        self.h_seg_off = slot[bk] * seg + (lo - bk * seg)
+        self.h_seg_len = hi - lo
+        self.h_starts = np.concatenate([[0], np.cumsum(nseg)])
+        self.h_pos, self.h_lens, self.stream = pos, lens, stream
+        self.buf = torch.from_numpy(host).to(dev)
+        self.seg_off = torch.from_numpy(self.h_seg_off).to(dev)
+        self.seg_len = torch.from_numpy(self.h_seg_len).to(dev)
+        self.starts = torch.from_numpy(self.h_starts).to(dev)
+        self.total = total
+        self.out = torch.empty(lens.size, dtype=torch.uint64, device=dev)
+        self.bytes_per_step = total
+        # payload + per segment (offset, length) + per chain (start, digest)
+        self.algorithmic_bytes_per_step = total + 16 * int(nseg.sum()) + 16 * lens.size
+        multi = nseg > 1
+        self.data_desc = (f"synthetic: splitmix64 stream (state 0x{STATE:X}) in {nbuf} shuffled {seg} B "
+                          f"PacketBuffers; {lens.size} Zipf packets, {int(multi.sum())} spanning 2+ buffers "
+                          f"({int(lens[multi].sum()) >> 20} MiB)")
+        self.config = {"workload": f"{lens.size} Zipf(1.0) 64 B - 16 KiB packets over {seg} B PacketBuffer chains "
+                                   f"({int(nseg.sum())} segments)", "packets": int(lens.size),
+                       "segments": int(nseg.sum()), "total_bytes": total}
+
+    def step(self, stream):
+        self.X.batch_chained(self.buf, self.seg_off, self.seg_len, self.starts, total_bytes=self.total,
+                             out=self.out, stream=stream)
+
+    def verify(self):
+        from oracle import oracle as O
+        got = self.out.cpu().numpy().view(np.uint64)
+        want = O.ref_xxh3_batch_varlen(self.stream, self.h_pos.astype(np.uint64), self.h_lens.astype(np.uint64)) \
+            if O.xxh3_reference_available() else O.xxh3_batch_varlen(self.stream, self.h_pos, self.h_lens)
+        return bool(np.array_equal(got, want))
+
+    def cpu_sample(self):
+        k = 120000
+        end = int(self.h_pos[k - 1] + self.h_lens[k - 1])
+        host = self.stream[:end]
+        offs, lens = self.h_pos[:k].astype(np.uint64), self.h_lens[:k].astype(np.uint64)
+        return CpuSample(f"first {k} packets ({int(lens.sum()) >> 20} MiB) contiguous, reference flow/xxhash.c "
+                         "XXH3_64bits (the reference's chained update over the same bytes does no less work)",
+                         int(lens.sum()), host,
+                         ref=lambda O_: O_.ref_xxh3_batch_varlen(host, offs, lens),
+                         port=lambda O_: O_.xxh3_batch_varlen(host, offs, lens, threads=1))
+
+
 class PacketsVerify:
     """FlowTransport receive verification (scanPackets, fdbrpc/FlowTransport.cpp:1260-1366)
     over many connections' receive buffers at once (fdb_packets_verify, include/fdb_packets.h):
@@ -818,4 +891,5 @@ WORKLOADS = {
     "sqlite-seal": lambda dev, rank: SqliteSeal(dev, rank),
     "diskqueue-seal": lambda dev, rank: DiskQueueSeal(dev, rank),
     "packets-verify": lambda dev, rank: PacketsVerify(dev, rank),
+    "xxh3-chained": lambda dev, rank: Xxh3Chained(dev, rank),
 }

@@ -102,45 +102,84 @@ __global__ __launch_bounds__(kScanT) void k_seg_scan(const uint64_t* __restrict_
 	}
 }
 
-// Segment j -> staging[pre[j], pre[j] + len[j]).  Bytes past `cap` are
-// dropped (the caller's total_bytes bound was wrong: results undefined, but no
-// write leaves the staging area).
+// Segment j -> staging[pre[j], pre[j] + len[j]), for the segments of chains
+// of two or more (segflag[j] == 0; a one-segment chain is hashed where it
+// lies).  Bytes past `cap` are dropped (the caller's total_bytes bound was
+// wrong: results undefined, but no write leaves the staging area).  One wave
+// per 64 consecutive segments: their metadata in the lanes (one load each),
+// then segment after segment, the body in 16-byte pieces -- aligned in
+// staging (the staging area is 16-byte aligned), loaded from the segment at
+// whatever alignment it has, four pieces per lane in flight -- and the < 16
+// bytes before and after it byte by byte.  (One workgroup per segment spent
+// its time on the metadata round trip: 509 us for the bench's 900 MiB.)
 __global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                     const uint64_t* __restrict__ len, const uint64_t* __restrict__ pre,
-                                                    uint64_t nsegs, uint8_t* __restrict__ staging, uint64_t cap) {
-	for (uint64_t j = blockIdx.x; j < nsegs; j += gridDim.x) {
-		const uint8_t* src = base + off[j];
-		const uint64_t n = len[j], d = pre[j];
-		uint8_t* dst = staging + d;
-		const uint64_t lim = d >= cap ? 0 : (cap - d < n ? cap - d : n);
-		// 4-byte words where source and destination agree mod 4, bytes otherwise
-		const uint64_t mis = (reinterpret_cast<uintptr_t>(src) ^ reinterpret_cast<uintptr_t>(dst)) & 3;
-		uint64_t head = mis ? lim : (4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3;
-		if (head > lim) head = lim;
-		for (uint64_t k = threadIdx.x; k < head; k += blockDim.x) dst[k] = src[k];
-		if (!mis) {
-			const uint64_t nw = (lim - head) / 4;
-			const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src + head);
-			uint32_t* d4 = reinterpret_cast<uint32_t*>(dst + head);
-			for (uint64_t k = threadIdx.x; k < nw; k += blockDim.x) d4[k] = s4[k];
-			for (uint64_t k = head + 4 * nw + threadIdx.x; k < lim; k += blockDim.x) dst[k] = src[k];
+                                                    const uint8_t* __restrict__ segflag, uint64_t nsegs,
+                                                    uint8_t* __restrict__ staging, uint64_t cap) {
+	typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+	typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+	typedef __attribute__((address_space(1))) const u32x4u g_u32x4u;
+	const uint32_t lane = threadIdx.x & 63;
+	const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	for (uint64_t j0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; j0 < nsegs; j0 += 64 * nw) {
+		const uint64_t jl = j0 + lane < nsegs ? j0 + lane : nsegs - 1;
+		const uint64_t m_off = off[jl], m_len = len[jl], m_pre = pre[jl];
+		const bool m_on = j0 + lane < nsegs && segflag[jl] == 0;
+		uint64_t todo = __ballot(m_on);
+		while (todo) {
+			const int k = __builtin_ctzll(todo);
+			todo &= todo - 1;
+			const uint64_t so = __shfl(m_off, k), n = __shfl(m_len, k), d = __shfl(m_pre, k);
+			const uint8_t* src = base + so;
+			uint8_t* dst = staging + d;
+			const uint64_t lim = d >= cap ? 0 : (cap - d < n ? cap - d : n);
+			uint64_t head = (16 - (d & 15)) & 15;
+			head = head < lim ? head : lim;
+			const uint64_t body = (lim - head) & ~uint64_t(15);
+			if (lane < head) dst[lane] = src[lane];
+			for (uint64_t q = head; q < head + body; q += 4 * 1024) {
+				u32x4u v[4];
+#pragma unroll
+				for (int u = 0; u < 4; ++u) {
+					const uint64_t o = q + 1024ull * u + 16ull * lane;
+					v[u] = __builtin_nontemporal_load((g_u32x4u*)reinterpret_cast<uintptr_t>(src + (o < head + body ? o : head)));
+				}
+#pragma unroll
+				for (int u = 0; u < 4; ++u) {
+					const uint64_t o = q + 1024ull * u + 16ull * lane;
+					if (o < head + body) *reinterpret_cast<u32x4*>(dst + o) = u32x4{v[u][0], v[u][1], v[u][2], v[u][3]};
+				}
+			}
+			const uint64_t t0 = head + body;
+			if (t0 + lane < lim) dst[t0 + lane] = src[t0 + lane];
 		}
 	}
 }
 
 // Ranges are clamped into the staging area [0, cap) and the chain starts to
 // [0, nsegs]: a wrong total_bytes (or chain start) gives undefined digests,
-// never a read past the staging area or past pre[].
+// never a read past the staging area or past pre[].  A chain of one segment
+// is hashed in place: its offset is taken relative to the staging area
+// (64-bit wrap-around: the kernels add it to the staging address), and its
+// segment is flagged so that the gather skips it.
 __global__ __launch_bounds__(256) void k_chain_ranges(const uint64_t* __restrict__ starts, uint64_t nchains,
                                                       uint64_t nsegs, const uint64_t* __restrict__ pre, uint64_t cap,
-                                                      uint64_t* __restrict__ ch_off, uint64_t* __restrict__ ch_len) {
+                                                      const uint8_t* __restrict__ base,
+                                                      const uint64_t* __restrict__ seg_off,
+                                                      const uint8_t* __restrict__ staging,
+                                                      uint8_t* __restrict__ segflag, uint64_t* __restrict__ ch_off,
+                                                      uint64_t* __restrict__ ch_len) {
 	const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (c >= nchains) return;
-	const uint64_t s0 = starts[c], s1 = starts[c + 1];
-	uint64_t a = pre[s0 < nsegs ? s0 : nsegs], b = pre[s1 < nsegs ? s1 : nsegs];
+	uint64_t s0 = starts[c], s1 = starts[c + 1];
+	s0 = s0 < nsegs ? s0 : nsegs;
+	s1 = s1 < nsegs ? s1 : nsegs;
+	uint64_t a = pre[s0], b = pre[s1];
 	a = a < cap ? a : cap;
 	b = b < cap ? b : cap;
-	ch_off[c] = a;
+	const bool one = s1 == s0 + 1;
+	for (uint64_t j = s0; j < s1; ++j) segflag[j] = one ? 1 : 0;
+	ch_off[c] = one ? reinterpret_cast<uint64_t>(base) + seg_off[s0] - reinterpret_cast<uint64_t>(staging) : a;
 	ch_len[c] = b > a ? b - a : 0;
 }
 
@@ -148,7 +187,8 @@ static uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 
 uint64_t xxh3_chain_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes, uint64_t nwave) {
 	const uint64_t nb = nsegs / kScanSpan + 1;  // the scan covers nsegs + 1 entries (pre[nsegs] = total)
-	return al16(8 * (nb + 1)) + al16(8 * (nsegs + 1)) + 2 * al16(8 * nchains) + al16(total_bytes + 16) +
+	return al16(8 * (nb + 1)) + al16(8 * (nsegs + 1)) + 2 * al16(8 * nchains) + al16(nsegs + 1) +
+	       al16(total_bytes + 16) +
 	       al16(xxh3_workspace_bytes_for(nchains ? nchains : 1, nwave, xxh3_long_blocks_bound(total_bytes)));
 }
 
@@ -165,6 +205,8 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	p += al16(8 * nchains);
 	uint64_t* ch_len = reinterpret_cast<uint64_t*>(p);
 	p += al16(8 * nchains);
+	uint8_t* segflag = p;
+	p += al16(nsegs + 1);
 	uint8_t* staging = p;
 	p += al16(total_bytes + 16);
 	void* eng = p;
@@ -172,13 +214,16 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 		k_seg_bsum<<<(unsigned)nb, kScanT, 0, s>>>(seg_len, nsegs, bsum);
 		k_seg_bscan<<<1, kScanT, 0, s>>>(bsum, nb);
 		k_seg_scan<<<(unsigned)nb, kScanT, 0, s>>>(seg_len, nsegs, bsum, pre);
-		const uint64_t g = nsegs < 65536 ? nsegs : 65536;
-		k_seg_gather<<<(unsigned)g, 256, 0, s>>>(base, seg_off, seg_len, pre, nsegs, staging, total_bytes);
 	} else if (hipMemsetAsync(pre, 0, 8, s) != hipSuccess) {
 		return -1;
 	}
-	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, nsegs, pre, total_bytes, ch_off,
-	                                                                   ch_len);
+	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, nsegs, pre, total_bytes, base,
+	                                                                   seg_off, staging, segflag, ch_off, ch_len);
+	if (nsegs) {
+		const uint64_t g = (nsegs + 255) / 256;  // a wave per 64 segments
+		k_seg_gather<<<(unsigned)(g < 65536 ? g : 65536), 256, 0, s>>>(base, seg_off, seg_len, pre, segflag, nsegs,
+		                                                                   staging, total_bytes);
+	}
 	XxhParams P{};
 	P.base = staging;
 	P.offsets = ch_off;
