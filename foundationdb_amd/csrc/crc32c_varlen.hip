@@ -348,6 +348,10 @@ __device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len, uint64_t bigmin 
 	g.zt = (uint32_t)(E - P1);
 	return g;
 }
+#ifndef FDBCRC_SELFSUM_UB
+#define FDBCRC_SELFSUM_UB 2
+#define FDBCRC_SELFSUM_UW 4
+#endif
 struct V7Params {
 	const uint8_t* base;
 	const uint64_t* offsets;   // nullptr: fixed stride
@@ -684,15 +688,18 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		// the predecessors' geometry recomputed here, eight buffers per thread
 		// in flight at once
 		const uint64_t n = (uint64_t)tile * kTileW;
-		for (uint64_t j0 = threadIdx.x; j0 < n; j0 += 8 * blockDim.x) {
-			uint64_t o[8], l[8];
+		// (SU buffers in flight per thread: 8 spilled 36 SGPRs with the block
+		// route's geometry, 2 spill none there; the windows-only form takes 4)
+		constexpr uint32_t SU = BIG ? FDBCRC_SELFSUM_UB : FDBCRC_SELFSUM_UW;
+		for (uint64_t j0 = threadIdx.x; j0 < n; j0 += SU * blockDim.x) {
+			uint64_t o[SU], l[SU];
 #pragma unroll
-			for (uint32_t u = 0; u < 8; ++u) {
+			for (uint32_t u = 0; u < SU; ++u) {
 				const uint64_t j = j0 + u * blockDim.x;
 				v7_buffer(P, j < n ? j : 0, o[u], l[u]);
 			}
 #pragma unroll
-			for (uint32_t u = 0; u < 8; ++u) {
+			for (uint32_t u = 0; u < SU; ++u) {
 				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o[u], l[u], bigmin);
 				const bool in = j0 + u * blockDim.x < n;
 				pre = sadd(pre, in ? gj.W : 0u);

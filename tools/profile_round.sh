@@ -7,7 +7,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-ROUND=${ROUND:-round4}
+ROUND=${ROUND:-round5}
 R=gpurun_out/$ROUND
 P=gpurun_out/pmc
 mkdir -p $R $P
@@ -18,7 +18,7 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-me
 tail -1 $R/pytest_gpu.txt
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $R/smoke.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $R/bench_pages4k.json 2> $R/bench_pages4k.err || exit 1
-for w in pages8k zipf chunks chunks-host pages4k-host xxh3-pages4k xxh3-zipf xxh3-chunks sqlite-verify sqlite-verify-host diskqueue-verify packets-verify; do
+for w in pages8k zipf chunks chunks-host pages4k-host xxh3-pages4k xxh3-zipf xxh3-chunks xxh3-chained sqlite-verify sqlite-verify-host diskqueue-verify sqlite-seal diskqueue-seal packets-verify; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --cpu-seconds 5 > $R/bench_$w.json 2> $R/bench_$w.err || { tail -3 $R/bench_$w.err; exit 1; }
 done
 echo benches done
@@ -31,7 +31,7 @@ for f in $R/bench_*.json; do echo "$f $(cut -c1-200 $f)"; done
 exit 0
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_pages4k -o pages4k -- python bench.py --cpu-seconds 0 > $R/prof_pages4k.log 2>&1 || exit 1
-for w in pages8k zipf chunks xxh3-pages4k xxh3-zipf xxh3-chunks sqlite-verify diskqueue-verify packets-verify; do
+for w in pages8k zipf chunks xxh3-pages4k xxh3-zipf xxh3-chunks xxh3-chained sqlite-verify diskqueue-verify sqlite-seal diskqueue-seal packets-verify; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_$w -o $w -- python bench.py --workload $w --steps 20 --cpu-seconds 0 --no-verify > $R/prof_$w.log 2>&1 || exit 1
 done
 echo rocprof done
