@@ -324,3 +324,99 @@ def test_gpu_sqlite_codec_pages(cuda, page_size):
     for op in (0, 2, 5, 8):
         with pytest.raises(CRC32CError):
             PC.sqlite_codec_pages(d, page_size, op)
+
+
+@pytest.mark.gpu
+def test_gpu_verify_and_seal_replay_from_a_hip_graph(cuda):
+    """The _ws forms launch without allocating or synchronising; their counters
+    live in the stream's own words and every call's last kernel puts them back
+    to zero, so a captured graph of a seal and two verifications replays
+    correctly again and again (a counter left non-zero would shift every later
+    list)."""
+    import ctypes
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    L = PC._lib()
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    L.fdb_sqlite_verify_pages_ws.argtypes = [vp, u64, u64, u32, vp, vp, vp, u64, vp]
+    L.fdb_diskqueue_check_pages_ws.argtypes = [vp, u64, vp, vp, vp, u64, vp]
+    L.fdb_sqlite_seal_pages_ws.argtypes = [vp, u64, u64, u32, vp, u64, vp]
+    pages, exp = make_sqlite_batch(1500, 4096, 3, 77)
+    dq, dq_exp = make_dq_batch(1200, 78)
+    raw = sm_bytes(700 * 4096, 79)
+    sealed = O.sqlite_seal_pages(raw, 4096, 700, 1)
+    d_sq = torch.from_numpy(pages.reshape(-1).copy()).to(cuda)
+    d_dq = torch.from_numpy(dq.reshape(-1).copy()).to(cuda)
+    d_raw = torch.from_numpy(raw.copy()).to(cuda)
+    nws = int(L.fdb_pagecheck_workspace_bytes(1500))
+    ws = torch.empty(nws, dtype=torch.uint8, device=cuda)
+    st = torch.empty(1500, dtype=torch.uint8, device=cuda)
+    ok = torch.empty(1200, dtype=torch.uint8, device=cuda)
+    bad = torch.empty(2, dtype=torch.int64, device=cuda)
+    s = torch.cuda.Stream(cuda)
+    h = ctypes.c_void_p(s.cuda_stream)
+
+    def calls():
+        assert L.fdb_sqlite_seal_pages_ws(d_raw.data_ptr(), 4096, 700, 1, ws.data_ptr(), nws, h) == 0
+        assert L.fdb_sqlite_verify_pages_ws(d_sq.data_ptr(), 4096, 1500, 3, st.data_ptr(), bad.data_ptr(),
+                                            ws.data_ptr(), nws, h) == 0
+        assert L.fdb_diskqueue_check_pages_ws(d_dq.data_ptr(), 1200, ok.data_ptr(), bad.data_ptr() + 8,
+                                              ws.data_ptr(), nws, h) == 0
+    with torch.cuda.stream(s):
+        calls()  # warm: the stream's counter words are allocated on first use
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        calls()
+    for rep in range(3):
+        st.zero_()
+        ok.zero_()
+        bad.fill_(-1)
+        d_raw.copy_(torch.from_numpy(raw))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), exp), rep
+        assert np.array_equal(ok.cpu().numpy(), dq_exp), rep
+        b = bad.cpu().numpy()
+        assert b[0] == int((exp == 0).sum()) and b[1] == int((dq_exp == 0).sum()), rep
+        assert np.array_equal(d_raw.cpu().numpy(), sealed), rep
+    del g
+
+
+@pytest.mark.gpu
+def test_gpu_verifiers_between_other_calls_on_one_stream(cuda):
+    """The library's per-stream workspace is shared by every API on the stream;
+    the verifiers' and the packet walk's counters are not in it, so verify,
+    XXH3 and CRC varlen batches and packet verification interleaved on one
+    stream all stay correct."""
+    import torch
+    import foundationdb_amd as F
+    import foundationdb_amd.pagecheck as PC
+    import foundationdb_amd.xxh3 as X
+    pages, exp = make_sqlite_batch(900, 4096, 1, 81)
+    dq, dq_exp = make_dq_batch(700, 82)
+    d_sq = torch.from_numpy(pages.reshape(-1).copy()).to(cuda)
+    d_dq = torch.from_numpy(dq.reshape(-1).copy()).to(cuda)
+    rng = np.random.default_rng(83)
+    h = sm_bytes(8 << 20, 84)
+    lens = rng.integers(0, 40000, 500)
+    offs = rng.integers(0, h.size - lens)
+    d = torch.from_numpy(h).to(cuda)
+    o, l = torch.from_numpy(offs).to(cuda), torch.from_numpy(lens).to(cuda)
+    want_x = O.xxh3_batch_varlen(h, offs, lens)
+    want_c = O.batch_varlen(h, offs, lens)
+    s = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(s):
+        for rep in range(3):
+            st, b1 = PC.sqlite_verify_pages(d_sq, 4096, stream=s)
+            gx = X.batch_varlen(d, o, l, stream=s)
+            ok, b2 = PC.diskqueue_check_pages(d_dq, stream=s)
+            gc = F.batch_varlen(d, o, l, stream=s)
+            s.synchronize()
+            assert np.array_equal(st.cpu().numpy(), exp) and np.array_equal(ok.cpu().numpy(), dq_exp), rep
+            assert int(b1.cpu().numpy().view(np.uint64)[0]) == int((exp == 0).sum())
+            assert int(b2.cpu().numpy().view(np.uint64)[0]) == int((dq_exp == 0).sum())
+            assert np.array_equal(gx.cpu().numpy().view(np.uint64), want_x)
+            assert np.array_equal(gc.cpu().numpy().view(np.uint32), want_c)
+    F.release_stream(s)
