@@ -854,7 +854,7 @@ __device__ __forceinline__ uint32_t wave_chain(const uint32_t* agg, const uint32
 	const uint64_t v0 = ws + lane * sl < we ? ws + lane * sl : we;
 	const uint64_t v1 = v0 + sl < we ? v0 + sl : we;
 	uint32_t part = 0;
-	for (uint64_t v = v0; v < v1; v += 4) {
+	for (uint64_t v = v0; v < v1; v += 4) {  // four aggregates per round trip (eight: an SGPR spill)
 		uint32_t a[4];
 #pragma unroll
 		for (uint32_t t = 0; t < 4; ++t) a[t] = xld32(agg + (v + t < v1 ? v + t : v1 - 1));
@@ -960,10 +960,13 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	};
 	// A buffer spanning units ws < we: the end point takes the aggregates of
 	// the units from ws to we - 1 (the start point's unit start is the origin)
+	// (a lane past the batch holds a clamped copy of the last buffer: it chains
+	// nothing -- its result is discarded, and a huge last buffer's chain run by
+	// every idle lane of the grid took 14 ms for one 1.1 GB buffer)
 	auto units = [&](In& I) {
 		const uint32_t ks = x_blk(I.P0 - G.S), ke = x_blk(I.P1 - G.S);
 		I.ws = lgp < 64 ? ks >> lgp : ks / per;
-		I.we = lgp < 64 ? ke >> lgp : ke / per;
+		I.we = !I.ok ? I.ws : (lgp < 64 ? ke >> lgp : ke / per);
 	};
 	// Dq (long chains): the aggregate chain, computed by the wave
 	auto finish = [&](const In& I, bool queued, uint32_t Dq) -> uint32_t {

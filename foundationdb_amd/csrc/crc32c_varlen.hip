@@ -509,6 +509,26 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 	}
 }
 
+// wq[g] = v for g in [lo, hi): a lane writes a short range itself; a range of
+// more than 64 grabs (a buffer spanning them, e.g. one of a few huge buffers)
+// is written by the whole wave, 64 entries per store -- one lane writing a
+// 1.1 GB buffer's 34 k entries took 581 us.  Every lane of the wave calls it
+// (on = false: no range of its own).
+__device__ __forceinline__ void fill_grab_map(uint32_t* wq, uint64_t lo, uint64_t hi, uint32_t v, bool on) {
+	const bool lng = on && hi > lo + 64;
+	if (on && !lng)
+		for (uint64_t g = lo; g < hi; ++g) wq[g] = v;
+	uint64_t m = __ballot(lng);
+	const uint32_t lane = threadIdx.x & 63;
+	while (m) {
+		const int j = __builtin_ctzll(m);
+		m &= m - 1;
+		const uint64_t a = __shfl(lo, j), b = __shfl(hi, j);
+		const uint32_t x = (uint32_t)__shfl((int)v, j);
+		for (uint64_t g = a + lane; g < b; g += 64) wq[g] = x;
+	}
+}
+
 // The extent route's only planning pass (crc32c_extent.hip): the packing and
 // extent checks (epoch-tagged flags), the stream's route statistics (tile 0)
 // and k_xgrab's grab map, from one coalesced load of each buffer's offset and
@@ -542,19 +562,23 @@ __global__ __launch_bounds__(256) void k_xcount(V7Params P) {
 		if (P.hstat) P.hstat[kHstatNblk] = nblk;
 	}
 	if (blockIdx.x == 0 && P.hstat) v7_route_stats(P, i, off, len, s_stat);
-	if (P.xwq && in && nblk && E - S < kXMaxExtent && !bad) {
+	// (every lane reaches both calls: a wave fills long ranges together)
+	const bool act = P.xwq && in && nblk && E - S < kXMaxExtent && !bad;
+	uint64_t lo0 = 0, hi0 = 0, glo = 0, ghi = 0;
+	uint32_t v = 0;
+	if (act) {
 		const uint64_t gsz = x_gsz(nblk, P.xcapg), ngrab = (nblk + gsz - 1) / gsz;
 		const uint32_t lt = 12 + x_log2(gsz);  // bytes per grab: 2^lt
 		const uint64_t base = reinterpret_cast<uint64_t>(P.base);
 		const uint64_t ei = base + e - S;  // (>= 0 for an ordered pair)
 		auto ceil_g = [&](uint64_t p) { return (p + (1ull << lt) - 1) >> lt; };
-		if (i == 0)
-			for (uint64_t g = 0; g < ceil_g(ei) && g < ngrab; ++g) P.xwq[g] = 0;
-		const uint64_t glo = ceil_g(ei);
-		const uint64_t ghi = has_next ? ceil_g(base + on + ln - S) : ngrab;
-		const uint32_t v = has_next ? (uint32_t)(i + 1) : (uint32_t)P.count;
-		for (uint64_t g = glo; g < ghi && g < ngrab; ++g) P.xwq[g] = v;
+		if (i == 0) hi0 = min(ceil_g(ei), ngrab);
+		glo = ceil_g(ei);
+		ghi = min(has_next ? ceil_g(base + on + ln - S) : ngrab, ngrab);
+		v = has_next ? (uint32_t)(i + 1) : (uint32_t)P.count;
 	}
+	fill_grab_map(P.xwq, lo0, hi0, 0u, act && i == 0);
+	fill_grab_map(P.xwq, glo, ghi, v, act);
 }
 
 // BIG: the block route is on (bigmin != 0); without it the route's sums
