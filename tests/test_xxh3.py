@@ -171,6 +171,27 @@ def test_gpu_fixed_lengths_vs_oracle(cuda):
 
 
 @pytest.mark.gpu
+def test_gpu_fixed_rows_eight_byte_aligned(cuda):
+    """The row kernel's 8-byte-aligned form: rows starting at 8 mod 16 (the
+    DiskQueue V2 region) load 16-byte aligned and shift by 8 bytes across
+    lanes; a stride of 8 mod 16 (rows alternating 0 / 8 mod 16) keeps the
+    exact loads.  Lengths around the block and stripe boundaries, batches that
+    start at the tensor's first byte."""
+    import foundationdb_amd.xxh3 as X
+    h = sm_bytes(3 << 20, 0x5EA8)
+    d = dev_bytes(h, cuda)
+    for off, stride in ((8, 4096), (8, 2048), (8, 8192), (0, 4104), (8, 4104), (24, 1040)):
+        for length in (241, 1000, 1024, 1025, 1032, 2047, 2048, 2049, 3000, 4088):
+            if length > stride - (off & 15) and stride < 4096:
+                continue
+            count = min(300, (h.size - off - length) // stride + 1)
+            for seed in (0, 0x1234567):
+                got = host(X.batch_fixed(d, stride, length, count, seed=seed, byte_offset=off))
+                want = O.xxh3_batch_fixed(h[off:], stride, length, count, seed=seed)
+                assert np.array_equal(got, want), (off, stride, length, seed)
+
+
+@pytest.mark.gpu
 def test_gpu_varlen_random_vs_oracle(cuda):
     import torch
     import foundationdb_amd.xxh3 as X
