@@ -41,10 +41,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
 typedef __attribute__((address_space(1))) const uint64_t g_u64;
 
-__device__ __forceinline__ uint32_t rdfirst(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-__device__ __forceinline__ uint64_t rdfirst64(uint64_t v) {
-	return ((uint64_t)rdfirst((uint32_t)(v >> 32)) << 32) | (uint64_t)rdfirst((uint32_t)v);
-}
 
 
 }  // namespace

@@ -901,7 +901,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 	// ac: the rows that need a buffer pull theirs with ds_bpermute, all rows
 	// at once (a serial pick per row cost ~40 instructions a buffer, the
 	// bound for buffers of a block or two).
-	uint64_t ab = 0, bb = 0, pnext = begin;
+	uint64_t bb = 0, pnext = begin;
 	uint64_t alen = 0, aoff = 0, aseed = 0, blen = 0, boff = 0, bseed = 0;
 	uint32_t aj = 0, bfl = 0, na = 0, ac = 0;
 	bool bpend = false;  // B loaded, not yet taken (uniform)
