@@ -428,14 +428,23 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	uint32_t q = 0;
 	uint32_t wbs, wbe, wcs, wce, wqs, wqe, wlast;
 	uint32_t Vs = 0, Ve = 0, Ys = 0, Ye = 0;
-	uint64_t pf0 = 0, pf1 = 0;  // the next window's buffer (prefetched)
+	// The next window's buffer, prefetched as the raw offset and length: any
+	// arithmetic on them here would wait on the loads at once -- and, the
+	// counter being in order, on every block load issued before them.
+	uint64_t pf0 = 0, pf1 = 0;
+	const uint64_t bS = reinterpret_cast<uint64_t>(P.base) - G.S;
+	// (unconditional loads, a strided batch's from the extent start: a load
+	// under a branch leaves the wait counter unknown where the paths join)
 	auto prefetch = [&](uint32_t q0) {
 		const uint32_t j = q0 + lane < cnt32 ? q0 + lane : cnt32 - 1;
-		x_buffer(P, j, pf0, pf1);
+		const uint64_t* const dflt = reinterpret_cast<const uint64_t*>(G.S);
+		pf0 = xld64(P.offsets ? P.offsets + j : dflt);
+		pf1 = xld64(P.lengths ? P.lengths + j : dflt);
 	};
 	auto make_window = [&](uint32_t q0) {
 		const bool ok = q0 + lane < cnt32;
-		const uint64_t s = pf0 - G.S, e = pf1 - G.S;
+		const uint32_t j = ok ? q0 + lane : cnt32 - 1;
+		const uint64_t s = bS + (P.offsets ? pf0 : (uint64_t)j * P.stride), e = s + (P.lengths ? pf1 : P.length);
 		wbs = ok ? x_blk(s) : 0xFFFFFFFEu;
 		wbe = ok ? x_blk(e) : 0xFFFFFFFEu;
 		wcs = x_cnt(s, wbs);
@@ -573,13 +582,19 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 #pragma unroll
 		for (uint32_t j = 0; j < kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
 		const uint32_t kn = k + kXU < kend ? k + kXU : kend;
-		while (wlast < kn) {  // every buffer of the window ends in the blocks so far: the next 64
+		auto retire = [&]() {  // every buffer of the window ends in the blocks so far: the next 64
 			flush(q, gb0, gb1);
 			q += 64;
 			make_window(q);
 			prefetch(q + 64);
 #pragma unroll
 			for (uint32_t j = 0; j < kXU; ++j) capture(H[j], Y[j], Z[j], k + j, k + j < kend);
+		};
+		// (the first retirement peeled: a loop's wait on the window loads would
+		// assume they were just issued, and drain the next unit's block loads)
+		if (wlast < kn) {
+			retire();
+			while (wlast < kn) retire();
 		}
 	};
 
@@ -622,14 +637,14 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 
 	// ---- dynamic grabs: steps of 4 blocks, two units in ping-pong ----------
 	uint32_t s = 0;
+	uint32_t wqv = 0;
 	while (gA < nd) {
 		const uint32_t gb0 = gA * gsz, gb1 = gb0 + gsz;
 		const uint32_t k = gb0 + 4 * s;
 		uint32_t qnx = 0;
-		if (s == 0) {  // the grab's window (its metadata was prefetched a grab ahead)
-			make_window(q);
-			prefetch(q + 64);
+		if (s == 0) {
 			X = 0;
+			wqv = xld32(P.x.wq + (gB < nd ? gB : 0u));  // the next grab's window start, read at this grab's end
 		}
 		load_step_unit(u1, gA, s, 1);
 		__builtin_amdgcn_sched_barrier(0);
@@ -638,9 +653,14 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			unit_h(u0, H, Y);
 			__builtin_amdgcn_sched_barrier(0);
 			const bool last_step = s + 1 == spg;
-			uint32_t qnx0 = 0;
-			if (last_step && gB < nd) qnx0 = wq_of(gB);  // (ahead of the next unit's loads)
-			qnx = qnx0;
+			qnx = last_step ? rdfirst(wqv) : 0u;
+			// the grab's window (its metadata prefetched a grab ahead; the next
+			// window's loads issued ahead of the next unit's, so that a window
+			// retired in this unit waits only for them)
+			if (s == 0) {
+				make_window(q);
+				prefetch(q + 64);
+			}
 			// the next unit's loads go out before this unit's points are captured
 			load_step_unit(u0, last_step ? gB : gA, last_step ? 0u : s + 1, 0);
 			__builtin_amdgcn_sched_barrier(0);

@@ -350,6 +350,8 @@ __device__ __forceinline__ Geo7 geo7(uint64_t P0, uint64_t len, uint64_t bigmin 
 }
 #ifndef FDBCRC_SELFSUM_UB
 #define FDBCRC_SELFSUM_UB 2
+#endif
+#ifndef FDBCRC_SELFSUM_UW
 #define FDBCRC_SELFSUM_UW 4
 #endif
 struct V7Params {
