@@ -1454,18 +1454,47 @@ __device__ __forceinline__ uint64_t rdlane63(uint64_t v) {
 	return ((uint64_t)hi << 32) | lo;
 }
 
-// One workgroup per tile of 256 buffers: the tile's sums.
+// Planner tiles: 256 buffers (one per thread) for batches of up to
+// 256 x kXFuseTiles buffers, else 256 x kXPerBig (kXPerBig per thread).  A
+// zipf batch (406 k buffers) is then 397 tiles, under kXFuseTiles, so
+// k_xassign reduces the tile sums itself and k_xscan is not launched: planner
+// kernels 7.1 + 6.6 + 7.3 us -> 5.4 + 7.9 us (same box).  Eight per thread
+// (199 tiles) measured 5.5 + 8.7 us: a thread's buffers are a serial chain,
+// and a fused k_xassign of 199 workgroups holds under one wave per SIMD.
+#ifndef FDBXXH_PLAN_PER
+#define FDBXXH_PLAN_PER 4
+#endif
+constexpr uint32_t kXPerBig = FDBXXH_PLAN_PER;
+static_assert(256ull * kXPerBig < 65536, "a tile's class counts are 16-bit fields");
+
+// One workgroup per tile: the tile's sums (thread t takes buffers t + 256u).
+template <uint32_t kXPer>
 __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
+	constexpr uint64_t kXTile = 256ull * kXPer;
 	__shared__ uint64_t part[4][8];
 	if (Q.dcount) Q.count = min(Q.count, (uint64_t)*Q.dcount);
-	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	const uint64_t i0 = (uint64_t)blockIdx.x * kXTile + threadIdx.x;
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
-	const bool lg = i < Q.count && xp_long(len);
-	const uint64_t nb = lg ? xp_blocks(len) : 0;
-	const uint32_t cl = lg ? xp_class(nb) : 0;
-	uint64_t v[8] = {i < Q.count ? xp_cost(len, lg) : 0, i < Q.count ? xp_cost(len, false) : 0, nb, 0, 0, 0, 0, 0};
-	if (lg) v[4 + (cl >> 2)] = 1ull << (16 * (cl & 3));
+	uint64_t len[kXPer];
+#pragma unroll
+	for (uint32_t u = 0; u < kXPer; ++u) {
+		const uint64_t i = i0 + 256u * u;
+		len[u] = i < Q.count ? xp_len(Q, i) : 0;
+	}
+	uint64_t v[8] = {};
+#pragma unroll
+	for (uint32_t u = 0; u < kXPer; ++u) {
+		const bool in = i0 + 256u * u < Q.count;
+		const bool lg = in && xp_long(len[u]);
+		const uint64_t nb = lg ? xp_blocks(len[u]) : 0;
+		const uint32_t cl = lg ? xp_class(nb) : 0;
+		v[0] += in ? xp_cost(len[u], lg) : 0;
+		v[1] += in ? xp_cost(len[u], false) : 0;
+		v[2] += nb;
+		const uint64_t bit = lg ? 1ull << (16 * (cl & 3)) : 0;  // (16-bit fields: at most kXTile per tile)
+#pragma unroll
+		for (uint32_t w = 0; w < 4; ++w) v[4 + w] += (cl >> 2) == w ? bit : 0;
+	}
 #pragma unroll
 	for (int q = 0; q < 8; ++q) v[q] = rdlane63(dpp_incl64(v[q]));
 	if (lane == 0)
@@ -1474,7 +1503,7 @@ __global__ __launch_bounds__(256) void k_xplan(XPlanP Q) {
 	__syncthreads();
 	if (threadIdx.x < 8 && threadIdx.x != 3) {
 		const int q = threadIdx.x;
-		const uint64_t s = part[0][q] + part[1][q] + part[2][q] + part[3][q];  // (16-bit fields: <= 256 each)
+		const uint64_t s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
 		uint64_t* dst = q == 0 ? Q.tiles : q == 1 ? Q.tcns : q == 2 ? Q.tneed : Q.tcls + (uint64_t)(q - 4) * Q.ntile;
 		dst[blockIdx.x] = s;
 	}
@@ -1564,7 +1593,8 @@ __global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
 	}
 }
 
-// One workgroup per tile of 256 buffers: buffer i (cost c_i, start s_i) is
+// One workgroup per tile (thread t: buffers t*kXPer .. t*kXPer + kXPer - 1 of
+// it, contiguous, so their starts follow from one scan): buffer i (cost c_i, start s_i) is
 // the first buffer of every wave w with s_{i-1} < w*Q <= s_i; waves past
 // the last buffer get `count`.  A routed long buffer writes its entry in its
 // size class (any order within the class).
@@ -1574,17 +1604,32 @@ __global__ __launch_bounds__(1024) void k_xscan(XPlanP Q) {
 // route, its tile's start and the quantum, and its classes' bases from the
 // counts of the tiles before it (no cursor atomics); workgroup 0 writes sh[].
 #ifndef FDBXXH_FUSE_TILES
-#define FDBXXH_FUSE_TILES 256
+#define FDBXXH_FUSE_TILES 512
 #endif
 constexpr uint64_t kXFuseTiles = FDBXXH_FUSE_TILES;
-template <bool FUSED>
+template <bool FUSED, uint32_t kXPer>
 __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
+	constexpr uint64_t kXTile = 256ull * kXPer;
 	__shared__ uint64_t wsum[4];
 	if (Q.dcount) Q.count = min(Q.count, (uint64_t)*Q.dcount);
 	__shared__ uint32_t ccount[kXClasses];
 	__shared__ uint64_t cbase[kXClasses];
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-	const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+	// this thread's kXPer consecutive buffers, their metadata loaded before
+	// the tile sums are reduced (no load waits behind the barriers)
+	const uint64_t ib = (uint64_t)blockIdx.x * kXTile + (uint64_t)t * kXPer;
+	uint64_t len[kXPer], off[kXPer], sdv[kXPer];
+#pragma unroll
+	for (uint32_t u = 0; u < kXPer; ++u) len[u] = ib + u < Q.count ? xp_len(Q, ib + u) : 0;
+	// the buffer before this thread's first (its start gives that buffer's wave range)
+	const uint64_t lp = ib != 0 && ib < Q.count ? xp_len(Q, ib - 1) : 0;
+	// a long buffer's entry: its offset and seed (with room for the long route)
+#pragma unroll
+	for (uint32_t u = 0; u < kXPer; ++u) {
+		const bool in = Q.capS && ib + u < Q.count;
+		off[u] = in && Q.offsets ? Q.offsets[ib + u] : 0;
+		sdv[u] = in && Q.seeds ? Q.seeds[ib + u] : Q.seed;
+	}
 	bool routed;
 	uint64_t tile_start;
 	XQuant W;
@@ -1596,7 +1641,9 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 		constexpr int kR = 21;
 		__shared__ uint64_t red[kR][4];
 		uint64_t r[kR] = {};
-		for (uint32_t k = t; k < Q.ntile; k += 256) {  // (thread t takes tiles t, t + 256, ...)
+		// (thread t takes tiles t, t + 256, ...: two at a time, their loads together)
+#pragma unroll 2
+		for (uint32_t k = t; k < Q.ntile; k += 256) {
 			const uint64_t cr = Q.tiles[k], cu = Q.tcns[k], nb = Q.tneed[k];
 			const bool before = k < blockIdx.x;
 			r[18] += cr;
@@ -1661,43 +1708,60 @@ __global__ __launch_bounds__(256) void k_xassign(XPlanP Q) {
 		W = xquant(Q.tiles[Q.ntile], Q.nwave, Q.older);
 		tile_start = Q.tiles[blockIdx.x];
 	}
-	const uint64_t len = i < Q.count ? xp_len(Q, i) : 0;
-	const bool lg = i < Q.count && routed && xp_long(len);
-	if (Q.capS && i < Q.count) Q.flag[i] = lg ? 1 : 0;
-	const uint64_t cost = i < Q.count ? xp_cost(len, lg) : 0;
-	const uint64_t inc = dpp_incl64(cost);
+	uint64_t cost[kXPer];
+	uint32_t cl[kXPer], rank[kXPer];
+	bool lg[kXPer];
+	uint64_t tsum = 0;
+#pragma unroll
+	for (uint32_t u = 0; u < kXPer; ++u) {
+		const bool in = ib + u < Q.count;
+		lg[u] = in && routed && xp_long(len[u]);
+		cost[u] = in ? xp_cost(len[u], lg[u]) : 0;
+		cl[u] = lg[u] ? xp_class(xp_blocks(len[u])) : 0;
+		tsum += cost[u];
+		if (Q.capS && in) Q.flag[ib + u] = lg[u] ? 1 : 0;
+	}
+	const uint64_t inc = dpp_incl64(tsum);
 	if (lane == 63) wsum[wv] = inc;
 	if (t < kXClasses) ccount[t] = 0;
 	__syncthreads();
 	// a long buffer's rank in its class within the tile (LDS), then one global
 	// add per class and tile (the classes' cursors are a handful of words: one
 	// add per buffer measured 16 us of contention on the chunks batch)
-	const uint32_t cl = lg ? xp_class(xp_blocks(len)) : 0;
-	const uint32_t rank = lg ? atomicAdd(&ccount[cl], 1u) : 0;
+#pragma unroll
+	for (uint32_t u = 0; u < kXPer; ++u) rank[u] = lg[u] ? atomicAdd(&ccount[cl[u]], 1u) : 0;
 	__syncthreads();
 	if (!FUSED && t < kXClasses && ccount[t]) cbase[t] = atomicAdd((unsigned long long*)&Q.sh[8 + t], (unsigned long long)ccount[t]);
 	__syncthreads();
-	uint64_t ex = inc - cost;
+	uint64_t ex = inc - tsum;
 	for (uint32_t u = 0; u < wv; ++u) ex += wsum[u];
-	const uint64_t start = tile_start + ex;
-	if (i < Q.count) {
-		// waves w with s_{i-1} < w*q <= s_i, i.e. [floor(s_{i-1}/q) + 1, floor(s_i/q)];
-		// buffer 0 takes w = 0
-		uint64_t prev = 0;
-		if (i != 0) {
-			const uint64_t lp = xp_len(Q, i - 1);
-			prev = start - xp_cost(lp, routed && xp_long(lp));  // (the route is batch-wide)
+	uint64_t start = tile_start + ex;
+	// waves w with s_{i-1} < B(w) <= s_i, i.e. [floor(s_{i-1}/q) + 1, floor(s_i/q)]
+	// for a single quantum; buffer 0 takes w = 0.  One division per thread:
+	// the starts grow along its buffers, so the next wave's boundary B(wn) is
+	// stepped, not divided for (a 64-bit division per buffer, in a chain per
+	// thread, cost the 8-buffer tiles ~0.4 us per buffer).
+	uint64_t wn = ib == 0 ? 0 : xquant_wave(W, start - xp_cost(lp, routed && xp_long(lp))) + 1;
+	const uint64_t ha = W.h * W.qa;
+	auto bound = [&](uint64_t w) { return w < W.h ? w * W.qa : ha + (w - W.h) * W.qb; };
+	uint64_t bn = bound(wn);
+#pragma unroll
+	for (uint32_t u = 0; u < kXPer; ++u) {
+		const uint64_t i = ib + u;
+		if (i < Q.count) {
+			while (wn < Q.nwave && bn <= start) {
+				Q.wave_first[wn] = i;
+				bn = bound(++wn);
+			}
+			if (lg[u]) {
+				const uint64_t pos = cbase[cl[u]] + rank[u];
+				const uint64_t o = Q.offsets ? off[u] : i * Q.stride;
+				Q.ents[pos] = XEnt{reinterpret_cast<uint64_t>(Q.base) + o, len[u], sdv[u], i};
+			}
+			start += cost[u];
+			if (i + 1 == Q.count)  // waves whose first byte lies past the last buffer's start: none
+				for (uint64_t w = wn; w <= Q.nwave; ++w) Q.wave_first[w] = Q.count;
 		}
-		const uint64_t w_lo = i == 0 ? 0 : xquant_wave(W, prev) + 1;
-		const uint64_t w_hi = xquant_wave(W, start);
-		for (uint64_t w = w_lo; w <= w_hi && w < Q.nwave; ++w) Q.wave_first[w] = i;
-		if (i + 1 == Q.count)  // waves whose first byte lies past the last buffer's start: none
-			for (uint64_t w = w_hi + 1; w <= Q.nwave; ++w) Q.wave_first[w] = Q.count;
-	}
-	if (lg) {
-		const uint64_t pos = cbase[cl] + rank;
-		const uint64_t sd = Q.seeds ? Q.seeds[i] : Q.seed;
-		Q.ents[pos] = XEnt{reinterpret_cast<uint64_t>(Q.base) + xp_off(Q, i), len, sd, i};
 	}
 }
 
@@ -1709,7 +1773,7 @@ struct XLayout {
 };
 static uint64_t al64(uint64_t x) { return (x + 63) & ~uint64_t(63); }
 static XLayout xlayout(uint64_t count, uint64_t nwave, uint64_t ws_bytes) {
-	const uint64_t ntile = (count + 255) / 256;
+	const uint64_t ntile = (count + 255) / 256;  // (the largest tile count: tiles of 256)
 	XLayout L{};
 	L.tiles = 0;
 	L.tcns = al64(8 * (ntile + 2));
@@ -1760,7 +1824,12 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 	// the planner: varlen batches, and fixed-length long buffers given room for the long route
 	const bool fixed_split = !P.offsets && ws && P.length > kXSplitMin;
 	if (P.offsets || fixed_split) {
-		const uint64_t ntile = (P.count + 255) / 256;
+		// tiles of 256 buffers for small batches (more workgroups, short
+		// per-thread chains), of 256 x kXPerBig past 256 such tiles (fewer
+		// tiles to reduce: zipf's 1587 become 199, and k_xscan drops out)
+		const bool big = P.count > 256 * kXFuseTiles;
+		const uint64_t tile = big ? 256ull * kXPerBig : 256ull;
+		const uint64_t ntile = (P.count + tile - 1) / tile;
 		const XLayout L = xlayout(P.count, nwave, P.ws_bytes);
 		uint8_t* w8 = static_cast<uint8_t*>(ws);
 		XPlanP Q{};
@@ -1786,12 +1855,17 @@ int launch_xxh3(const XxhParams& P0, int num_cus, void* ws, hipStream_t stream) 
 		Q.capS = L.capS;
 		Q.hneed = P.hneed;
 		Q.dcount = P.d_count;
-		k_xplan<<<(unsigned)ntile, 256, 0, stream>>>(Q);
-		if (ntile <= kXFuseTiles) {
-			k_xassign<true><<<(unsigned)ntile, 256, 0, stream>>>(Q);
+		if (!big) {
+			k_xplan<1><<<(unsigned)ntile, 256, 0, stream>>>(Q);
+			k_xassign<true, 1><<<(unsigned)ntile, 256, 0, stream>>>(Q);
 		} else {
-			k_xscan<<<1, 1024, 0, stream>>>(Q);
-			k_xassign<false><<<(unsigned)ntile, 256, 0, stream>>>(Q);
+			k_xplan<kXPerBig><<<(unsigned)ntile, 256, 0, stream>>>(Q);
+			if (ntile <= kXFuseTiles) {
+				k_xassign<true, kXPerBig><<<(unsigned)ntile, 256, 0, stream>>>(Q);
+			} else {
+				k_xscan<<<1, 1024, 0, stream>>>(Q);
+				k_xassign<false, kXPerBig><<<(unsigned)ntile, 256, 0, stream>>>(Q);
+			}
 		}
 		if (L.capS) {
 			XLong S{};
