@@ -57,15 +57,24 @@ constexpr uint32_t kPageCtrWords = 32;
 #define FDBCRC_XCD_ODD_W 31
 #endif
 constexpr uint64_t kXcdEvenW = FDBCRC_XCD_EVEN_W, kXcdOddW = FDBCRC_XCD_ODD_W;  // (32nds)
+struct XcdRanges {
+	uint64_t n, pe, po;  // items; an even / odd workgroup's range
+	__device__ __forceinline__ XcdRanges(uint64_t n_, uint64_t G) : n(n_) {
+		const uint64_t ne = (G + 1) / 2, no = G / 2;
+		const uint64_t den = ne * kXcdEvenW + no * kXcdOddW;
+		const uint64_t unit = (n * 32 + den - 1) / den;
+		pe = (unit * kXcdEvenW + 31) / 32;
+		po = (unit * kXcdOddW + 31) / 32;
+	}
+	__device__ __forceinline__ void get(uint64_t b, uint64_t& g0, uint64_t& g1) const {
+		const uint64_t s0 = ((b + 1) / 2) * pe + (b / 2) * po;  // the even and odd workgroups before b
+		const uint64_t e0 = s0 + ((b & 1) ? po : pe);
+		g0 = s0 < n ? s0 : n;
+		g1 = e0 < n ? e0 : n;
+	}
+};
 __device__ __forceinline__ void xcd_range(uint64_t n, uint64_t b, uint64_t G, uint64_t& g0, uint64_t& g1) {
-	const uint64_t ne = (G + 1) / 2, no = G / 2;
-	const uint64_t den = ne * kXcdEvenW + no * kXcdOddW;
-	const uint64_t unit = (n * 32 + den - 1) / den;
-	const uint64_t pe = (unit * kXcdEvenW + 31) / 32, po = (unit * kXcdOddW + 31) / 32;
-	const uint64_t s0 = ((b + 1) / 2) * pe + (b / 2) * po;  // the even and odd workgroups before b
-	const uint64_t e0 = s0 + ((b & 1) ? po : pe);
-	g0 = s0 < n ? s0 : n;
-	g1 = e0 < n ? e0 : n;
+	XcdRanges(n, G).get(b, g0, g1);
 }
 int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr);  // crc32c_capi.cpp
 // per-stream counter words (crc32c_capi.cpp: stream_aux), zero between calls

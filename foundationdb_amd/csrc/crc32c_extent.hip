@@ -416,8 +416,10 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 #pragma unroll
 		for (uint32_t j = 0; j < kXU; ++j) load_block(u[j], blk_ptr(k + j), c.ld_off);
 	};
-	uint32_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
-	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
+	// grab A static (g0 + wi), then one request per grab, issued at its start
+	// and read in its first step (k_pages4k: a wave holds at most its grab and
+	// the next when the range runs out)
+	uint32_t gA = clampg(g0 + wi), gB = nd;
 	Block u0[kXU], u1[kXU];
 	// wave 0 of workgroup 0 streams the last grab first (below): its first
 	// dynamic unit is loaded after that
@@ -642,9 +644,10 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		const uint32_t gb0 = gA * gsz, gb1 = gb0 + gsz;
 		const uint32_t k = gb0 + 4 * s;
 		uint32_t qnx = 0;
+		uint32_t req = 0;
 		if (s == 0) {
 			X = 0;
-			wqv = xld32(P.x.wq + (gB < nd ? gB : 0u));  // the next grab's window start, read at this grab's end
+			req = request();
 		}
 		load_step_unit(u1, gA, s, 1);
 		__builtin_amdgcn_sched_barrier(0);
@@ -652,14 +655,17 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			uint32_t H[kXU], Y[kXU][3];
 			unit_h(u0, H, Y);
 			__builtin_amdgcn_sched_barrier(0);
-			const bool last_step = s + 1 == spg;
+			const bool last_step = s + 1 == spg;  // (not step 0: a grab has at least two)
 			qnx = last_step ? rdfirst(wqv) : 0u;
 			// the grab's window (its metadata prefetched a grab ahead; the next
 			// window's loads issued ahead of the next unit's, so that a window
-			// retired in this unit waits only for them)
+			// retired in this unit waits only for them); the next grab and its
+			// window start (read at this grab's end)
 			if (s == 0) {
 				make_window(q);
 				prefetch(q + 64);
+				gB = clampg(g0 + wpb + rdlane(req, 0));
+				wqv = xld32(P.x.wq + (gB < nd ? gB : 0u));
 			}
 			// the next unit's loads go out before this unit's points are captured
 			load_step_unit(u0, last_step ? gB : gA, last_step ? 0u : s + 1, 0);
@@ -683,8 +689,6 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			q = qnx;
 			if (gB < nd) prefetch(q);  // the next grab's window, consumed a step later
 			gA = gB;
-			gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
-			req = request();
 			s = 0;
 		} else {
 			++s;

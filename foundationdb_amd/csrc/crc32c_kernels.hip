@@ -243,9 +243,14 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		const uint32_t sd = seeds ? v : seed;
 		return (PAIR && (c.lane & 1)) ? ~0u : sd;  // second halves carry no seed (~0 -> 0)
 	};
-	uint64_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
-	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
-	uint32_t sdA = seed_of(gA), sdB = seed_of(gB);
+	// Grab A is static (g0 + wi); then one request per grab, issued at the
+	// grab's start and read at its middle, just before the next grab's first
+	// unit is loaded (the atomic returns during the first unit's compute), so
+	// a wave holds at most its grab and the next when the range runs out.
+	// (Requesting a grab further ahead, as before, left the waves ~2 grabs
+	// apart at the end: 1 Mi pages 672 -> 667 us, same box, 6 launches each.)
+	uint64_t gA = clampg(g0 + wi), gB = ngrab;
+	uint32_t sdA = seed_of(gA), sdB = 0;
 	Blk u0[U], u1[U];
 	load_u(u0, gA * C);  // in flight during the LDS fill
 	if constexpr (STRIDED)
@@ -301,6 +306,7 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		const uint64_t first = gA * C;
 		const uint32_t l0 = f * C;
 		uint32_t sd[U], crc[U];
+		const uint32_t req = request();
 		load_u(u1, first + U);
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -309,6 +315,8 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 #pragma unroll
 		for (int j = 0; j < U; ++j) mine = (uint32_t)c.lane == l0 + j ? crc[j] : mine;
 		__builtin_amdgcn_sched_barrier(0);
+		gB = clampg(g0 + wpb + rdlane(req, 0));
+		sdB = seed_of(gB);
 		load_u(u0, gB * C);  // the next grab's first unit
 		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -321,9 +329,6 @@ __global__ __launch_bounds__(1024) void k_pages4k(const uint8_t* __restrict__ ba
 		myi = k < C ? first + k : myi;
 		gA = gB;
 		sdA = sdB;
-		gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
-		req = request();
-		sdB = seed_of(gB);
 		if (++f == F) {
 			store();
 			f = 0;
@@ -490,29 +495,10 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		uint32_t alo, ahi, kt, ek, sd, idx;
 	};
 	auto rd = [](uint32_t v, uint32_t j) { return rdlane(v, (int)j); };
-	auto meta_of = [&](uint32_t g, Meta& M) {
-		const uint64_t bf = (uint64_t)g * C;
-		if (bf >= count) {  // nothing left: duplicates of the window's first entry's last block, discarded
-			const uint64_t a0 = rdlane64(wE, 0) - 4096;
-			// a buffer of one block starts lo bytes into it: its loads clamp there
-			const uint32_t lo16 = rdlane(ws, 1) - rdlane(ws, 0) == 1 ? rdlane(wL, 0) & 0xFFu : 0u;
-			M.alo = (uint32_t)a0;
-			M.ahi = (uint32_t)(a0 >> 32);
-			M.kt = 0;
-			M.ek = lo16;
-			M.sd = 0;
-			M.idx = ~0u;
-			return;
-		}
-		const uint32_t b0 = (uint32_t)bf;
-		const uint32_t bl = bf + C - 1 < count ? b0 + C - 1 : last;
-		while (bl >= wend) {
-			const uint32_t adv = b0 < wend ? (uint32_t)__builtin_popcountll(__ballot(ws <= b0)) - 1u : 64u;
-			load_window(wj + adv);
-		}
-		// lane j (< C): block b0 + j (past the batch's last block: a duplicate
-		// of it, result discarded); its entry e = the last window entry whose
-		// first block is <= b, one ballot per block
+	// lane j (< C): block b0 + j (past the batch's last block: a duplicate
+	// of it, result discarded); its entry e = the last window entry whose
+	// first block is <= b, one ballot per block
+	auto pick = [&](Meta& M, uint32_t b0) {
 		const uint32_t j = lane & (C - 1);
 		int e = 0;
 #pragma unroll
@@ -540,6 +526,36 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		M.ek = m == 0 ? lot & 0xFFFu : 0u;
 		M.sd = m == 0 ? sdv : 0u;
 		M.idx = b0 + j <= last ? ixv : ~0u;
+	};
+	auto meta_of = [&](uint32_t g, Meta& M) {
+		const uint64_t bf = (uint64_t)g * C;
+		if (bf >= count) {  // nothing left: duplicates of the window's first entry's last block, discarded
+			const uint64_t a0 = rdlane64(wE, 0) - 4096;
+			// a buffer of one block starts lo bytes into it: its loads clamp there
+			const uint32_t lo16 = rdlane(ws, 1) - rdlane(ws, 0) == 1 ? rdlane(wL, 0) & 0xFFu : 0u;
+			M.alo = (uint32_t)a0;
+			M.ahi = (uint32_t)(a0 >> 32);
+			M.kt = 0;
+			M.ek = lo16;
+			M.sd = 0;
+			M.idx = ~0u;
+			return;
+		}
+		const uint32_t b0 = (uint32_t)bf;
+		const uint32_t bl = bf + C - 1 < count ? b0 + C - 1 : last;
+		// The window moves (rarely): its loads are waited for on that path
+		// only.  With one path the compiler's wait before the lookups below
+		// assumed the window had just been loaded and drained every block load
+		// in flight, once per grab.
+		if (bl >= wend) {
+			do {
+				const uint32_t adv = b0 < wend ? (uint32_t)__builtin_popcountll(__ballot(ws <= b0)) - 1u : 64u;
+				load_window(wj + adv);
+			} while (bl >= wend);
+			pick(M, b0);
+		} else {
+			pick(M, b0);
+		}
 	};
 	auto load_u = [&](Block (&u)[U], const Meta& M, uint32_t j0) {
 #pragma unroll
@@ -628,21 +644,22 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		if (lane == 0) r = atomicAdd(my_ctr, 1u);
 		return r;
 	};
-	uint32_t gA = clampg(g0 + wi), gB = clampg(g0 + wi + wpb);
-	uint32_t req = request();  // grab g0 + 2*wpb + req: becomes gB after grab A
+	// grab A static (g0 + wi), then one request per grab, issued at its start
+	// and read at its middle (k_pages4k)
+	uint32_t gA = clampg(g0 + wi);
 	load_window(find(g0 * C < count ? (uint32_t)(g0 * C) : last));
 	Meta MA, MB;
 	meta_of(gA, MA);
-	meta_of(gB, MB);
 	Block u0[U], u1[U];
 	load_u(u0, MA, 0);  // in flight while the tables are written
 	fill_commit_1024(fill, lds);
 	uint32_t f = 0;
-	// one grab: X is its metadata, Y the next grab's (its first unit is
-	// loaded here), rebuilt for the grab after it
+	// one grab: X is its metadata; Y becomes the next grab's (its first unit
+	// is loaded here)
 	auto step = [&](Meta& X, Meta& Y) {
 		const uint32_t l0 = f * C;
 		uint32_t crc[U];
+		const uint32_t req = request();
 		load_u(u1, X, U);
 		__builtin_amdgcn_sched_barrier(0);
 		crc_u(u0, X, 0, crc);
@@ -657,6 +674,8 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 			midx = mine_grab ? ix : midx;
 		}
 		__builtin_amdgcn_sched_barrier(0);
+		const uint32_t gB = clampg(g0 + wpb + rdlane(req, 0));
+		meta_of(gB, Y);
 		load_u(u0, Y, 0);  // the next grab's first unit
 		__builtin_amdgcn_sched_barrier(0);
 		crc_u(u1, X, U, crc);
@@ -664,9 +683,6 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		for (uint32_t j = 0; j < U; ++j) mine = lane == l0 + U + j ? crc[j] : mine;
 		__builtin_amdgcn_sched_barrier(0);
 		gA = gB;
-		gB = clampg(g0 + 2 * wpb + rdlane(req, 0));
-		req = request();
-		meta_of(gB, X);
 		if (++f == F) {
 			store();
 			f = 0;

@@ -583,10 +583,21 @@ __global__ __launch_bounds__(256) void k_xcount(V7Params P) {
 	fill_grab_map(P.xwq, glo, ghi, v, act);
 }
 
+#ifdef FDBCRC_PTIMES
+// development: per-tile timestamps of the prep kernels (s_memrealtime, 100 MHz):
+// start, tables and chunks in, prefixes known, entries out
+__device__ uint64_t g_pt[4096][4];
+#define FDBCRC_PT(k) \
+	if (threadIdx.x == 0 && blockIdx.x < 4096) g_pt[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define FDBCRC_PT(k)
+#endif
+
 // BIG: the block route is on (bigmin != 0); without it the route's sums
 // and entries are compiled out (fewer registers: 8 blocks per CU).
 template <bool BIG>
 __device__ __forceinline__ void v7prep(const V7Params& P) {
+	FDBCRC_PT(0)
 	const uint64_t bigmin = BIG ? P.bigmin : 0;
 	__shared__ uint32_t s4[4][256];    // slice4 tables (no bank replication: this kernel is not LDS-bound)
 	__shared__ uint32_t iz[16 * 128];  // inv_z nibble tables: x^(-8z), z < 16 (small buffers' trailing zeros)
@@ -656,6 +667,7 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 	// fence waits for every load in flight) also collects the chunks and the
 	// first round of tile sums, which were all in flight together.
 	__syncthreads();
+	FDBCRC_PT(1)
 	// small buffer: its chunks [A, E) as 4-byte words from a zero register,
 	// the bytes before P0 zeroed and ~seed injected at P0 (crc32c.cpp:197),
 	// the zt bytes after P1 zeroed and then divided out (x^(-8 zt), LDS
@@ -717,16 +729,25 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		// (SU buffers in flight per thread: 8 spilled 36 SGPRs with the block
 		// route's geometry, 2 spill none there; the windows-only form takes 4)
 		constexpr uint32_t SU = BIG ? FDBCRC_SELFSUM_UB : FDBCRC_SELFSUM_UW;
+		// (unconditional loads -- a fixed stride or length reads word 0 of its
+		// array's stand-in and replaces it: a load behind a branch is waited
+		// for where the paths join, which made the loads one round trip each)
+		const uint64_t* const po = P.offsets ? P.offsets : P.tsum;
+		const uint64_t* const pl = P.lengths ? P.lengths : P.tsum;
+		const uint64_t mo = P.offsets ? ~0ull : 0ull, ml = P.lengths ? ~0ull : 0ull;
 		for (uint64_t j0 = threadIdx.x; j0 < n; j0 += SU * blockDim.x) {
 			uint64_t o[SU], l[SU];
 #pragma unroll
 			for (uint32_t u = 0; u < SU; ++u) {
-				const uint64_t j = j0 + u * blockDim.x;
-				v7_buffer(P, j < n ? j : 0, o[u], l[u]);
+				const uint64_t j = j0 + u * blockDim.x < n ? j0 + u * blockDim.x : 0;
+				o[u] = gld64(po + (j & mo));
+				l[u] = gld64(pl + (j & ml));
 			}
 #pragma unroll
 			for (uint32_t u = 0; u < SU; ++u) {
-				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o[u], l[u], bigmin);
+				const uint64_t j = j0 + u * blockDim.x;
+				const uint64_t ou = P.offsets ? o[u] : j * P.stride, lu = P.lengths ? l[u] : P.length;
+				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + ou, lu, bigmin);
 				const bool in = j0 + u * blockDim.x < n;
 				pre = sadd(pre, in ? gj.W : 0u);
 				preB = sadd(preB, in ? gj.nb : 0u);
@@ -771,6 +792,7 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		inN += k < wv ? wsum[2][k] : 0u;
 		aggN += wsum[2][k];
 	}
+	FDBCRC_PT(2)
 	const uint32_t excl = sadd(sadd(s_pre[0][0], s_pre[0][1]), sadd(s_pre[0][2], s_pre[0][3]));
 	const uint32_t exclB = sadd(sadd(s_pre[1][0], s_pre[1][1]), sadd(s_pre[1][2], s_pre[1][3]));
 	const uint32_t exclN = s_pre[2][0] + s_pre[2][1] + s_pre[2][2] + s_pre[2][3];
@@ -791,6 +813,7 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 			if (refused && P.err) *P.err = 1u;
 		}
 	}
+	FDBCRC_PT(3)
 	if (!ok) return;
 	const uint32_t gi = excl + inwave + incl - W;
 	P.gs[i] = gi;
@@ -1383,5 +1406,11 @@ extern "C" int crc32c_debug_read(uint64_t* d_out8) {
 	}
 	a[2] += b[2];
 	return hipMemcpy(d_out8, a, 64, hipMemcpyHostToDevice) == hipSuccess ? 0 : -3;
+}
+#endif
+
+#ifdef FDBCRC_PTIMES
+extern "C" int fdbcrc_debug_ptimes(void* host, uint64_t ntile) {
+	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbcrc::g_pt), ntile * 32, 0, hipMemcpyDeviceToHost);
 }
 #endif
