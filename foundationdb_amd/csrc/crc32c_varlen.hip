@@ -729,25 +729,20 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		// (SU buffers in flight per thread: 8 spilled 36 SGPRs with the block
 		// route's geometry, 2 spill none there; the windows-only form takes 4)
 		constexpr uint32_t SU = BIG ? FDBCRC_SELFSUM_UB : FDBCRC_SELFSUM_UW;
-		// (unconditional loads -- a fixed stride or length reads word 0 of its
-		// array's stand-in and replaces it: a load behind a branch is waited
-		// for where the paths join, which made the loads one round trip each)
-		const uint64_t* const po = P.offsets ? P.offsets : P.tsum;
-		const uint64_t* const pl = P.lengths ? P.lengths : P.tsum;
-		const uint64_t mo = P.offsets ? ~0ull : 0ull, ml = P.lengths ? ~0ull : 0ull;
+		// (The loads sit behind v7_buffer's stride/list branch, so each pair is
+		// waited for where the paths join; unconditional loads, 3-8 in flight,
+		// measured the same on the chunks batch -- its prep is ~7 us of
+		// dispatch and barriers, `tools/probe_ptimes.py` -- and spilled SGPRs.)
 		for (uint64_t j0 = threadIdx.x; j0 < n; j0 += SU * blockDim.x) {
 			uint64_t o[SU], l[SU];
 #pragma unroll
 			for (uint32_t u = 0; u < SU; ++u) {
-				const uint64_t j = j0 + u * blockDim.x < n ? j0 + u * blockDim.x : 0;
-				o[u] = gld64(po + (j & mo));
-				l[u] = gld64(pl + (j & ml));
+				const uint64_t j = j0 + u * blockDim.x;
+				v7_buffer(P, j < n ? j : 0, o[u], l[u]);
 			}
 #pragma unroll
 			for (uint32_t u = 0; u < SU; ++u) {
-				const uint64_t j = j0 + u * blockDim.x;
-				const uint64_t ou = P.offsets ? o[u] : j * P.stride, lu = P.lengths ? l[u] : P.length;
-				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + ou, lu, bigmin);
+				const Geo7 gj = geo7(reinterpret_cast<uint64_t>(P.base) + o[u], l[u], bigmin);
 				const bool in = j0 + u * blockDim.x < n;
 				pre = sadd(pre, in ? gj.W : 0u);
 				preB = sadd(preB, in ? gj.nb : 0u);
