@@ -112,6 +112,12 @@ __global__ __launch_bounds__(kScanT) void k_seg_scan(const uint64_t* __restrict_
 // whatever alignment it has, four pieces per lane in flight -- and the < 16
 // bytes before and after it byte by byte.  (One workgroup per segment spent
 // its time on the metadata round trip: 509 us for the bench's 900 MiB.)
+// A wave takes 64 segments (their metadata in its lanes) and copies them four
+// at a time, one per 16-lane quarter: a 4 KiB segment is sixteen 16-byte
+// loads per lane, all in flight before the stores, and the head and tail
+// bytes (the staging offset's misalignment) load with them.  One segment per
+// wave at a time -- a load round trip and a store round trip per segment --
+// took 422 us on the bench's 668 k segments.
 __global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                     const uint64_t* __restrict__ len, const uint64_t* __restrict__ pre,
                                                     const uint8_t* __restrict__ segflag, uint64_t nsegs,
@@ -119,7 +125,8 @@ __global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ 
 	typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 	typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 	typedef __attribute__((address_space(1))) const u32x4u g_u32x4u;
-	const uint32_t lane = threadIdx.x & 63;
+	constexpr int kR = 16;  // 16-byte chunks per lane per round: 4 KiB per quarter
+	const uint32_t lane = threadIdx.x & 63, sub = lane >> 4, sl = lane & 15;
 	const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
 	for (uint64_t j0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; j0 < nsegs; j0 += 64 * nw) {
 		const uint64_t jl = j0 + lane < nsegs ? j0 + lane : nsegs - 1;
@@ -127,31 +134,41 @@ __global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ 
 		const bool m_on = j0 + lane < nsegs && segflag[jl] == 0;
 		uint64_t todo = __ballot(m_on);
 		while (todo) {
-			const int k = __builtin_ctzll(todo);
-			todo &= todo - 1;
-			const uint64_t so = __shfl(m_off, k), n = __shfl(m_len, k), d = __shfl(m_pre, k);
+			// up to four segments: quarter q takes the q-th lowest left
+			int kq = -1;
+#pragma unroll
+			for (uint32_t q = 0; q < 4; ++q) {
+				const int k = todo ? __builtin_ctzll(todo) : -1;
+				todo &= todo ? todo - 1 : 0;
+				kq = sub == q ? k : kq;
+			}
+			const bool act = kq >= 0;
+			const int ks = act ? kq : 0;
+			const uint64_t so = __shfl(m_off, ks), n = __shfl(m_len, ks), d = __shfl(m_pre, ks);
 			const uint8_t* src = base + so;
 			uint8_t* dst = staging + d;
-			const uint64_t lim = d >= cap ? 0 : (cap - d < n ? cap - d : n);
+			const uint64_t lim = !act || d >= cap ? 0 : (cap - d < n ? cap - d : n);
 			uint64_t head = (16 - (d & 15)) & 15;
 			head = head < lim ? head : lim;
 			const uint64_t body = (lim - head) & ~uint64_t(15);
-			if (lane < head) dst[lane] = src[lane];
-			for (uint64_t q = head; q < head + body; q += 4 * 1024) {
-				u32x4u v[4];
+			const uint64_t t0 = head + body, ntail = lim - t0;
+			const uint8_t hb = sl < head ? src[sl] : 0;
+			const uint8_t tb = sl < ntail ? src[t0 + sl] : 0;
+			for (uint64_t q = 0; q < body; q += 256ull * kR) {
+				u32x4u v[kR];
 #pragma unroll
-				for (int u = 0; u < 4; ++u) {
-					const uint64_t o = q + 1024ull * u + 16ull * lane;
-					v[u] = __builtin_nontemporal_load((g_u32x4u*)reinterpret_cast<uintptr_t>(src + (o < head + body ? o : head)));
+				for (int r = 0; r < kR; ++r) {
+					const uint64_t o = head + q + 256ull * r + 16ull * sl;
+					v[r] = __builtin_nontemporal_load((g_u32x4u*)reinterpret_cast<uintptr_t>(src + (o < t0 ? o : head)));
 				}
 #pragma unroll
-				for (int u = 0; u < 4; ++u) {
-					const uint64_t o = q + 1024ull * u + 16ull * lane;
-					if (o < head + body) *reinterpret_cast<u32x4*>(dst + o) = u32x4{v[u][0], v[u][1], v[u][2], v[u][3]};
+				for (int r = 0; r < kR; ++r) {
+					const uint64_t o = head + q + 256ull * r + 16ull * sl;
+					if (o < t0) *reinterpret_cast<u32x4*>(dst + o) = u32x4{v[r][0], v[r][1], v[r][2], v[r][3]};
 				}
 			}
-			const uint64_t t0 = head + body;
-			if (t0 + lane < lim) dst[t0 + lane] = src[t0 + lane];
+			if (sl < head) dst[sl] = hb;
+			if (sl < ntail) dst[t0 + sl] = tb;
 		}
 	}
 }
