@@ -647,7 +647,18 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	// grab A static (g0 + wi), then one request per grab, issued at its start
 	// and read at its middle (k_pages4k)
 	uint32_t gA = clampg(g0 + wi);
-	load_window(find(g0 * C < count ? (uint32_t)(g0 * C) : last));
+	// One entry search per workgroup (wave 0; every wave searching put 16x the
+	// scattered entry loads at the kernel's start), handed to each wave in an
+	// LDS word of its OWN table-fill share: wave w reads it before its
+	// fill_commit overwrites it, so no wave's fill races another's read.  (The
+	// barrier's fence waits for the table loads in flight: they return during
+	// the search anyway.)
+	if (wi == 0) {
+		const uint32_t q = find(g0 * C < count ? (uint32_t)(g0 * C) : last);
+		if (lane < wpb) lds[kS4Off / 4 + 256 * lane] = q;  // (thread 64w's first fill word)
+	}
+	__syncthreads();
+	load_window(rdfirst(lds[kS4Off / 4 + 256 * wi]));
 	Meta MA, MB;
 	meta_of(gA, MA);
 	Block u0[U], u1[U];
