@@ -155,6 +155,12 @@ __host__ __device__ inline uint32_t x_log2(uint64_t v) {  // v a power of two
 	return l;
 }
 constexpr uint64_t kXGrabCap = 1ull << 18;  // grabs the per-stream state holds (2 MiB)
+// u64 word of xhdr (256 bytes) from which the extent route's count kernel
+// stages the route statistics (hstat's layout, words 0..kHstatPacked): k_xfin
+// copies them to the stream's host-mapped words beside its back-off word, so
+// the count kernel touches no host memory (its PCIe read-modify-write of the
+// back-off word and the system-scope release cost ~2 us of a ~6 us kernel)
+constexpr int kXStage = 8;
 struct XState {
 	uint32_t* xhdr;
 	uint32_t* ps;         // per buffer, 2 words: its start point's G and Y (k_xstream)

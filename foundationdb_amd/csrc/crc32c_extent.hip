@@ -896,8 +896,17 @@ __device__ __forceinline__ uint32_t wave_chain(const uint32_t* agg, const uint32
 __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	__shared__ uint32_t lds[kFinWords];
 	const bool packed = x_packed(P);
-	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat)  // for the stream's next route choice
+	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat) {  // for the stream's next route choice
+		// the count kernel's statistics (staged in xhdr, kXStage) and this
+		// batch's back-off word (one round trip: issued with x_packed's loads)
+		const uint64_t* st = reinterpret_cast<const uint64_t*>(P.x.xhdr) + kXStage;
+		uint64_t v[kHstatPacked + 1];
+#pragma unroll
+		for (int k = 0; k <= kHstatPacked; ++k) v[k] = st[k];
+#pragma unroll
+		for (int k = 0; k <= kHstatPacked; ++k) P.hstat[k] = v[k];
 		P.hstat[kHstatXfail] = x_unordered(P) ? kXfailBackoff : 0;
+	}
 	const DevTables* T = P.tabs;
 	if (!packed) {
 		for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) lds[kFinS4 + k] = xld32(&T->slice4[0][0] + k);

@@ -413,7 +413,12 @@ __device__ __forceinline__ bool v7_packed_pair(const V7Params& P, uint64_t i, ui
 // The first 256 buffers' bytes by span class and whether they are packed,
 // for the stream's next route choice (tile 0 of prep, or of the count kernel
 // on the extent route).  All threads of the block call it.
-__device__ void v7_route_stats(const V7Params& P, uint64_t i, uint64_t off, uint64_t len, uint64_t (*s_stat)[4]) {
+// st: where the statistics go (hstat's layout: the stream's host-mapped words,
+// or the extent route's device staging, kXStage); backoff: count the extent
+// route's back-off down (host-mapped words only: on the extent route k_xfin
+// sets that word from the batch's own check).
+__device__ void v7_route_stats(const V7Params& P, uint64_t i, uint64_t off, uint64_t len, uint64_t (*s_stat)[4],
+                               uint64_t* st, bool backoff) {
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const bool ok = i < P.count;
 	const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
@@ -428,12 +433,10 @@ __device__ void v7_route_stats(const V7Params& P, uint64_t i, uint64_t off, uint
 		for (int k = 0; k < 4; ++k) s_stat[wv][k] = c[k];
 	__syncthreads();
 	if (threadIdx.x == 0) {
-		for (int k = 0; k < 3; ++k) P.hstat[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
-		P.hstat[kHstatPacked] = (s_stat[0][3] | s_stat[1][3] | s_stat[2][3] | s_stat[3][3]) ? 0 : 1;
+		for (int k = 0; k < 3; ++k) st[k] = s_stat[0][k] + s_stat[1][k] + s_stat[2][k] + s_stat[3][k];
+		st[kHstatPacked] = (s_stat[0][3] | s_stat[1][3] | s_stat[2][3] | s_stat[3][3]) ? 0 : 1;
 		// a window/block-route batch counts the extent route's back-off down
-		// (the count kernel of an extent-route batch calls this too: k_xfin then
-		// sets the word again from that batch's check)
-		if (P.hstat[kHstatXfail] > 0 && P.hstat[kHstatXfail] <= kXfailBackoff) --P.hstat[kHstatXfail];
+		if (backoff && P.hstat[kHstatXfail] > 0 && P.hstat[kHstatXfail] <= kXfailBackoff) --P.hstat[kHstatXfail];
 	}
 }
 __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
@@ -461,9 +464,10 @@ __global__ __launch_bounds__(256) void k_v7count(V7Params P) {
 			// (an unordered batch may give E < S: the packing check refuses it anyway)
 			const uint64_t nblk = E > S ? (E - S + 4095) >> 12 : 0;
 			if (E - S >= kXMaxExtent) P.xhdr[1] = P.epoch;
-			if (P.hstat) P.hstat[kHstatNblk] = nblk;
+			if (P.hstat) reinterpret_cast<uint64_t*>(P.xhdr)[kXStage + kHstatNblk] = nblk;
 		}
-		if (blockIdx.x == 0 && P.hstat) v7_route_stats(P, i, off, len, s_stat);
+		if (blockIdx.x == 0 && P.hstat)
+			v7_route_stats(P, i, off, len, s_stat, reinterpret_cast<uint64_t*>(P.xhdr) + kXStage, false);
 		// k_xgrab's grab map: buffer i is the first to end past the start T(g)
 		// of grabs g with end(i-1) <= T(g) < end(i); the last buffer also
 		// covers the grabs after its end.  Only ordered pairs write (a batch
@@ -561,9 +565,10 @@ __global__ __launch_bounds__(256) void k_xcount(V7Params P) {
 	const uint64_t nblk = E > S ? (E - S + 4095) >> 12 : 0;
 	if (blockIdx.x == 0 && threadIdx.x == 0) {
 		if (E - S >= kXMaxExtent) P.xhdr[1] = P.epoch;
-		if (P.hstat) P.hstat[kHstatNblk] = nblk;
+		if (P.hstat) reinterpret_cast<uint64_t*>(P.xhdr)[kXStage + kHstatNblk] = nblk;
 	}
-	if (blockIdx.x == 0 && P.hstat) v7_route_stats(P, i, off, len, s_stat);
+	if (blockIdx.x == 0 && P.hstat)
+		v7_route_stats(P, i, off, len, s_stat, reinterpret_cast<uint64_t*>(P.xhdr) + kXStage, false);
 	// (every lane reaches both calls: a wave fills long ranges together)
 	const bool act = P.xwq && in && nblk && E - S < kXMaxExtent && !bad;
 	uint64_t lo0 = 0, hi0 = 0, glo = 0, ghi = 0;
@@ -770,7 +775,7 @@ __device__ __forceinline__ void v7prep(const V7Params& P) {
 		s_pre[2][wv] = preN;
 	}
 	const uint32_t W = ok ? g.W : 0u, B = ok ? g.nb : 0u, N = (ok && g.nb) ? 1u : 0u;
-	if (tile == 0 && P.hstat && !P.xhdr) v7_route_stats(P, i, off, len, s_stat);
+	if (tile == 0 && P.hstat && !P.xhdr) v7_route_stats(P, i, off, len, s_stat, P.hstat, true);
 	const uint32_t incl = scan_sadd(W), inclB = scan_sadd(B), inclN = scan_add(N);
 	if (lane == 63) {
 		wsum[0][wv] = incl;
