@@ -110,6 +110,35 @@ __device__ __forceinline__ XGeo x_geo(const XParams& P) {
 	return g;
 }
 
+// The launch's checks and the extent with every load issued at once (at the
+// start of k_xgrab): x_packed, then x_geo behind x_buffer's
+// stride / list branches, were four dependent scalar round trips before any
+// wave could load a block.  Unconditional: a fixed-stride or fixed-length
+// batch reads xhdr instead and discards it.
+struct XStart {
+	bool packed, unordered;
+	XGeo G;
+};
+__device__ __forceinline__ XStart x_start(const XParams& P) {
+	const uint64_t* const dflt = reinterpret_cast<const uint64_t*>(P.x.xhdr);
+	const uint64_t* const po = P.offsets ? P.offsets : dflt;
+	const uint64_t* const pl = P.lengths ? P.lengths : dflt;
+	const uint64_t il = P.count - 1;
+	const uint64_t o0 = xld64(po), o1 = xld64(po + (P.offsets ? il : 0)), l1 = xld64(pl + (P.lengths ? il : 0));
+	const uint32_t a = rdfirst(xld32(P.x.xhdr)), b = rdfirst(xld32(P.x.xhdr + 1));
+	XStart x;
+	x.packed = a != P.x.epoch && b != P.x.epoch;
+	x.unordered = a == P.x.epoch;
+	const uint64_t base = reinterpret_cast<uint64_t>(P.base);
+	const uint64_t a0 = base + (P.offsets ? o0 : 0);
+	const uint64_t b0 = base + (P.offsets ? o1 : il * P.stride);
+	const uint64_t b1 = b0 + (P.lengths ? l1 : P.length);
+	x.G.S = rdfirst64(a0 & ~uint64_t(15));
+	x.G.Eend = rdfirst64((b1 + 15) & ~uint64_t(15));
+	x.G.nblk = (x.G.Eend - x.G.S + 4095) >> 12;
+	return x;
+}
+
 // Blocks per wave of k_xstream's static ranges: whole units of 2U blocks.
 __device__ __forceinline__ uint64_t x_per(uint64_t nblk, uint64_t nwave) {
 	return (((nblk + nwave - 1) / nwave) + 3) / 4 * 4;
@@ -374,16 +403,19 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 __device__ uint64_t g_xt[16384][4];
 #endif
 __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
-	if (!x_packed(P)) return;  // k_xfin checksums this batch buffer by buffer
-	if (x_geo(P).nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
 #ifdef FDBX_TIMES
 	const uint64_t xt0 = __builtin_amdgcn_s_memrealtime();
 	uint32_t xt_grabs = 0;
 #endif
+	// (the table loads first: vector loads, in flight while the checks' scalar
+	// loads return)
 	FillRegs fill;
 	fill_issue_1024(fill, P.tabs);
+	const XStart X0 = x_start(P);
+	if (!X0.packed) return;  // k_xfin checksums this batch buffer by buffer
+	if (X0.G.nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
 	__shared__ uint32_t lds[kLdsBytesB / 4];
-	const XGeo G = x_geo(P);
+	const XGeo G = X0.G;
 	const LaneCtx c = make_ctx();
 	const uint32_t lane = (uint32_t)c.lane;
 	const uint32_t col4 = (lane & 31) * 4;
@@ -914,6 +946,8 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		x_fallback(P, lds + kFinS4);
 		return;
 	}
+	// (x_start's one-round-trip form here holds the kernel's arguments in
+	// SGPRs across the pass: 5 SGPR spills)
 	const XGeo G = x_geo(P);
 	if (G.nblk == 0) {  // every buffer empty at one 16-byte-aligned address: crc32c_append(seed, p, 0) == seed
 		for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.count;
