@@ -37,6 +37,10 @@ struct StreamState {
 	uint32_t* ctr = nullptr;  // page-kernel grab counters
 	uint64_t ctr_bytes = 0;
 	uint64_t* aux = nullptr;  // the verifiers' counters (stream_aux)
+	// held from a call's stream_aux lookup through its last launch: the counters
+	// are shared by every call on the stream, so two host threads' calls must
+	// not interleave their kernels on it (taken after `mu`, never before it)
+	std::mutex aux_mu;
 	uint64_t* hst_h = nullptr;  // varlen route statistics of the stream's last batch (host-mapped)
 	uint64_t* hst_d = nullptr;  // ... its device address
 	// extent route state (crc32c_extent.hip): grown to the batches seen
@@ -234,12 +238,23 @@ int check_launch(const char* what) {
 // The zeroing is enqueued on `stream` itself, ahead of the first page launch.
 // (Allocation happens under g_mu, not the stream lock: the verifiers launch
 // page kernels while holding their stream's workspace lock.)
+// The first use of a stream allocates and zeroes its counters: that cannot be
+// recorded into a graph (hipMalloc invalidates a capture, and the zeroing
+// would only run at replay), so it is refused while the stream captures.
+static bool capturing(hipStream_t s) {
+	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+	return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
 int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr) {
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	StreamState* ss = stream_state(st, stream);
 	std::lock_guard<std::mutex> lock(g_mu);
 	if (!ss->ctr) {
+		if (capturing(stream))
+			return fail(FDB_CRC32C_EINVAL, "first use of a stream inside a stream capture: run one call on it "
+			                               "outside the capture first (its counters are allocated then)");
 		const size_t bytes = (size_t)(num_cus > st->num_cus ? num_cus : st->num_cus) * kPageCtrWords * 4;
 		uint32_t* q = nullptr;
 		hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), bytes);
@@ -263,12 +278,16 @@ int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr) {
 // of a call replays correctly: it ends with them at zero too).  Per stream,
 // not in the workspace: the convenience entry points share one workspace per
 // stream between every API, and a caller's workspace is not ours to keep.
-int stream_aux(hipStream_t stream, uint64_t** aux) {
+int stream_aux(hipStream_t stream, uint64_t** aux, std::unique_lock<std::mutex>* hold) {
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	StreamState* ss = stream_state(st, stream);
+	std::unique_lock<std::mutex> alock(ss->aux_mu);
 	std::lock_guard<std::mutex> lock(g_mu);
 	if (!ss->aux) {
+		if (capturing(stream))
+			return fail(FDB_CRC32C_EINVAL, "first use of a stream inside a stream capture: run one call on it "
+			                               "outside the capture first (its counters are allocated then)");
 		uint64_t* q = nullptr;
 		hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), kAuxBytes);
 		if (e != hipSuccess) return fail(FDB_CRC32C_ENOMEM, "hipMalloc(stream counters)", e);
@@ -280,6 +299,7 @@ int stream_aux(hipStream_t stream, uint64_t** aux) {
 		ss->aux = q;
 	}
 	*aux = ss->aux;
+	if (hold) *hold = std::move(alock);
 	return 0;
 }
 
@@ -733,7 +753,8 @@ int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	uint64_t* aux = nullptr;
-	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux)) return rc;
+	std::unique_lock<std::mutex> aux_hold;  // until the call's last launch
+	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux, &aux_hold)) return rc;
 	if (fdbpc::sqlite_verify(static_cast<const uint8_t*>(d_pages), page_size, count, first_pgno, d_status, d_bad,
 	                         st->tables, st->num_cus, d_workspace,
 	                         reinterpret_cast<unsigned long long*>(aux + kAuxPageCtr),
@@ -770,7 +791,8 @@ int fdb_diskqueue_check_pages_ws(const void* d_pages, uint64_t count, uint8_t* d
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	uint64_t* aux = nullptr;
-	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux)) return rc;
+	std::unique_lock<std::mutex> aux_hold;  // until the call's last launch
+	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux, &aux_hold)) return rc;
 	if (fdbpc::diskqueue_check(static_cast<const uint8_t*>(d_pages), count, d_ok, d_bad, st->tables, st->num_cus,
 	                           d_workspace, reinterpret_cast<unsigned long long*>(aux + kAuxPageCtr),
 	                           reinterpret_cast<hipStream_t>(stream)))
@@ -888,7 +910,8 @@ int fdb_diskqueue_seal_pages_ws(void* d_pages, uint64_t count, void* d_workspace
 	DeviceState* st = nullptr;
 	if (int rc = device_state(&st)) return rc;
 	uint64_t* aux = nullptr;
-	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux)) return rc;
+	std::unique_lock<std::mutex> aux_hold;  // until the call's last launch
+	if (int rc = stream_aux(reinterpret_cast<hipStream_t>(stream), &aux, &aux_hold)) return rc;
 	if (fdbpc::diskqueue_seal(static_cast<uint8_t*>(d_pages), count, st->tables, st->num_cus, d_workspace,
 	                          reinterpret_cast<unsigned long long*>(aux + kAuxPageCtr),
 	                          reinterpret_cast<hipStream_t>(stream)))
@@ -934,7 +957,8 @@ int fdb_packets_verify_ws(const void* d_base, const uint64_t* d_buf_offsets, con
 		return fail(FDB_CRC32C_EINVAL, "fdb_packets_verify: workspace too small or misaligned");
 	const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 	uint64_t* aux = nullptr;
-	if (int rc = stream_aux(s, &aux)) return rc;
+	std::unique_lock<std::mutex> aux_hold;  // until the call's last launch
+	if (int rc = stream_aux(s, &aux, &aux_hold)) return rc;
 	// the split route's room from the long frames the stream's last batch
 	// needed (host-mapped, no synchronisation; a stale hint costs speed only:
 	// long frames past the room are hashed by the row kernel, and the next call

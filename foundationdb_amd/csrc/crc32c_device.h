@@ -4,6 +4,8 @@
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 namespace fdbcrc {
 
 // Window engine (crc32c_varlen.hip): slots per table (4 slots per pass, 16
@@ -81,7 +83,9 @@ int page_counters(hipStream_t stream, int num_cus, uint32_t** ctr);  // crc32c_c
 constexpr uint64_t kAuxBytes = 256;
 constexpr int kAuxPktFrames = 0;  // u64: the packet verifier's frame counter
 constexpr int kAuxPageCtr = 8;    // u64[8]: the page verifiers' list counters and failures
-int stream_aux(hipStream_t stream, uint64_t** aux);
+// hold (may be null): receives the stream's counter lock, to be kept until the
+// call's last kernel using the counters is enqueued
+int stream_aux(hipStream_t stream, uint64_t** aux, std::unique_lock<std::mutex>* hold = nullptr);
 
 int launch_pages(int blocks_per_page, const uint8_t* base, uint64_t stride, uint64_t count, uint32_t seed,
                  const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, hipStream_t stream);
@@ -143,6 +147,9 @@ constexpr uint64_t kXMaxExtent = 1ull << 40;  // 32-bit block numbers with room
 #define FDBX_GRAB_MIN 8
 #endif
 constexpr uint64_t kXGrabMin = FDBX_GRAB_MIN;
+// k_xgrab reads the next grab's window start on a grab's last step and sets it
+// up on its first step: a grab needs at least two steps of 4 blocks
+static_assert(kXGrabMin >= 8 && (kXGrabMin & (kXGrabMin - 1)) == 0, "grabs: a power of two of at least 8 blocks");
 // (a power of two: grab numbers are shifts, not 64-bit divisions)
 __host__ __device__ inline uint64_t x_gsz(uint64_t nblk, uint64_t capg) {
 	uint64_t gsz = kXGrabMin;

@@ -643,10 +643,30 @@ static Ws carve(void* ws, uint64_t count) {
 
 static unsigned blocks(uint64_t n, uint64_t per = 256) { return (unsigned)((n + per - 1) / per); }
 
+// The setup a verify / seal call can fail in, done before its classify pass
+// counts into the stream's counters: the page kernels' grab counters (first
+// use of the stream allocates them) and the XXH3 list kernel's shape rule.
+static int setup_lists(const uint8_t* xxh_base, uint64_t ps, bool crc_pages, int num_cus, hipStream_t s) {
+	uint32_t* pctr = nullptr;
+	if (crc_pages && fdbcrc::page_counters(s, num_cus, &pctr)) return -1;
+	if (((reinterpret_cast<uint64_t>(xxh_base) | ps) & 7) != 0 || ps - 8 <= 240) return -1;
+	return 0;
+}
+// An error after the classify pass: the counters still go back to zero (in
+// stream order, behind what was enqueued), so the stream's next call starts
+// clean.
+static int bail(unsigned long long* ctr, hipStream_t s) {
+	k_pc_done<<<1, 64, 0, s>>>(ctr, nullptr);
+	return -1;
+}
+
 int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t first_pgno, uint8_t* status,
                   uint64_t* d_bad, const fdbcrc::DevTables* tabs, int num_cus, void* ws, unsigned long long* ctr,
                   hipStream_t s) {
 	const Ws w = carve(ws, count);
+	// every fallible setup step before the classify pass, which starts counting
+	// into the stream's counters (only k_pc_done puts them back to zero)
+	if (setup_lists(pages, ps, ps == 4096, num_cus, s)) return -1;
 	k_sq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, count, status, w.list_a, w.list_b, w.list_c, ctr,
 	                                                  w.trl);
 	const uint64_t* n_crc = reinterpret_cast<const uint64_t*>(&ctr[L_CRC]);
@@ -654,7 +674,7 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 	if (ps == 4096) {
 		if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n_crc, count, 0, 8, 0xFDBEEFDBu, w.crc_out, tabs,
 		                                     num_cus, s))
-			return -1;
+			return bail(ctr, s);
 		k_sq_after_crc<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_a, w.crc_out, false, status, w.list_b, ctr,
 		                                                   w.trl);
 	} else {
@@ -671,7 +691,7 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 	P.out = w.xxh_out;
 	P.idx = w.list_b;
 	P.d_count = n_xxh;
-	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
+	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return bail(ctr, s);
 	k_sq_after_xxh<<<blocks(count, kSpan), kCB, 0, s>>>(pages, ps, w.list_b, w.xxh_out, status, w.list_c, ctr, w.trl);
 	k_sq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, ps, first_pgno, w.list_c, status, ctr, w.trl);
 	k_pc_done<<<1, 64, 0, s>>>(ctr, d_bad);
@@ -681,12 +701,13 @@ int sqlite_verify(const uint8_t* pages, uint64_t ps, uint64_t count, uint32_t fi
 int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t* d_bad,
                     const fdbcrc::DevTables* tabs, int num_cus, void* ws, unsigned long long* ctr, hipStream_t s) {
 	const Ws w = carve(ws, count);
+	if (setup_lists(pages + 8, 4096, true, num_cus, s)) return -1;
 	k_dq_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, ok, w.list_a, w.list_b, w.list_c, ctr, w.trl);
 	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&ctr[0]);
 	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&ctr[1]);
 	// V1: crc32c(0xfdbeefdb, bytes [4, 4096))
 	if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n1, count, 4, 0, 0xFDBEEFDBu, w.crc_out, tabs, num_cus, s))
-		return -1;
+		return bail(ctr, s);
 	// V2: XXH3_64bits(bytes [8, 4096))
 	fdbxxh::XxhParams P{};
 	P.base = pages + 8;
@@ -696,7 +717,7 @@ int diskqueue_check(const uint8_t* pages, uint64_t count, uint8_t* ok, uint64_t*
 	P.out = w.xxh_out;
 	P.idx = w.list_b;
 	P.d_count = n2;
-	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
+	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return bail(ctr, s);
 	k_dq_compare<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, ctr, w.crc_out, w.xxh_out, ok, &ctr[3],
 	                                           w.trl);
 	k_dq_final<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ok, ctr);
@@ -738,11 +759,12 @@ int sqlite_seal(uint8_t* pages, uint64_t ps, uint64_t count, uint32_t first_pgno
 int diskqueue_seal(uint8_t* pages, uint64_t count, const fdbcrc::DevTables* tabs, int num_cus, void* ws,
                    unsigned long long* ctr, hipStream_t s) {
 	const Ws w = carve(ws, count);
+	if (setup_lists(pages + 8, 4096, true, num_cus, s)) return -1;
 	k_dq_seal_classify<<<blocks(count, kSpan), kCB, 0, s>>>(pages, count, w.list_a, w.list_b, w.list_c, ctr);
 	const uint64_t* n1 = reinterpret_cast<const uint64_t*>(&ctr[0]);
 	const uint64_t* n2 = reinterpret_cast<const uint64_t*>(&ctr[1]);
 	if (fdbcrc::launch_pages_window_list(pages, 4096, w.list_a, n1, count, 4, 0, 0xFDBEEFDBu, w.crc_out, tabs, num_cus, s))
-		return -1;
+		return bail(ctr, s);
 	fdbxxh::XxhParams P{};
 	P.base = pages + 8;
 	P.stride = 4096;
@@ -751,7 +773,7 @@ int diskqueue_seal(uint8_t* pages, uint64_t count, const fdbcrc::DevTables* tabs
 	P.out = w.xxh_out;
 	P.idx = w.list_b;
 	P.d_count = n2;
-	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return -1;
+	if (fdbxxh::launch_xxh3_pages_list(P, num_cus, s)) return bail(ctr, s);
 	k_dq_seal_write<<<blocks(count, kSpan), kCB, 0, s>>>(pages, w.list_a, w.list_b, ctr, w.crc_out, w.xxh_out);
 	k_dq_seal_v0<<<blocks(count, 4 * kL3PerWave), 256, 0, s>>>(pages, w.list_c, ctr);
 	k_pc_done<<<1, 64, 0, s>>>(ctr, nullptr);

@@ -83,8 +83,12 @@ int fdb_packets_verify_ws(const void* d_base, const uint64_t* d_buf_offsets, con
 /* Same with the library's per-stream workspace.
  * Both forms keep the walk's frame counter in a word of the stream's own
  * (zeroed when the stream is first used, put back to zero by each call's last
- * kernel: no memset per call), so calls on one stream run in stream order, and
- * a captured graph of a call replays on one stream at a time.  Frames over
+ * kernel: no memset per call), so calls on one stream run in stream order
+ * (host threads sharing a stream are serialised by a per-stream lock held
+ * through the call's last launch), and a captured graph of a call replays on
+ * the stream it was captured on, one replay at a time.  The first call on a
+ * stream allocates that word and is refused (FDB_CRC32C_EINVAL) inside a
+ * stream capture: use the stream once outside the capture first.  Frames over
  * 16 KiB take the XXH3 split route only when the packet limit allows them and
  * the stream's previous batch had some (a host-mapped hint, no
  * synchronisation); otherwise the row kernel hashes them -- the same digests,

@@ -40,11 +40,20 @@ int fdb_sqlite_verify_pages(const void* d_pages, uint64_t page_size, uint64_t co
                             uint8_t* d_status, uint64_t* d_bad, void* stream);
 int fdb_diskqueue_check_pages(const void* d_pages, uint64_t count, uint8_t* d_ok, uint64_t* d_bad, void* stream);
 
-/* Caller-owned workspace variants (no allocation, capture-safe); size from
- * fdb_pagecheck_workspace_bytes(count), 16-byte aligned.  Every form keeps its
- * list counters in words of the stream's own (zeroed when the stream is first
- * used, put back to zero by each call's last kernel: no memset per call), so a
- * captured graph of a call replays on one stream at a time. */
+/* Caller-owned workspace variants; size from fdb_pagecheck_workspace_bytes(count),
+ * 16-byte aligned.  Every form keeps its list counters in words of the
+ * stream's own (allocated and zeroed when the stream is first used, put back
+ * to zero by each call's last kernel, also on an error after its first
+ * launch: no memset per call).
+ * Threading: calls on one stream from several host threads are serialised by
+ * the library (a per-stream lock held from the counter lookup through the
+ * call's last launch), whatever workspace each passes.
+ * Capture: the _ws forms allocate nothing once the stream has been used; the
+ * first call on a stream allocates its counters and is refused with
+ * FDB_CRC32C_EINVAL inside a stream capture -- make one call on the stream
+ * outside the capture first.  A captured graph uses the counters of the stream
+ * it was captured on: replay it on that stream (or on one no other call is
+ * using at the same time), one replay at a time. */
 uint64_t fdb_pagecheck_workspace_bytes(uint64_t count);
 int fdb_sqlite_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t count, uint32_t first_pgno,
                                uint8_t* d_status, uint64_t* d_bad, void* d_workspace, uint64_t workspace_bytes,

@@ -420,3 +420,110 @@ def test_gpu_verifiers_between_other_calls_on_one_stream(cuda):
             assert np.array_equal(gx.cpu().numpy().view(np.uint64), want_x)
             assert np.array_equal(gc.cpu().numpy().view(np.uint32), want_c)
     F.release_stream(s)
+
+
+@pytest.mark.gpu
+def test_gpu_ws_calls_from_two_threads_on_one_stream(cuda):
+    """the _ws forms keep their list counters in words of the
+    stream's own; two host threads each passing its own workspace on the same
+    stream used to interleave their kernels on those counters.  The library now
+    holds a per-stream lock from the counter lookup through the call's last
+    launch: every call's verdicts stay exact."""
+    import ctypes
+    import threading
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    L = PC._lib()
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    L.fdb_sqlite_verify_pages_ws.argtypes = [vp, u64, u64, u32, vp, vp, vp, u64, vp]
+    L.fdb_diskqueue_check_pages_ws.argtypes = [vp, u64, vp, vp, vp, u64, vp]
+    pages, exp = make_sqlite_batch(1100, 4096, 5, 91)
+    dq, dq_exp = make_dq_batch(900, 92)
+    d_sq = torch.from_numpy(pages.reshape(-1).copy()).to(cuda)
+    d_dq = torch.from_numpy(dq.reshape(-1).copy()).to(cuda)
+    s = torch.cuda.Stream(cuda)
+    h = ctypes.c_void_p(s.cuda_stream)
+    reps = 12
+    nws = int(L.fdb_pagecheck_workspace_bytes(1100))
+    outs = {}
+
+    def worker(kind):
+        ws = torch.empty(nws, dtype=torch.uint8, device=cuda)
+        res = torch.empty((reps, 1100), dtype=torch.uint8, device=cuda)
+        bad = torch.empty(reps, dtype=torch.int64, device=cuda)
+        for r in range(reps):
+            if kind == "sq":
+                rc = L.fdb_sqlite_verify_pages_ws(d_sq.data_ptr(), 4096, 1100, 5, res[r].data_ptr(),
+                                                  bad[r:].data_ptr(), ws.data_ptr(), nws, h)
+            else:
+                rc = L.fdb_diskqueue_check_pages_ws(d_dq.data_ptr(), 900, res[r].data_ptr(), bad[r:].data_ptr(),
+                                                    ws.data_ptr(), nws, h)
+            assert rc == 0
+        outs[kind] = (res, bad, ws)
+
+    with torch.cuda.stream(s):
+        warm = torch.empty(1100, dtype=torch.uint8, device=cuda)
+        PC.sqlite_verify_pages(d_sq, 4096, first_pgno=5, stream=s, status=warm)
+    s.synchronize()
+    ts = [threading.Thread(target=worker, args=(k,)) for k in ("sq", "dq")]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    s.synchronize()
+    res, bad, _ = outs["sq"]
+    for r in range(reps):
+        assert np.array_equal(res[r].cpu().numpy(), exp), r
+        assert int(bad[r].item()) == int((exp == 0).sum()), r
+    res, bad, _ = outs["dq"]
+    for r in range(reps):
+        assert np.array_equal(res[r, :900].cpu().numpy(), dq_exp), r
+        assert int(bad[r].item()) == int((dq_exp == 0).sum()), r
+
+
+@pytest.mark.gpu
+def test_gpu_first_use_of_a_stream_inside_a_capture_is_refused(cuda):
+    """ADVICE r5: a stream's counters are allocated and zeroed on its first use;
+    inside a stream capture that would invalidate the capture (hipMalloc) and
+    record the zeroing into the graph, so the call is refused with EINVAL and
+    the capture stays usable; after one call outside the capture, capturing
+    works."""
+    import ctypes
+    import torch
+    import foundationdb_amd.pagecheck as PC
+    FDB_CRC32C_EINVAL = -1  # include/fdb_crc32c.h
+    L = PC._lib()
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    L.fdb_diskqueue_check_pages_ws.argtypes = [vp, u64, vp, vp, vp, u64, vp]
+    dq, dq_exp = make_dq_batch(300, 93)
+    d_dq = torch.from_numpy(dq.reshape(-1).copy()).to(cuda)
+    nws = int(L.fdb_pagecheck_workspace_bytes(300))
+    ws = torch.empty(nws, dtype=torch.uint8, device=cuda)
+    ok = torch.zeros(300, dtype=torch.uint8, device=cuda)
+    bad = torch.empty(1, dtype=torch.int64, device=cuda)
+    x = torch.zeros(4, device=cuda)
+    s = torch.cuda.Stream(cuda)
+    h = ctypes.c_void_p(s.cuda_stream)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        rc = L.fdb_diskqueue_check_pages_ws(d_dq.data_ptr(), 300, ok.data_ptr(), bad.data_ptr(), ws.data_ptr(), nws, h)
+        x.add_(1)
+    assert rc == FDB_CRC32C_EINVAL
+    g.replay()
+    torch.cuda.synchronize()
+    assert x.cpu().tolist() == [1.0] * 4
+    with torch.cuda.stream(s):
+        assert L.fdb_diskqueue_check_pages_ws(d_dq.data_ptr(), 300, ok.data_ptr(), bad.data_ptr(), ws.data_ptr(),
+                                              nws, h) == 0
+    s.synchronize()
+    assert np.array_equal(ok.cpu().numpy(), dq_exp)
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, stream=s):
+        assert L.fdb_diskqueue_check_pages_ws(d_dq.data_ptr(), 300, ok.data_ptr(), bad.data_ptr(), ws.data_ptr(),
+                                              nws, h) == 0
+    ok.zero_()
+    torch.cuda.synchronize()
+    g2.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(ok.cpu().numpy(), dq_exp)
+    del g, g2
