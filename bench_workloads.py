@@ -657,6 +657,144 @@ class DiskQueueSeal:
                          port=lambda O_: O_.diskqueue_seal_pages(host, n))
 
 
+def _redwood_pages_on_device(dev, count, ps, first_id, state):
+    """Redwood BTree pages in HBM as ArenaPage::init(XXHash64, BTreeNode, 1) +
+    setWriteInfo(pageID, version) leave them (fdbserver/kvstore/IPager.h:448-502):
+    header version 1, encoding header at 43, payload at 51, firstPhysicalPageID
+    first_id + i; splitmix64 payloads.  Not sealed."""
+    from oracle import oracle as O
+    buf = torch.empty(count * ps, dtype=torch.uint8, device=dev)
+    F.fill_splitmix64(buf, state)
+    tmpl = np.zeros(O.REDWOOD_HEADER, np.uint8)
+    O.redwood_init_page(tmpl, 0, page_type=2, sub_type=1, write_version=1)
+    pages = buf.view(count, ps)
+    pages[:, :43] = torch.from_numpy(tmpl[:43]).to(dev)
+    ids = (first_id + torch.arange(count, device=dev, dtype=torch.int64)).to(torch.int32)
+    pages[:, 15:19] = ids.view(torch.uint8).view(count, 4)
+    return buf
+
+
+class RedwoodVerify:
+    """Redwood page reads (ArenaPage::postReadHeader + postReadPayload,
+    fdbserver/kvstore/IPager.h:527-565, run per page by the pager at
+    VersionedBTree.cpp:2842-2844) over a batch: 512 Ki BTree pages of the
+    default 8 KiB (REDWOOD_DEFAULT_PAGE_SIZE, fdbserver/core/ServerKnobs.cpp:1332),
+    sealed by the engine's own preWrite batch, one in 16 with a flipped payload
+    byte (fdb_redwood_verify_pages)."""
+    metric = ("device-resident Redwood page verification GiB/s (512 Ki 8 KiB BTree pages: header XXH3 + seeded "
+              "payload XXH3); % of HBM-read peak")
+    kernel_name = "fdb_redwood_verify_pages (k_rw_head + XXH3 planner + k_xxh3_vrows (seeded) + k_rw_verify_fin)"
+    PS, FIRST = 8192, 1000
+
+    def __init__(self, dev, rank, count=1 << 19):
+        import foundationdb_amd.redwood as RW
+        self.RW, self.count = RW, count
+        ps = self.PS
+        self.buf = _redwood_pages_on_device(dev, count, ps, self.FIRST, STATE ^ 0x4ED0)
+        st = RW.seal_pages(self.buf, ps, count, first_page_id=self.FIRST)
+        assert bool((st == 0).all())
+        pages = self.buf.view(count, ps)
+        bad = torch.arange(count, device=dev) % 16 == 5
+        col = 51 + (torch.arange(count, device=dev) * 131) % (ps - 51)
+        rows = torch.nonzero(bad).view(-1)
+        pages[rows, col[rows]] ^= 0x20
+        self.expect = torch.where(bad, 5, 0).to(torch.uint8)
+        self.bytes_per_step = count * ps
+        # every page read once (header + payload) + the status byte
+        self.algorithmic_bytes_per_step = count * (ps + 1)
+        self.data_desc = (f"synthetic: splitmix64 payloads (state 0x{STATE ^ 0x4ED0:X}) in HBM, Redwood header "
+                          "version 1 / XXHash64 encoding, sealed by fdb_redwood_seal_pages, 1 in 16 payloads corrupt")
+        self.config = {"workload": f"{count} x {ps >> 10} KiB Redwood BTree pages, device-resident", "pages": count,
+                       "page_size": ps}
+        self.status = torch.empty(count, dtype=torch.uint8, device=dev)
+        self.nbad = torch.empty(1, dtype=torch.uint64, device=dev)
+
+    def step(self, stream):
+        self.RW.verify_pages(self.buf, self.PS, self.count, first_page_id=self.FIRST, stream=stream,
+                             status=self.status, bad=self.nbad)
+
+    def verify(self):
+        from oracle import oracle as O
+        if not torch.equal(self.status, self.expect):
+            return False
+        if int(self.nbad.cpu().numpy().view(np.uint64)[0]) != int((self.expect != 0).sum()):
+            return False
+        idx = np.random.default_rng(3).choice(self.count, 256, replace=False)
+        host = self.buf.view(self.count, self.PS)[torch.from_numpy(idx).to(self.buf.device)].cpu().numpy()
+        st = self.status.cpu().numpy()
+        if O.pagecheck_reference_available():
+            want, _ = O.ref_redwood_verify_pages(host, self.PS, idx.size, ids=(self.FIRST + idx).astype(np.uint32))
+        else:
+            want = [O.redwood_verify_page(host[j], self.FIRST + int(i)) for j, i in enumerate(idx)]
+        return all(int(want[j]) == int(st[i]) for j, i in enumerate(idx))
+
+    def cpu_sample(self):
+        n = 32768
+        host = self.buf[:n * self.PS].cpu().numpy()
+        return CpuSample(f"first {n} pages through postReadHeader + postReadPayload (IPager.h:527-565) composed "
+                         "from the reference's own XXH3_64bits / XXH3_64bits_withSeed compiled unmodified "
+                         "(oracle/ref_pagecheck.c), one page per call",
+                         n * self.PS, host,
+                         ref=lambda O_: O_.ref_redwood_verify_pages(host, self.PS, n, first_id=self.FIRST, inplace=True),
+                         ref_available=lambda O_: O_.pagecheck_reference_available(),
+                         port=lambda O_: [O_.redwood_verify_page(host[self.PS * i:self.PS * (i + 1)], self.FIRST + i)
+                                          for i in range(n)])
+
+
+class RedwoodSeal:
+    """Redwood page writes (ArenaPage::preWrite, fdbserver/kvstore/IPager.h:500-525,
+    per page at VersionedBTree.cpp:2595): 512 Ki 8 KiB BTree pages sealed in
+    place each step (fdb_redwood_seal_pages)."""
+    metric = ("device-resident Redwood page sealing GiB/s (512 Ki 8 KiB BTree pages: seeded payload XXH3 + header "
+              "XXH3); % of HBM-read peak")
+    kernel_name = "fdb_redwood_seal_pages (k_rw_head + XXH3 planner + k_xxh3_vrows (seeded) + k_rw_seal_fin)"
+    PS, FIRST = 8192, 77
+
+    def __init__(self, dev, rank, count=1 << 19):
+        import foundationdb_amd.redwood as RW
+        self.RW, self.count = RW, count
+        self.buf = _redwood_pages_on_device(dev, count, self.PS, self.FIRST, STATE ^ 0x4ED1)
+        self.sample = np.random.default_rng(4).choice(count, 64, replace=False)
+        self.orig = self.buf.view(count, self.PS)[torch.from_numpy(self.sample).to(dev)].cpu().numpy()
+        self.status = torch.empty(count, dtype=torch.uint8, device=dev)
+        self.bytes_per_step = count * self.PS
+        self.algorithmic_bytes_per_step = count * self.PS  # each page read once, 16 header bytes written
+        self.data_desc = f"synthetic: splitmix64 payloads (state 0x{STATE ^ 0x4ED1:X}), Redwood headers, sealed in place"
+        self.config = {"workload": f"{count} x {self.PS >> 10} KiB Redwood BTree pages sealed in place, "
+                                   "device-resident", "pages": count, "page_size": self.PS}
+
+    def step(self, stream):
+        self.RW.seal_pages(self.buf, self.PS, self.count, first_page_id=self.FIRST, stream=stream, status=self.status)
+
+    def verify(self):
+        from oracle import oracle as O
+        if not bool((self.status == 0).all()):
+            return False
+        st, bad = self.RW.verify_pages(self.buf, self.PS, self.count, first_page_id=self.FIRST)
+        if not bool((st == 0).all()) or int(bad.cpu().numpy().view(np.uint64)[0]) != 0:
+            return False
+        got = self.buf.view(self.count, self.PS)[torch.from_numpy(self.sample).to(self.buf.device)].cpu().numpy()
+        for j, i in enumerate(self.sample):
+            if O.pagecheck_reference_available():
+                want, _ = O.ref_redwood_seal_pages(self.orig[j], self.PS, 1, first_id=self.FIRST + int(i))
+            else:
+                want = O.redwood_seal_page(self.orig[j], self.FIRST + int(i))[1]
+            if not np.array_equal(got[j], want):
+                return False
+        return True
+
+    def cpu_sample(self):
+        n = 32768
+        host = self.buf[:n * self.PS].cpu().numpy().copy()
+        return CpuSample(f"first {n} pages sealed in place by preWrite (IPager.h:500-525) composed from the "
+                         "reference's own XXH3_64bits / XXH3_64bits_withSeed (oracle/ref_pagecheck.c)",
+                         n * self.PS, host,
+                         ref=lambda O_: O_.ref_redwood_seal_pages(host, self.PS, n, first_id=self.FIRST, inplace=True),
+                         ref_available=lambda O_: O_.pagecheck_reference_available(),
+                         port=lambda O_: [O_.redwood_seal_page(host[self.PS * i:self.PS * (i + 1)], self.FIRST + i)
+                                          for i in range(n)])
+
+
 class Xxh3Zipf(VarLen):
     """XXH3-64 of every packet of the configs[2] Zipf batch (FlowTransport packet
     checksum, fdbrpc/FlowTransport.cpp:2025-2068), device-resident."""
@@ -892,4 +1030,6 @@ WORKLOADS = {
     "diskqueue-seal": lambda dev, rank: DiskQueueSeal(dev, rank),
     "packets-verify": lambda dev, rank: PacketsVerify(dev, rank),
     "xxh3-chained": lambda dev, rank: Xxh3Chained(dev, rank),
+    "redwood-verify": lambda dev, rank: RedwoodVerify(dev, rank),
+    "redwood-seal": lambda dev, rank: RedwoodSeal(dev, rank),
 }

@@ -13,10 +13,12 @@
 #include "../../include/fdb_crc32c.h"
 #include "../../include/fdb_packets.h"
 #include "../../include/fdb_pagecheck.h"
+#include "../../include/fdb_redwood.h"
 #include "../../include/fdb_xxh3.h"
 #include "crc32c_device.h"
 #include "packets.h"
 #include "pagecheck.h"
+#include "redwood.h"
 #include "xxh3_device.h"
 
 namespace fdbcrc {
@@ -931,6 +933,92 @@ int fdb_diskqueue_seal_pages(void* d_pages, uint64_t count, void* stream) {
 	                              &hold))
 		return rc;
 	return fdb_diskqueue_seal_pages_ws(d_pages, count, ws, have, stream);
+}
+
+// ---- Redwood pages (include/fdb_redwood.h) ----------------------------------
+static int redwood_args(const void* d_pages, uint64_t page_size, uint64_t count, const char* who) {
+	if (!d_pages) return fail(FDB_CRC32C_EINVAL, who);
+	if (page_size % 16 || page_size < 512 || page_size >= (1ull << 31))
+		return fail(FDB_CRC32C_EINVAL, "redwood pages: page_size must be a multiple of 16 in [512, 2^31)");
+	if (reinterpret_cast<uintptr_t>(d_pages) % 16) return fail(FDB_CRC32C_EINVAL, "redwood pages: pages not 16-byte aligned");
+	if (count > 0xFFFFFFFFull) return fail(FDB_CRC32C_EINVAL, "redwood pages: more than 2^32 - 1 pages");
+	return 0;
+}
+
+uint64_t fdb_redwood_workspace_bytes(uint64_t count, uint64_t page_size) {
+	DeviceState* st = nullptr;
+	if (device_state(&st)) return 0;
+	return fdbrw::workspace_bytes(count, page_size, st->num_cus);
+}
+
+int fdb_redwood_verify_pages_ws(const void* d_pages, uint64_t page_size, uint64_t count, const uint32_t* d_page_ids,
+                                uint32_t first_page_id, uint8_t* d_status, uint64_t* d_bad, void* d_workspace,
+                                uint64_t workspace_bytes, void* stream) {
+	const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+	if (count == 0) {
+		if (d_bad) (void)hipMemsetAsync(d_bad, 0, 8, s);
+		return 0;
+	}
+	if (int rc = redwood_args(d_pages, page_size, count, "fdb_redwood_verify_pages: null pointer")) return rc;
+	if (!d_status) return fail(FDB_CRC32C_EINVAL, "fdb_redwood_verify_pages: null status");
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	if (!d_workspace || workspace_bytes < fdbrw::workspace_bytes(count, page_size, st->num_cus) ||
+	    reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_redwood_verify_pages: workspace too small or misaligned");
+	if (fdbrw::verify(static_cast<const uint8_t*>(d_pages), page_size, count, d_page_ids, first_page_id, d_status,
+	                  d_bad, st->num_cus, d_workspace, workspace_bytes, s))
+		return fail(FDB_CRC32C_EHIP, "fdb_redwood_verify_pages: launch setup failed");
+	return check_launch("fdb_redwood_verify_pages launch");
+}
+
+int fdb_redwood_verify_pages(const void* d_pages, uint64_t page_size, uint64_t count, const uint32_t* d_page_ids,
+                             uint32_t first_page_id, uint8_t* d_status, uint64_t* d_bad, void* stream) {
+	if (count == 0)
+		return fdb_redwood_verify_pages_ws(d_pages, page_size, 0, d_page_ids, first_page_id, d_status, d_bad, nullptr,
+		                                   0, stream);
+	if (int rc = redwood_args(d_pages, page_size, count, "fdb_redwood_verify_pages: null pointer")) return rc;
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
+	                              fdbrw::workspace_bytes(count, page_size, st->num_cus), &ws, &have, &hold))
+		return rc;
+	return fdb_redwood_verify_pages_ws(d_pages, page_size, count, d_page_ids, first_page_id, d_status, d_bad, ws, have,
+	                                   stream);
+}
+
+int fdb_redwood_seal_pages_ws(void* d_pages, uint64_t page_size, uint64_t count, const uint32_t* d_page_ids,
+                              uint32_t first_page_id, uint8_t* d_status, void* d_workspace, uint64_t workspace_bytes,
+                              void* stream) {
+	if (count == 0) return 0;
+	if (int rc = redwood_args(d_pages, page_size, count, "fdb_redwood_seal_pages: null pointer")) return rc;
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	if (!d_workspace || workspace_bytes < fdbrw::workspace_bytes(count, page_size, st->num_cus) ||
+	    reinterpret_cast<uintptr_t>(d_workspace) % 16)
+		return fail(FDB_CRC32C_EINVAL, "fdb_redwood_seal_pages: workspace too small or misaligned");
+	if (fdbrw::seal(static_cast<uint8_t*>(d_pages), page_size, count, d_page_ids, first_page_id, d_status, st->num_cus,
+	                d_workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream)))
+		return fail(FDB_CRC32C_EHIP, "fdb_redwood_seal_pages: launch setup failed");
+	return check_launch("fdb_redwood_seal_pages launch");
+}
+
+int fdb_redwood_seal_pages(void* d_pages, uint64_t page_size, uint64_t count, const uint32_t* d_page_ids,
+                           uint32_t first_page_id, uint8_t* d_status, void* stream) {
+	if (count == 0) return 0;
+	if (int rc = redwood_args(d_pages, page_size, count, "fdb_redwood_seal_pages: null pointer")) return rc;
+	DeviceState* st = nullptr;
+	if (int rc = device_state(&st)) return rc;
+	void* ws = nullptr;
+	uint64_t have = 0;
+	std::unique_lock<std::mutex> hold;
+	if (int rc = stream_workspace(st, reinterpret_cast<hipStream_t>(stream),
+	                              fdbrw::workspace_bytes(count, page_size, st->num_cus), &ws, &have, &hold))
+		return rc;
+	return fdb_redwood_seal_pages_ws(d_pages, page_size, count, d_page_ids, first_page_id, d_status, ws, have, stream);
 }
 
 // ---- FlowTransport receive verification (include/fdb_packets.h) ------------

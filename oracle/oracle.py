@@ -346,6 +346,10 @@ def pagecheck_reference():
         L.ref_sqlite_seal_pages.argtypes = [vp, u64, u64, ctypes.c_uint32]
         L.ref_diskqueue_seal_pages.restype = None
         L.ref_diskqueue_seal_pages.argtypes = [vp, u64]
+        L.ref_redwood_verify_pages.restype = u64
+        L.ref_redwood_verify_pages.argtypes = [vp, u64, u64, vp, ctypes.c_uint32, vp]
+        L.ref_redwood_seal_pages.restype = None
+        L.ref_redwood_seal_pages.argtypes = [vp, u64, u64, vp, ctypes.c_uint32, vp]
         _pcref = L
     return _pcref
 
@@ -391,6 +395,36 @@ def ref_diskqueue_seal_pages(pages, count, inplace=False):
     assert count * 4096 <= out.nbytes
     pagecheck_reference().ref_diskqueue_seal_pages(out.ctypes.data, count)
     return out
+
+
+def _ids_ptr(ids):
+    if ids is None:
+        return None, None
+    a = np.ascontiguousarray(ids, dtype=np.uint32)
+    return a, a.ctypes.data
+
+
+def ref_redwood_verify_pages(pages, page_size, count, ids=None, first_id=0, inplace=False):
+    """(status per page, bad count): postReadHeader + postReadPayload composed
+    from the reference's XXH3_64bits / XXH3_64bits_withSeed (oracle/ref_pagecheck.c).
+    The reference zeroes and restores the checksum field in place, so the
+    pages come back unchanged; without `inplace` a copy is checked."""
+    buf = _seal_target(pages, inplace)
+    st = np.zeros(count, np.uint8)
+    keep, ip = _ids_ptr(ids)
+    bad = pagecheck_reference().ref_redwood_verify_pages(buf.ctypes.data, page_size, count, ip, first_id,
+                                                         st.ctypes.data)
+    return st, int(bad)
+
+
+def ref_redwood_seal_pages(pages, page_size, count, ids=None, first_id=0, inplace=False):
+    """(sealed copy -- or `pages` itself with inplace --, status per page):
+    preWrite(pageID) from the reference primitives."""
+    out = _seal_target(pages, inplace)
+    st = np.zeros(count, np.uint8)
+    keep, ip = _ids_ptr(ids)
+    pagecheck_reference().ref_redwood_seal_pages(out.ctypes.data, page_size, count, ip, first_id, st.ctypes.data)
+    return out, st
 
 
 # ---------------------------------------------------------------- page formats
@@ -489,6 +523,59 @@ def diskqueue_check_page(page):
         return int(int.from_bytes(page[:4], "little") == crc32c(0xFDBEEFDB, page[4:]))
     if ver == 2:
         return int(int.from_bytes(page[:8], "little") == xxh3_64(page[8:]))
+    return 0
+
+
+# Redwood pages (fdbserver/kvstore/IPager.h:246-331, 480-565): the byte layout
+# of header version 1 and the XXHash64 encoding.
+REDWOOD_HEADER = 51  # PageHeader (4) + RedwoodHeaderV1 (39) + XXHashEncoder::Header (8)
+
+
+def redwood_init_page(page, page_id, page_type=2, sub_type=1, write_version=1, write_time=0.0):
+    """ArenaPage::init(XXHash64, pageType, pageSubType) (:448-470) and
+    setWriteInfo(pageID, version) (:496-502) on a page buffer (in place):
+    header version 1, encoding header at 43, payload at 51."""
+    import struct
+    page[0:4] = np.frombuffer(bytes([1, 0, 43, REDWOOD_HEADER]), np.uint8)
+    hdr = struct.pack("<BBBQIIIdq", page_type, sub_type, 0, 0, page_id, 0xFFFFFFFF, 0xFFFFFFFF, write_time,
+                      write_version)
+    page[4:43] = np.frombuffer(hdr, np.uint8)
+    return page
+
+
+def redwood_seal_page(page, page_id):
+    """preWrite(pageID) (:500-525) on a copy: (status, page')."""
+    pg = np.array(np.frombuffer(bytes(page), np.uint8), copy=True)
+    enc, eho, po = int(pg[1]), int(pg[2]), int(pg[3])
+    if enc != 0:
+        return 4, pg
+    pg[eho:eho + 8] = np.frombuffer(xxh3_64(bytes(pg[po:]), page_id).to_bytes(8, "little"), np.uint8)
+    if pg[0] != 1:
+        return 1, pg
+    pg[7:15] = 0
+    pg[7:15] = np.frombuffer(xxh3_64(bytes(pg[:po])).to_bytes(8, "little"), np.uint8)
+    return 0, pg
+
+
+def redwood_verify_page(page, page_id):
+    """postReadHeader(pageID, verify = true) then postReadPayload(pageID):
+    0, or the first failure (1 version, 2 header checksum, 3 page ID, 4 encoding, 5 decoding)."""
+    pg = bytearray(bytes(page))
+    ver, enc, eho, po = pg[0], pg[1], pg[2], pg[3]
+    if ver != 1:
+        return 1
+    saved = int.from_bytes(pg[7:15], "little")
+    pg[7:15] = bytes(8)
+    calc = xxh3_64(bytes(pg[:po]))
+    pg[7:15] = saved.to_bytes(8, "little")
+    if saved != calc:
+        return 2
+    if int.from_bytes(pg[15:19], "little") != page_id:
+        return 3
+    if enc != 0:
+        return 4
+    if int.from_bytes(pg[eho:eho + 8], "little") != xxh3_64(bytes(pg[po:]), page_id):
+        return 5
     return 0
 
 

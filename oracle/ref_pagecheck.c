@@ -25,6 +25,17 @@
  * (DiskQueue.cpp:1089-1105) by implementationVersion: V0 the hashlittle2 UID,
  * V1 hash32 = crc32c_append(0xfdbeefdb, &_unused, 4092), V2 and every other
  * version hash64 = XXH3_64bits(&magic, 4088).
+ *
+ * Redwood (fdbserver/kvstore/IPager.h): ref_redwood_verify_pages restates
+ * ArenaPage::postReadHeader(pageID, verify = true) then postReadPayload(pageID)
+ * (:527-565) -- header version 1, RedwoodHeaderV1::verifyChecksum (:303-313:
+ * the checksum field at byte 7 zeroed, XXH3_64bits over [0, payloadOffset),
+ * restored), firstPhysicalPageID (byte 15) == pageID, XXHashEncoder::decode
+ * (:325-331: XXH3_64bits_withSeed(payload, logicalSize - payloadOffset,
+ * pageID) against the u64 at the encoding header); status 0 or the first
+ * failure (1 version, 2 header checksum, 3 page ID, 4 encoding, 5 decoding).
+ * ref_redwood_seal_pages restates preWrite(pageID) (:500-525): encode, then
+ * RedwoodHeaderV1::updateChecksum (:297-301).
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -32,6 +43,7 @@
 
 uint32_t crc32c_append(uint32_t crc, const uint8_t* input, size_t length);
 uint64_t XXH3_64bits(const void* data, size_t len);
+uint64_t XXH3_64bits_withSeed(const void* data, size_t len, uint64_t seed);
 void hashlittle2(const void* key, size_t length, uint32_t* pc, uint32_t* pb);
 
 static uint32_t rd32(const uint8_t* p) {
@@ -129,4 +141,51 @@ uint64_t ref_diskqueue_check_pages(const uint8_t* pages, uint64_t count, uint8_t
 		bad += !ok[i];
 	}
 	return bad;
+}
+
+/* Redwood: PageHeader (4 bytes) + RedwoodHeaderV1 (39 bytes), byte-packed. */
+static int redwood_check(uint8_t* page, uint64_t page_size, uint32_t id) {
+	const uint8_t ver = page[0], enc = page[1], eho = page[2], po = page[3];
+	if (ver != 1) return 1;
+	const uint64_t saved = rd64(page + 7);
+	wr64(page + 7, 0);
+	const uint64_t calc = XXH3_64bits(page, po);
+	wr64(page + 7, saved);
+	if (saved != calc) return 2;
+	if (rd32(page + 15) != id) return 3;
+	if (enc != 0) return 4;
+	if (rd64(page + eho) != XXH3_64bits_withSeed(page + po, (size_t)(page_size - po), id)) return 5;
+	return 0;
+}
+
+uint64_t ref_redwood_verify_pages(uint8_t* pages, uint64_t page_size, uint64_t count, const uint32_t* ids,
+                                  uint32_t first_id, uint8_t* status) {
+	uint64_t bad = 0;
+	for (uint64_t i = 0; i < count; ++i) {
+		const int s = redwood_check(pages + i * page_size, page_size, ids ? ids[i] : first_id + (uint32_t)i);
+		status[i] = (uint8_t)s;
+		bad += s != 0;
+	}
+	return bad;
+}
+
+void ref_redwood_seal_pages(uint8_t* pages, uint64_t page_size, uint64_t count, const uint32_t* ids,
+                            uint32_t first_id, uint8_t* status) {
+	for (uint64_t i = 0; i < count; ++i) {
+		uint8_t* page = pages + i * page_size;
+		const uint32_t id = ids ? ids[i] : first_id + (uint32_t)i;
+		const uint8_t enc = page[1], eho = page[2], po = page[3];
+		if (enc != 0) {
+			status[i] = 4;
+			continue;
+		}
+		wr64(page + eho, XXH3_64bits_withSeed(page + po, (size_t)(page_size - po), id));
+		if (page[0] != 1) {
+			status[i] = 1;
+			continue;
+		}
+		wr64(page + 7, 0);
+		wr64(page + 7, XXH3_64bits(page, po));
+		status[i] = 0;
+	}
 }
