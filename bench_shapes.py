@@ -62,6 +62,21 @@ def layout(lengths, align):
     return offsets, (total + 7) // 8 * 8
 
 
+def scattered_layout(lengths, align, seed=9):
+    """The same buffers laid out in a shuffled order (packets gathered from many
+    connections' receive buffers, fdbrpc/FlowTransport.cpp:1260): buffer i's
+    offset is not ascending in i, so the extent route's packing check refuses
+    the batch and it takes the general window route.  Same extent as layout()."""
+    lengths = np.asarray(lengths, dtype=np.uint64)
+    padded = (lengths + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    perm = np.random.default_rng(seed).permutation(lengths.size)
+    pos = np.concatenate([[0], np.cumsum(padded[perm])[:-1]]).astype(np.uint64)
+    offsets = np.empty(lengths.size, np.uint64)
+    offsets[perm] = pos
+    total = int(padded.sum()) if lengths.size else 0
+    return offsets, (total + 7) // 8 * 8
+
+
 def lengths_digest(lengths):
     """sha256 of the little-endian u64 length list: pins the shape across numpy versions."""
     return hashlib.sha256(np.ascontiguousarray(lengths, dtype="<u8").tobytes()).hexdigest()
@@ -70,6 +85,8 @@ def lengths_digest(lengths):
 SHAPES = {
     "zipf": (zipf_lengths, ZIPF_ALIGN),
     "chunks": (chunk_lengths, CHUNK_ALIGN),
+    # configs[2]'s packets, scattered: the general (window) route's batch
+    "zipf-scattered": (zipf_lengths, ZIPF_ALIGN),
 }
 
 
@@ -77,7 +94,7 @@ def shape(name):
     """(lengths, offsets, extent_bytes) of the named configs batch."""
     fn, align = SHAPES[name]
     lengths = fn()
-    offsets, extent = layout(lengths, align)
+    offsets, extent = (scattered_layout if name.endswith("-scattered") else layout)(lengths, align)
     return lengths, offsets, extent
 
 

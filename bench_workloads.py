@@ -186,7 +186,7 @@ class VarLen:
         self.dev, self.seed = dev, seed
         self.metric, self.shape = metric, shape
         lengths = np.asarray(lengths, dtype=np.uint64)
-        offsets, extent = S.layout(lengths, align)
+        offsets, extent = (S.scattered_layout if shape and shape.endswith("-scattered") else S.layout)(lengths, align)
         self.h_offsets, self.h_lengths = offsets, lengths
         self.buf = torch.empty(extent, dtype=torch.uint8, device=dev)
         F.fill_splitmix64(self.buf, STATE)
@@ -1014,6 +1014,11 @@ WORKLOADS = {
                                      "Zipf(1.0) packet sizes 64 B - 16 KiB, ~1 GiB per batch, 256 B-aligned offsets",
                                      metric="device-resident CRC32C GiB/s on Zipf 64 B-16 KiB packet batches; "
                                             "% of HBM-read peak", shape="zipf"),
+    "zipf-scattered": lambda dev, rank: VarLen(dev, rank, zipf_lengths(), 256,
+                                               "Zipf(1.0) packet sizes 64 B - 16 KiB, ~1 GiB per batch, 256 B-aligned, "
+                                               "laid out in shuffled order (offsets not ascending: the window route)",
+                                               metric="device-resident CRC32C GiB/s on scattered Zipf 64 B-16 KiB "
+                                                      "packet batches; % of HBM-read peak", shape="zipf-scattered"),
     "chunks": lambda dev, rank: VarLen(dev, rank, chunk_lengths(), 4096,
                                        "log-uniform 4 KiB - 1 MiB backup chunks, ~1 GiB per batch",
                                        metric="device-resident CRC32C GiB/s on 4 KiB-1 MiB chunk batches; "

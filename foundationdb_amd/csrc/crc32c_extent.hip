@@ -42,6 +42,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "crc32c_common.h"
 
@@ -53,6 +54,13 @@ typedef __attribute__((address_space(1))) const uint32_t xg_u32;
 typedef __attribute__((address_space(1))) const uint64_t xg_u64;
 __device__ __forceinline__ uint32_t xld32(const uint32_t* p) { return *((xg_u32*)reinterpret_cast<uintptr_t>(p)); }
 __device__ __forceinline__ uint64_t xld64(const uint64_t* p) { return *((xg_u64*)reinterpret_cast<uintptr_t>(p)); }
+// A uniform word through the constant address space: s_load (lgkmcnt), so
+// waiting for it never waits for the block loads in flight (in-order vmcnt);
+// only for words no kernel of the launch writes (the grab map).
+__device__ __forceinline__ uint32_t sld32(const uint32_t* p) {
+	typedef __attribute__((address_space(4))) const uint32_t c_u32;
+	return *((const c_u32*)reinterpret_cast<uintptr_t>(p));
+}
 
 // Lane-parallel multiply by a constant whose nibble tables are in global
 // memory (8 gathers, L2-resident).
@@ -77,6 +85,7 @@ struct XParams {
 	uint64_t nwave;  // waves of k_xstream (its static ranges)
 	uint32_t* ctr;   // k_xgrab: the stream's per-workgroup grab counters (page_counters)
 	bool grabs;      // k_xgrab streamed the batch (else k_xstream's static ranges)
+	uint64_t ngrid;  // workgroups of the grab stream (k_xgrab / k_xgf): one per CU
 };
 
 __device__ __forceinline__ void x_buffer(const XParams& P, uint64_t i, uint64_t& P0, uint64_t& P1) {
@@ -401,21 +410,20 @@ __global__ __launch_bounds__(1024) void k_xstream(XParams P) {
 #ifdef FDBX_TIMES
 // development: per-wave start / end timestamps of k_xgrab (s_memrealtime, 100 MHz)
 __device__ uint64_t g_xt[16384][4];
+// ... per workgroup of k_xgf: start, stream done, finishing set up, own buffers done, end
+__device__ uint64_t g_xft[1024][8];
 #endif
-__global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
+// The grab streaming of one workgroup (k_xgrab, and the first phase of
+// k_xgf): every grab of its range and, in workgroup 0, the last grab; the
+// points and aggregates stored; returns after a barrier once every wave's
+// stores have completed and the workgroup's grab counter is back at zero.
+// fill: the table loads issued by the caller (in flight while it ran the
+// launch checks); lds: the 160 KiB image.
+__device__ __forceinline__ void xgrab_stream(const XParams& P, const XGeo G, FillRegs& fill, uint32_t* lds) {
 #ifdef FDBX_TIMES
 	const uint64_t xt0 = __builtin_amdgcn_s_memrealtime();
 	uint32_t xt_grabs = 0;
 #endif
-	// (the table loads first: vector loads, in flight while the checks' scalar
-	// loads return)
-	FillRegs fill;
-	fill_issue_1024(fill, P.tabs);
-	const XStart X0 = x_start(P);
-	if (!X0.packed) return;  // k_xfin checksums this batch buffer by buffer
-	if (X0.G.nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
-	__shared__ uint32_t lds[kLdsBytesB / 4];
-	const XGeo G = X0.G;
 	const LaneCtx c = make_ctx();
 	const uint32_t lane = (uint32_t)c.lane;
 	const uint32_t col4 = (lane & 31) * 4;
@@ -538,7 +546,7 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 		if (qn + (uint32_t)__builtin_popcountll(__ballot(oe)) > 64) store_queue();
 		push(oe, 2 * (q0 + lane) + 1, Ve, Ye);
 	};
-	auto wq_of = [&](uint32_t g) -> uint32_t { return rdfirst(xld32(P.x.wq + g)); };
+	auto wq_of = [&](uint32_t g) -> uint32_t { return sld32(P.x.wq + g); };
 	if (gA < nd) {
 		q = wq_of(gA);
 		prefetch(q);
@@ -688,7 +696,7 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 			unit_h(u0, H, Y);
 			__builtin_amdgcn_sched_barrier(0);
 			const bool last_step = s + 1 == spg;  // (not step 0: a grab has at least two)
-			qnx = last_step ? rdfirst(wqv) : 0u;
+			qnx = last_step ? wqv : 0u;
 			// the grab's window (its metadata prefetched a grab ahead; the next
 			// window's loads issued ahead of the next unit's, so that a window
 			// retired in this unit waits only for them); the next grab and its
@@ -697,7 +705,7 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 				make_window(q);
 				prefetch(q + 64);
 				gB = clampg(g0 + wpb + rdlane(req, 0));
-				wqv = xld32(P.x.wq + (gB < nd ? gB : 0u));
+				wqv = sld32(P.x.wq + (gB < nd ? gB : 0u));
 			}
 			// the next unit's loads go out before this unit's points are captured
 			load_step_unit(u0, last_step ? gB : gA, last_step ? 0u : s + 1, 0);
@@ -741,6 +749,18 @@ __global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
 	__builtin_amdgcn_s_waitcnt(0);
 	__syncthreads();
 	if (threadIdx.x == 0) *my_ctr = 0;
+}
+
+__global__ __launch_bounds__(1024) void k_xgrab(XParams P) {
+	// (the table loads first: vector loads, in flight while the checks' scalar
+	// loads return)
+	FillRegs fill;
+	fill_issue_1024(fill, P.tabs);
+	const XStart X0 = x_start(P);
+	if (!X0.packed) return;  // k_xfin checksums this batch buffer by buffer
+	if (X0.G.nblk == 0) return;  // every buffer empty at one 16-byte-aligned address: k_xfin alone
+	__shared__ uint32_t lds[kLdsBytesB / 4];
+	xgrab_stream(P, X0.G, fill, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -925,49 +945,29 @@ __device__ __forceinline__ uint32_t wave_chain(const uint32_t* agg, const uint32
 	return part;
 }
 
-__global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
-	__shared__ uint32_t lds[kFinWords];
-	const bool packed = x_packed(P);
-	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat) {  // for the stream's next route choice
-		// the count kernel's statistics (staged in xhdr, kXStage) and this
-		// batch's back-off word (one round trip: issued with x_packed's loads)
-		const uint64_t* st = reinterpret_cast<const uint64_t*>(P.x.xhdr) + kXStage;
-		uint64_t v[kHstatPacked + 1];
-#pragma unroll
-		for (int k = 0; k <= kHstatPacked; ++k) v[k] = st[k];
-#pragma unroll
-		for (int k = 0; k <= kHstatPacked; ++k) P.hstat[k] = v[k];
-		P.hstat[kHstatXfail] = x_unordered(P) ? kXfailBackoff : 0;
-	}
+// The finishing pass's setup (k_xfin, and the second phase of k_xgf): its
+// LDS tables and the chained units' geometry.  Ends with a barrier.
+struct XFin {
+	uint64_t per;         // blocks per chained unit (grab or static range)
+	uint32_t lgp;         // log2(per) for grabs (a power of two), else 64
+	uint32_t cbase;       // LDS nibble tables of C = M^per
+	const uint32_t* agg;  // the units' aggregates
+};
+__device__ __forceinline__ XFin xfin_setup(const XParams& P, uint32_t* lds, const XGeo& G) {
 	const DevTables* T = P.tabs;
-	if (!packed) {
-		for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) lds[kFinS4 + k] = xld32(&T->slice4[0][0] + k);
-		__syncthreads();
-		x_fallback(P, lds + kFinS4);
-		return;
-	}
-	// (x_start's one-round-trip form here holds the kernel's arguments in
-	// SGPRs across the pass: 5 SGPR spills)
-	const XGeo G = x_geo(P);
-	if (G.nblk == 0) {  // every buffer empty at one 16-byte-aligned address: crc32c_append(seed, p, 0) == seed
-		for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.count;
-		     i += (uint64_t)gridDim.x * blockDim.x)
-			P.out[i] = P.seeds ? xld32(P.seeds + i) : P.seed;
-		return;
-	}
+	XFin F;
 	// the chained units: k_xgrab's grabs or k_xstream's static ranges
-	const uint64_t per = P.grabs ? x_gsz(G.nblk, P.x.capg) : x_per(G.nblk, P.nwave);
-	const uint32_t lgp = P.grabs ? x_log2(per) : 64u;  // grabs: a power of two
-	const uint32_t* const agg = P.grabs ? P.x.gagg : P.x.ragg;
-	const uint32_t* s4 = lds + kFinS4;
+	F.per = P.grabs ? x_gsz(G.nblk, P.x.capg) : x_per(G.nblk, P.nwave);
+	F.lgp = P.grabs ? x_log2(F.per) : 64u;  // grabs: a power of two
+	F.agg = P.grabs ? P.x.gagg : P.x.ragg;
 	fin_fill(lds, T);
 	// nibble tables of C = M^per (the unit stride), for the straddling
 	// buffers' aggregate chains: entry [n][v] = (v x^4n) * C, bit by bit --
 	// except for grabs of fewer than 64 blocks, whose M^gsz is one of the
 	// block-power tables already copied (no build, no barrier wait on it)
-	const uint32_t cbase = per < 64 ? kFinBp0 + 128 * (uint32_t)per : kFinC;
-	if (per >= 64 && threadIdx.x < 128) {
-		const uint32_t C = xmul_blocks(T, 0x80000000u, (uint32_t)per);
+	F.cbase = F.per < 64 ? kFinBp0 + 128 * (uint32_t)F.per : kFinC;
+	if (F.per >= 64 && threadIdx.x < 128) {
+		const uint32_t C = xmul_blocks(T, 0x80000000u, (uint32_t)F.per);
 		uint32_t a = (threadIdx.x & 15u) << (4 * (threadIdx.x >> 4)), b = C, r = 0;
 		for (int q = 0; q < 32; ++q) {
 			r ^= (a & 0x80000000u) ? b : 0u;
@@ -977,6 +977,21 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		lds[kFinC + threadIdx.x] = r;
 	}
 	__syncthreads();
+	return F;
+}
+
+// Finish the buffers idx(j), j in [0, n): thread t takes j = start + t +
+// 2*stride*k and j + stride (two buffers per pass, their loads issued
+// together).  k_xfin: the whole batch over the grid; k_xgf: a workgroup's own
+// buffers, then its share of the buffers spanning several workgroups' grabs.
+template <class Idx>
+__device__ __forceinline__ void xfin_buffers(const XParams& P, const uint32_t* lds, const XGeo& G, const XFin& F,
+                                             uint64_t n, uint64_t start, uint64_t stride, Idx idx) {
+	const DevTables* T = P.tabs;
+	const uint64_t per = F.per;
+	const uint32_t lgp = F.lgp, cbase = F.cbase;
+	const uint32_t* const agg = F.agg;
+	const uint32_t* s4 = lds + kFinS4;
 	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 	typedef __attribute__((address_space(1))) const u32x2 xg_u2;
 	// Two buffers per thread per pass, their loads issued together: the pass
@@ -986,12 +1001,16 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		u32x2 cs, ce;
 		uint64_t P0, P1;
 		uint64_t ws, we;  // the units holding its start and end (set by units())
+		uint64_t i;       // the buffer
 		uint32_t sd;
 		bool ok;
 	};
-	auto load_in = [&](In& I, uint64_t i) {
-		I.ok = i < P.count;
-		const uint64_t ic = I.ok ? i : P.count - 1;
+	auto load_in = [&](In& I, uint64_t j) {
+		// (idx may return ~0: no buffer at j -- k_xshared's empty candidates)
+		const uint64_t ix = j < n ? idx(j) : ~0ull;
+		I.ok = ix < P.count;
+		const uint64_t ic = I.ok ? ix : 0;
+		I.i = ic;
 		// the captured point values do not depend on the metadata
 		I.cs = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.ps + 2 * ic));
 		I.ce = *((xg_u2*)reinterpret_cast<uintptr_t>(P.x.pe + 2 * ic));
@@ -1027,7 +1046,7 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 	};
 	// A buffer spanning units ws < we: the end point takes the aggregates of
 	// the units from ws to we - 1 (the start point's unit start is the origin)
-	// (a lane past the batch holds a clamped copy of the last buffer: it chains
+	// (a lane past the list holds a clamped copy of its last buffer: it chains
 	// nothing -- its result is discarded, and a huge last buffer's chain run by
 	// every idle lane of the grid took 14 ms for one 1.1 GB buffer)
 	auto units = [&](In& I) {
@@ -1085,18 +1104,212 @@ __global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
 		}
 		return lg;
 	};
-	const uint64_t span = (uint64_t)gridDim.x * blockDim.x;
-	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < P.count; i0 += 2 * span) {
+	for (uint64_t j0 = start; j0 < n; j0 += 2 * stride) {
 		In A, B;
-		load_in(A, i0 + threadIdx.x);
-		load_in(B, i0 + span + threadIdx.x);
+		load_in(A, j0 + threadIdx.x);
+		load_in(B, j0 + stride + threadIdx.x);
 		uint32_t Da, Db;
 		const bool la = long_chains(A, Da), lb = long_chains(B, Db);
 		const uint32_t ra = finish(A, la, Da);
 		const uint32_t rb = finish(B, lb, Db);
-		if (A.ok) P.out[i0 + threadIdx.x] = ra;
-		if (B.ok) P.out[i0 + span + threadIdx.x] = rb;
+		if (A.ok) P.out[A.i] = ra;
+		if (B.ok) P.out[B.i] = rb;
 	}
+}
+
+// The stream's next route choice: the count kernel's statistics (staged in
+// xhdr, kXStage) and this batch's back-off word (one thread).
+__device__ __forceinline__ void x_publish_stats(const XParams& P) {
+	const uint64_t* st = reinterpret_cast<const uint64_t*>(P.x.xhdr) + kXStage;
+	uint64_t v[kHstatPacked + 1];
+#pragma unroll
+	for (int k = 0; k <= kHstatPacked; ++k) v[k] = st[k];
+#pragma unroll
+	for (int k = 0; k <= kHstatPacked; ++k) P.hstat[k] = v[k];
+	P.hstat[kHstatXfail] = x_unordered(P) ? kXfailBackoff : 0;
+}
+
+// A batch that failed the packing check (x_fallback, slicing tables in LDS),
+// or whose buffers are all empty at one 16-byte-aligned address
+// (crc32c_append(seed, p, 0) == seed).
+__device__ __forceinline__ void x_unpacked(const XParams& P, uint32_t* lds) {
+	for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) lds[kFinS4 + k] = xld32(&P.tabs->slice4[0][0] + k);
+	__syncthreads();
+	x_fallback(P, lds + kFinS4);
+}
+__device__ __forceinline__ void x_all_empty(const XParams& P) {
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P.count; i += (uint64_t)gridDim.x * blockDim.x)
+		P.out[i] = P.seeds ? xld32(P.seeds + i) : P.seed;
+}
+
+__global__ __launch_bounds__(kFinThreads) void k_xfin(XParams P) {
+	__shared__ uint32_t lds[kFinWords];
+	const bool packed = x_packed(P);
+	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat) x_publish_stats(P);
+	if (!packed) {
+		x_unpacked(P, lds);
+		return;
+	}
+	// (x_start's one-round-trip form here holds the kernel's arguments in
+	// SGPRs across the pass: 5 SGPR spills)
+	const XGeo G = x_geo(P);
+	if (G.nblk == 0) {
+		x_all_empty(P);
+		return;
+	}
+	const XFin F = xfin_setup(P, lds, G);
+	xfin_buffers(P, lds, G, F, P.count, (uint64_t)blockIdx.x * blockDim.x, (uint64_t)gridDim.x * blockDim.x,
+	             [](uint64_t j) { return j; });
+}
+
+// ---------------------------------------------------------------------------
+// k_xgf: the grab stream and the finishing pass in one kernel.  Grid: one
+// 1024-thread workgroup per CU, as k_xgrab.  A workgroup that has streamed
+// its grabs (all its waves' points and aggregates stored) reloads its LDS with
+// the finishing tables and finishes the buffers whose END lies in its grabs
+// and whose start lies in them too -- those need nothing any other workgroup
+// wrote -- while other workgroups are still streaming (their stream ends
+// spread over ~30-50 us).  A buffer whose grabs belong to several workgroups
+// (the first buffer of a range when it starts in the range before, and the
+// first buffer of the extent's last grab, which workgroup 0 streams, when it
+// starts before that grab: at most one per workgroup) is left to k_xshared,
+// launched next, which finds the same buffers from the grab map and finishes
+// them after the kernel boundary has made every workgroup's stores visible.
+// (Finishing them in k_xgf behind per-workgroup flags measured ~60 us slower:
+// the agent-scope release / acquire each workgroup needs writes back and
+// invalidates its XCD's whole L2 while the other workgroups stream; by the
+// last workgroup to arrive, after a release per workgroup, ~5-15 us slower.
+// tools/probe_xftimes.py.)  Not the default: the own pass (~2.5 us of table
+// fill, ~7.5 us of finishing) lands on every workgroup's stream end, the
+// latest included, and k_xshared's chain of round trips costs ~13 us, so the
+// pair measured 0.2459-0.2470 ms per zipf step against k_xgrab + k_xfin's
+// 0.2326-0.2336 ms (same box).
+// ---------------------------------------------------------------------------
+static_assert(kFinWords + 16 <= kLdsBytesB / 4, "the finishing tables fit in the stream's LDS image");
+
+// The grab partition of k_xgf's grid (xgrab_stream's): grabs [g0, g1) of
+// workgroup b, the last grab nd streamed by workgroup 0.
+struct XParts {
+	uint32_t lgp, nd, gper;
+	__device__ __forceinline__ XParts(const XParams& P, const XGeo& G) {
+		const uint32_t nblk = (uint32_t)G.nblk;
+		const uint32_t gsz = (uint32_t)x_gsz(nblk, P.x.capg);
+		lgp = x_log2(gsz);
+		nd = (nblk + gsz - 1) / gsz - 1;
+		gper = (nd + (uint32_t)P.ngrid - 1) / (uint32_t)P.ngrid;
+	}
+	__device__ __forceinline__ void range(uint32_t b, uint32_t& g0, uint32_t& g1) const {
+		g0 = b * gper < nd ? b * gper : nd;
+		g1 = g0 + gper < nd ? g0 + gper : nd;
+	}
+	__device__ __forceinline__ uint32_t grab(uint64_t p) const { return x_blk(p) >> lgp; }  // p: bytes from S
+	__device__ __forceinline__ uint32_t owner(uint32_t g) const { return g >= nd ? 0u : g / gper; }
+};
+__device__ __forceinline__ uint32_t x_start_grab(const XParams& P, const XGeo& G, const XParts& X, uint32_t i) {
+	uint64_t a, b;
+	x_buffer(P, i, a, b);
+	return X.grab(a - G.S);
+}
+// The shared buffer of workgroup b (b < ngrid: the first buffer of its range
+// when it starts in an earlier workgroup's grabs) or of the last grab (b ==
+// ngrid: its first buffer when it starts before it), else ~0.  k_xgf's own
+// passes leave exactly these out.
+__device__ __forceinline__ uint64_t x_shared_of(const XParams& P, const XGeo& G, const XParts& X, uint32_t b) {
+	const uint32_t cnt32 = (uint32_t)P.count;
+	if (b < (uint32_t)P.ngrid) {
+		uint32_t g0, g1;
+		X.range(b, g0, g1);
+		if (g0 == 0 || g0 >= g1) return ~0ull;
+		const uint32_t lo = xld32(P.x.wq + g0), hi = xld32(P.x.wq + g1);
+		return lo < hi && X.owner(x_start_grab(P, G, X, lo)) != b ? lo : ~0ull;
+	}
+	if (X.nd == 0) return ~0ull;
+	const uint32_t c = xld32(P.x.wq + X.nd);
+	return c < cnt32 && x_start_grab(P, G, X, c) < X.nd ? c : ~0ull;
+}
+
+// The finishing phase of k_xgf (below): this workgroup's own buffers.
+__device__ __forceinline__ void xgf_finish(const XParams& P, const XGeo& G, uint32_t* lds) {
+	const XParts X(P, G);
+	uint32_t g0, g1;
+	X.range(blockIdx.x, g0, g1);
+	const uint32_t cnt32 = (uint32_t)P.count;
+#ifdef FDBX_TIMES
+	if (threadIdx.x == 0) g_xft[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
+	// the buffers whose end lies in this workgroup's grabs, [lo, hi) (wq[g]:
+	// the first buffer ending past grab g's start; buffer 0 may end at the
+	// extent's start), less the first when it starts in an earlier
+	// workgroup's grabs; in workgroup 0 also the last grab's [wq[nd], count),
+	// less its first when it starts before that grab
+	const uint32_t lo = g0 == 0 ? 0u : rdfirst(xld32(P.x.wq + g0));
+	const uint32_t hi = g0 < g1 ? rdfirst(xld32(P.x.wq + g1)) : lo;
+	const bool sh1 = lo < hi && g0 != 0 && X.owner(x_start_grab(P, G, X, lo)) != blockIdx.x;
+	const uint32_t a0 = lo + (sh1 ? 1u : 0u);
+	uint32_t b0 = cnt32;
+	if (blockIdx.x == 0) {
+		const uint32_t c = X.nd == 0 ? 0u : rdfirst(xld32(P.x.wq + X.nd));
+		b0 = c + (c < cnt32 && X.nd != 0 && x_start_grab(P, G, X, c) < X.nd ? 1u : 0u);
+	}
+	const XFin F = xfin_setup(P, lds, G);
+#ifdef FDBX_TIMES
+	if (threadIdx.x == 0) g_xft[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+#endif
+	xfin_buffers(P, lds, G, F, hi > a0 ? hi - a0 : 0u, 0, blockDim.x, [&](uint64_t j) { return a0 + j; });
+	if (blockIdx.x == 0)
+		xfin_buffers(P, lds, G, F, cnt32 > b0 ? cnt32 - b0 : 0u, 0, blockDim.x, [&](uint64_t j) { return b0 + j; });
+#ifdef FDBX_TIMES
+	if (threadIdx.x == 0) g_xft[blockIdx.x][3] = g_xft[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
+__global__ __launch_bounds__(1024) void k_xgf(XParams P) {
+#ifdef FDBX_TIMES
+	if (threadIdx.x == 0) g_xft[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+	__shared__ uint32_t lds[kLdsBytesB / 4];  // the stream's image, then the finishing tables
+	FillRegs fill;
+	fill_issue_1024(fill, P.tabs);
+	const XStart X0 = x_start(P);
+	if (blockIdx.x == 0 && threadIdx.x == 0 && P.hstat) x_publish_stats(P);
+	if (!X0.packed) {
+		x_unpacked(P, lds);
+		return;
+	}
+	if (X0.G.nblk == 0) {
+		x_all_empty(P);
+		return;
+	}
+	xgrab_stream(P, X0.G, fill, lds);
+	// The finishing phase reads its arguments again from the kernarg segment
+	// through an opaque pointer, so nothing it needs but the stream's own
+	// values is held in registers across the stream (held, they spilled: 85
+	// SGPRs into VGPR lanes, and a VGPR to scratch inside the grab loop).
+#if defined(__HIP_DEVICE_COMPILE__)
+	typedef __attribute__((address_space(4))) const XParams KParams;
+	KParams* kp = (KParams*)(__builtin_amdgcn_kernarg_segment_ptr());
+	asm volatile("" : "+s"(kp));
+	XParams P2;
+	__builtin_memcpy(&P2, (const XParams*)kp, sizeof(XParams));
+	xgf_finish(P2, X0.G, lds);
+#endif
+}
+
+// The buffers k_xgf left out: those whose grabs belong to several
+// workgroups, one per workgroup at most (x_shared_of), finished after the
+// kernel boundary by one workgroup.
+__global__ __launch_bounds__(kFinThreads) void k_xshared(XParams P) {
+	__shared__ uint32_t lds[kFinWords];
+	if (!x_packed(P)) return;  // (k_xgf checksummed the batch buffer by buffer)
+	const XGeo G = x_geo(P);
+	if (G.nblk == 0) return;
+	const XParts X(P, G);
+	const uint32_t nb = (uint32_t)P.ngrid + 1;
+	// (the grid has fewer than kFinThreads workgroups: one candidate per thread)
+	const uint64_t mine = threadIdx.x < nb ? x_shared_of(P, G, X, threadIdx.x) : ~0ull;
+	if (!__syncthreads_or(mine != ~0ull)) return;
+	const XFin F = xfin_setup(P, lds, G);
+	xfin_buffers(P, lds, G, F, nb, 0, blockDim.x, [&](uint64_t j) { return j == threadIdx.x ? mine : ~0ull; });
 }
 
 // ---------------------------------------------------------------------------
@@ -1128,6 +1341,20 @@ void extent_state_carve(void* mem, uint64_t count, uint64_t capg, int num_cus, X
 	x->capg = capg;
 }
 
+// The grab stream and the finishing pass in one kernel (k_xgf + k_xshared):
+// correct, measured slower than k_xgrab + k_xfin,
+// so off unless FDBX_FUSED=1 or fdbx_set_fused(1) (tests) turns it on.
+static int g_fused = -1;
+static bool extent_fused() {
+	if (__atomic_load_n(&g_fused, __ATOMIC_RELAXED) < 0) {
+		const char* e = getenv("FDBX_FUSED");
+		int expect = -1;
+		__atomic_compare_exchange_n(&g_fused, &expect, e && atoi(e) == 1 ? 1 : 0, false, __ATOMIC_RELAXED,
+		                            __ATOMIC_RELAXED);
+	}
+	return __atomic_load_n(&g_fused, __ATOMIC_RELAXED) == 1;
+}
+
 // phase 0: the streaming kernel; phase 1: the finishing kernel.  Both return
 // at once when the packing check failed.
 int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
@@ -1141,6 +1368,15 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 	P.nwave = (uint64_t)num_cus * 16;  // k_xstream: one 1024-thread workgroup per CU
 	P.ctr = xs.ctr;
 	P.grabs = xs.ctr != nullptr && xs.wq != nullptr;
+	P.ngrid = (uint64_t)num_cus;
+	if (num_cus + 1 > (int)kFinThreads) return -1;  // (k_xshared: one candidate per thread)
+	if (P.grabs && extent_fused()) {
+		if (phase == 0)
+			k_xgf<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+		else
+			k_xshared<<<1, kFinThreads, 0, stream>>>(P);
+		return 0;
+	}
 	if (phase == 0) {
 		if (P.grabs)
 			k_xgrab<<<(unsigned)num_cus, 1024, 0, stream>>>(P);
@@ -1156,8 +1392,19 @@ int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* 
 
 }  // namespace fdbcrc
 
+// Development / tests: select the extent route's fused kernels (1) or the
+// default pair (0) for later launches; returns the previous setting.
+extern "C" int fdbx_set_fused(int on) {
+	const int prev = fdbcrc::extent_fused() ? 1 : 0;
+	__atomic_store_n(&fdbcrc::g_fused, on ? 1 : 0, __ATOMIC_RELAXED);
+	return prev;
+}
+
 #ifdef FDBX_TIMES
 extern "C" int fdbx_debug_times(void* host, uint64_t nwave) {
 	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbcrc::g_xt), nwave * 32, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int fdbx_debug_ftimes(void* host, uint64_t nwg) {
+	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbcrc::g_xft), nwg * 64, 0, hipMemcpyDeviceToHost);
 }
 #endif

@@ -175,3 +175,57 @@ def schedule_grabs(P0, P1, gsz, order):
                     capture(k + j, k + j < gb1)
         flush()
     return vs, ve, blk, S, nblk
+
+
+def finish_plan(P0, P1, gsz, grid):
+    """Who finishes each buffer on the fused route (crc32c_extent.hip:
+    xgf_finish, x_shared_of), symbolic.  Workgroup b owns grabs [g0, g1)
+    (b * gper, clamped to nd = the last grab, which workgroup 0 streams).
+    k_xgf: each workgroup finishes the buffers whose end grab is its own --
+    [wq[g0], wq[g1]), buffer 0 from grab 0, and in workgroup 0 the last
+    grab's [wq[nd], n) -- except the first of a list when it starts in
+    another workgroup's grabs; k_xshared finishes those (x_shared_of).
+    Returns (fin, owners): fin[i] = list of ("own", b) / ("shared", b)
+    records, owners[i] = the workgroups holding buffer i's grabs."""
+    n = len(P0)
+    wq, S, nblk, ngrab = grab_map(P0, P1, gsz)
+    nd = ngrab - 1
+    gper = -(-nd // grid) if nd else 0
+
+    def grab(p):
+        return x_blk(p) // gsz
+
+    def owner(g):
+        return 0 if g >= nd else g // gper
+
+    def rng(b):
+        g0 = min(b * gper, nd)
+        return g0, min(g0 + gper, nd)
+
+    owners = [{owner(g) for g in range(grab(P0[i] - S), grab(P1[i] - S) + 1)} for i in range(n)]
+    fin = [[] for _ in range(n)]
+    for b in range(grid):  # k_xgf: own buffers
+        g0, g1 = rng(b)
+        lo = 0 if g0 == 0 else wq[g0]
+        hi = wq[g1] if g0 < g1 else lo
+        sh1 = lo < hi and g0 != 0 and owner(grab(P0[lo] - S)) != b
+        for i in range(lo + (1 if sh1 else 0), hi):
+            fin[i].append(("own", b))
+        if b == 0:
+            c = 0 if nd == 0 else wq[nd]
+            b0 = c + (1 if c < n and nd != 0 and grab(P0[c] - S) < nd else 0)
+            for i in range(b0, n):
+                fin[i].append(("own", b))
+    for b in range(grid + 1):  # k_xshared: x_shared_of(b)
+        if b < grid:
+            g0, g1 = rng(b)
+            if g0 == 0 or g0 >= g1:
+                continue
+            lo, hi = wq[g0], wq[g1]
+            if lo < hi and owner(grab(P0[lo] - S)) != b:
+                fin[lo].append(("shared", b))
+        elif nd:
+            c = wq[nd]
+            if c < n and grab(P0[c] - S) < nd:
+                fin[c].append(("shared", b))
+    return fin, owners

@@ -36,12 +36,13 @@ def sm_bytes(nbytes, state):
 
 def varlen_full(g):
     """BASELINE configs[2] (Zipf packets) and configs[4] (backup chunks) at their
-    exact bench shapes (bench_shapes.py): the reference's crc32c_append over
+    exact bench shapes (bench_shapes.py), and configs[2]'s packets scattered
+    (shuffled, non-ascending offsets: the window route's batch): the reference's crc32c_append over
     every buffer of each ~1 GiB batch, as xor/sum/sha256 digests plus the first 64
     checksums, for seeds 0 and 0xFDBEEFDB."""
     ref = O.reference()
     out = {}
-    for name in ("zipf", "chunks"):
+    for name in ("zipf", "chunks", "zipf-scattered"):
         lengths, offsets, extent = S.shape(name)
         data = O.splitmix64(extent // 8, S.STATE).view(np.uint8)
         ent = {"state": S.STATE, "count": int(lengths.size), "total_bytes": int(lengths.sum()),

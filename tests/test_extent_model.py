@@ -190,3 +190,41 @@ def test_grab_form_matches_oracle(gsz):
     want = O.batch_varlen(mem, np.array(offs, np.uint64), np.array(lens, np.uint64), seed=11)
     got = X.extent_crcs_ranges(mem, offs, lens, 11, None, per=gsz)
     assert np.array_equal(got, want)
+
+
+def _check_finish(P0, P1, gsz, grid):
+    from tests import extent_sched_model as M
+    fin, owners = M.finish_plan(P0, P1, gsz, grid)
+    for i, f in enumerate(fin):
+        assert len(f) == 1, ("every buffer finished exactly once", i, f, owners[i])
+        kind, b = f[0]
+        if kind == "own":  # k_xgf: only what its own grabs hold
+            assert owners[i] == {b}, (i, b, owners[i])
+        else:  # k_xshared: the buffers whose grabs several workgroups hold
+            assert len(owners[i]) > 1 or (b == grid and owners[i] == {0}), (i, b, owners[i])
+
+
+@pytest.mark.parametrize("grid", [1, 3, 8, 64])
+def test_fused_route_finishes_every_buffer_once(grid):
+    """k_xgf + k_xshared (crc32c_extent.hip): every buffer of a packed batch
+    is finished exactly once -- by the workgroup whose grabs hold all of its
+    points and the aggregates between them, inside k_xgf, or, when its grabs
+    belong to several workgroups (range boundaries, long buffers over many
+    ranges, the extent's last grab), by k_xshared after the kernel boundary."""
+    rng = np.random.default_rng(500 + grid)
+    for trial in range(10):
+        P0, P1, pos = [], [], int(rng.integers(0, 4096))
+        n = int(rng.integers(1, 500))
+        kind = trial % 5
+        for _ in range(n):
+            L = int({0: rng.integers(1, 3000), 1: rng.integers(0, 20000), 2: rng.choice([0, 1, 64, 4096, 32768]),
+                     3: rng.integers(2000, 70000), 4: rng.choice([100, 300000])}[kind])
+            g = int(rng.integers(0, min(max(L, 256), 4095) + 1)) if trial % 3 else 0
+            P0.append(pos)
+            P1.append(pos + L)
+            pos += L + g
+        for gsz in (8, 16):
+            _check_finish(P0, P1, gsz, grid)
+    _check_finish([0], [1 << 22], 8, grid)
+    _check_finish([0, 0], [0, 5], 8, grid)
+    _check_finish([7], [7], 8, grid)

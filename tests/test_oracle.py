@@ -106,7 +106,8 @@ def test_digest_pins_catch_compensating_errors(golden, oracle_mod):
     # every full-size entry carries the array hash
     for e in (golden["pages_full"]["digests"] + [golden["pages_full"]["digest_8k_fdbeefdb"]] +
               golden["pages_shards"]["pages4k"] + golden["pages_shards"]["pages8k"] +
-              golden["varlen_full"]["zipf"]["digests"] + golden["varlen_full"]["chunks"]["digests"]):
+              golden["varlen_full"]["zipf"]["digests"] + golden["varlen_full"]["chunks"]["digests"] +
+              golden["varlen_full"]["zipf-scattered"]["digests"]):
         assert len(e["sha256"]) == 64
 
 
@@ -143,7 +144,7 @@ def test_oracle_matches_compiled_reference_random():
         assert O.crc32c(s, buf[off:off + n]) == ref.append(s, buf[off:off + n])
 
 
-@pytest.mark.parametrize("name", ["zipf", "chunks"])
+@pytest.mark.parametrize("name", ["zipf", "chunks", "zipf-scattered"])
 def test_oracle_varlen_configs_exact_batches(oracle_mod, golden, name):
     """The oracle reproduces the reference's digests of the exact configs[2] /
     configs[4] batches (and the shape generator still yields the pinned list)."""
