@@ -912,6 +912,22 @@ struct Tab7 {
 // A slot whose chunks all hold its buffer's own bytes needs no masking.
 __device__ __forceinline__ bool slot_edge(uint32_t f) { return f & k7_LO; }
 
+// The kernel's arguments read again from the kernarg segment through an
+// opaque pointer: s_load at the use (scalar cache, lgkmcnt -- never waits for
+// the block loads in flight), so fields used once per 64-buffer batch or per
+// table are not held in SGPRs across the whole pass loop (held, they spilled:
+// 24 SGPRs into VGPR lanes).
+typedef __attribute__((address_space(4))) const V7Params KV7;
+__device__ __forceinline__ KV7* v7_kargs() {
+#if defined(__HIP_DEVICE_COMPILE__)
+	KV7* kp = (KV7*)__builtin_amdgcn_kernarg_segment_ptr();
+	asm volatile("" : "+s"(kp));
+	return kp;
+#else
+	return nullptr;
+#endif
+}
+
 __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	constexpr uint32_t kTS = kV7TabSlots;  // slots per table
 	__shared__ uint32_t lds[kLdsBytesB / 4];
@@ -968,18 +984,25 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	uint64_t pf_off = 0, pf_len = 0;
 	uint32_t pf_g = 0, pf_cl = 0;
 	auto prefetch = [&](uint64_t bi0) {  // unconditional, clamped into the batch
-		const uint64_t j = bi0 + lane < P.count ? bi0 + lane : P.count - 1;
-		v7_buffer(P, j, pf_off, pf_len);
-		pf_g = gld32(P.gs + j);
-		pf_cl = gld32(P.cl + j);
+		KV7* kp = v7_kargs();
+		const uint64_t cnt = kp->count;
+		const uint64_t j = bi0 + lane < cnt ? bi0 + lane : cnt - 1;
+		const uint64_t* const offs = kp->offsets;
+		const uint64_t* const lens = kp->lengths;
+		pf_off = offs ? offs[j] : j * kp->stride;
+		pf_len = lens ? lens[j] : kp->length;
+		pf_g = gld32(kp->gs + j);
+		pf_cl = gld32(kp->cl + j);
 	};
 	auto build = [&]() {
+		KV7* kp = v7_kargs();
+		const uint64_t cnt = kp->count;
 		const uint64_t bi0 = nb_bi0;
 		const uint64_t j = bi0 + lane;
-		const bool ok = j < P.count;
+		const bool ok = j < cnt;
 		const uint64_t off = pf_off, len = ok ? pf_len : 0;
 		const uint32_t g = ok ? pf_g : 0xFFFFFFFFu, cl = ok ? pf_cl : 0u;
-		const Geo7 ge = geo7(reinterpret_cast<uint64_t>(P.base) + off, len, P.bigmin);
+		const Geo7 ge = geo7(reinterpret_cast<uint64_t>(kp->base) + off, len, kp->bigmin);
 		const uint32_t W = ok ? ge.W : 0u;
 		B_bi0 = bi0;
 		B_wb = ge.A - ge.lo;
@@ -991,15 +1014,15 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		// where that window is masked anyway (k7_INJ)
 		B_cl = cl;
 		nb_bi0 = bi0 + 64;
-		prefetch(nb_bi0 < P.count ? nb_bi0 : bi0);
+		prefetch(nb_bi0 < cnt ? nb_bi0 : bi0);
 		// end of the slots of this batch: g + W is non-decreasing over the
 		// batch's buffers (pieces are in order; W = 0 pieces add nothing), so it
 		// is the last buffer's
-		const uint64_t nv = P.count - bi0;
+		const uint64_t nv = cnt - bi0;
 		const uint32_t emax = rdlane(g + W, nv < 64 ? (int)nv - 1 : 63);
 		Gb1 = (emax > hi_s ? hi_s : emax) - lo_s;
 		if (emax < lo_s) Gb1 = 0;
-		more = nb_bi0 < P.count && emax < hi_s;
+		more = nb_bi0 < cnt && emax < hi_s;
 	};
 	// slots [sb + k_lo, min(Gb1, sb + 64)) of the current batch into table lanes
 	auto expand = [&](Tab7& X, uint32_t sb, uint32_t k_lo) -> uint32_t {
@@ -1123,7 +1146,7 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 	auto phase1 = [&](Tab7& X, uint32_t filled) {
 		const uint32_t f = X.f;
 		const uint32_t d = (((f >> k7_KL) & 63u) - ((uint32_t)lane >> 2) * 4u) & 63u;
-		const uint32_t(*tab)[16] = T->slotw[d][(f >> k7_ZT) & 15u];
+		const uint32_t(*tab)[16] = v7_kargs()->tabs->slotw[d][(f >> k7_ZT) & 15u];
 		const uint32_t v = X.S;
 #pragma unroll
 		for (int n = 0; n < 8; ++n) gv[n] = gld32(&tab[n][(v >> (4 * n)) & 15u]);
@@ -1143,19 +1166,24 @@ __global__ __launch_bounds__(FDBCRC_V7_THREADS) void k_varlen7(V7Params P) {
 		const uint32_t kl0 = (f0 >> k7_KL) & 63u;
 		const bool fin0 = (f0 & k7_CONT) && (rdlane(f, (int)kl0) & k7_FIN);
 		uint32_t cc = 0;
-		if (carry) cc = umul(fin0 ? T->carryw[kl0][(f0 >> k7_ZT) & 15u] : T->table_shift, carry);
+		if (carry) {
+			const DevTables* Tk = v7_kargs()->tabs;
+			cc = umul(fin0 ? Tk->carryw[kl0][(f0 >> k7_ZT) & 15u] : Tk->table_shift, carry);
+		}
 		const bool fin = (f & k7_FIN) && (uint32_t)lane < pend_filled;
 		v ^= (cont && (fin || lane == (int)kTS - 1)) ? cc : 0u;
 		carry = (pend_filled == kTS && !(rdlane(f, kTS - 1) & k7_FIN)) ? rdlane(v, kTS - 1) : 0u;
 		const uint64_t pm = __ballot(fin && (f & k7_PEND));
 		if (pm) {  // the wave's last buffer continues in the next wave: shift its part to the buffer's end
 			const int k = __builtin_ctzll(pm);
-			const uint32_t vv = mul_xpow(T, rdlane(v, k), p_shift);
+			const uint32_t vv = mul_xpow(v7_kargs()->tabs, rdlane(v, k), p_shift);
 			v = lane == k ? vv : v;
 		}
 		// windowed buffers' out[] words are zeroed by the prep kernel; the part
 		// holding window 0 carries the final inversion
-		atomicXor(fin ? P.out + bi_w + X.oi : P.dummy + w * 64 + lane, fin ? ((f & k7_INV) ? ~v : v) : 0u);
+		KV7* kp = v7_kargs();
+		const uint64_t wd = (uint64_t)blockIdx.x * kV7RangesPerBlock + rdfirst(threadIdx.x >> 6);  // (w, not held)
+		atomicXor(fin ? kp->out + bi_w + X.oi : kp->dummy + wd * 64 + lane, fin ? ((f & k7_INV) ? ~v : v) : 0u);
 	};
 	// Two blocks in ping-pong (a register copy would wait for the loads in
 	// flight): pass p computes from one while pass p + 1 loads into the other.
