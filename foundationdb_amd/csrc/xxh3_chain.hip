@@ -9,11 +9,18 @@
 //
 //   k_seg_bsum / k_seg_bscan / k_seg_scan   exclusive prefix of the segment
 //                                           lengths (staging offsets)
-//   k_seg_gather                            one workgroup per segment copies
-//                                           it to its staging offset
 //   k_chain_ranges                          chain c = staging range
 //                                           [pre[starts[c]], pre[starts[c+1]])
+//                                           -- or, for a chain of 2..16
+//                                           segments and 241 B .. 1 MiB, a
+//                                           flag: hashed in place
+//   k_seg_gather                            the segments of the other chains
+//                                           of two or more, to their staging
+//                                           offsets
 //   launch_xxh3                             the varlen engine over the ranges
+//   launch_xxh3_segrows                     the flagged chains where their
+//                                           segments lie (xxh3_segrows.hip),
+//                                           over the varlen pass's empty digests
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -179,32 +186,39 @@ __global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ 
 // is hashed in place: its offset is taken relative to the staging area
 // (64-bit wrap-around: the kernels add it to the staging address), and its
 // segment is flagged so that the gather skips it.
+// A chain of 2 .. kSegRowsMax segments and 241 B .. kSegRowsMaxLen bytes is
+// hashed in place by the segment rows (chflag 2, its segments not gathered,
+// its varlen range empty: that digest is overwritten); shorter ones take the
+// closed forms from staging (a gather of at most 240 bytes), longer ones the
+// split route from staging.
 __global__ __launch_bounds__(256) void k_chain_ranges(const uint64_t* __restrict__ starts, uint64_t nchains,
                                                       uint64_t nsegs, const uint64_t* __restrict__ pre, uint64_t cap,
                                                       const uint8_t* __restrict__ base,
                                                       const uint64_t* __restrict__ seg_off,
                                                       const uint8_t* __restrict__ staging,
                                                       uint8_t* __restrict__ segflag, uint64_t* __restrict__ ch_off,
-                                                      uint64_t* __restrict__ ch_len) {
+                                                      uint64_t* __restrict__ ch_len, uint8_t* __restrict__ chflag) {
 	const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (c >= nchains) return;
 	uint64_t s0 = starts[c], s1 = starts[c + 1];
 	s0 = s0 < nsegs ? s0 : nsegs;
 	s1 = s1 < nsegs ? s1 : nsegs;
-	uint64_t a = pre[s0], b = pre[s1];
-	a = a < cap ? a : cap;
-	b = b < cap ? b : cap;
+	const uint64_t la = pre[s0], lb = pre[s1];  // (unclamped: the chain's true length)
+	uint64_t a = la < cap ? la : cap, b = lb < cap ? lb : cap;
 	const bool one = s1 == s0 + 1;
-	for (uint64_t j = s0; j < s1; ++j) segflag[j] = one ? 1 : 0;
+	const uint64_t L = lb > la ? lb - la : 0;
+	const bool rows = !one && s1 > s0 && s1 - s0 <= kSegRowsMax && L > 240 && L <= kSegRowsMaxLen;
+	for (uint64_t j = s0; j < s1; ++j) segflag[j] = one || rows ? 1 : 0;
 	ch_off[c] = one ? reinterpret_cast<uint64_t>(base) + seg_off[s0] - reinterpret_cast<uint64_t>(staging) : a;
-	ch_len[c] = b > a ? b - a : 0;
+	ch_len[c] = rows ? 0 : (b > a ? b - a : 0);
+	chflag[c] = rows ? 2 : 0;
 }
 
 static uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 
 uint64_t xxh3_chain_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes, uint64_t nwave) {
 	const uint64_t nb = nsegs / kScanSpan + 1;  // the scan covers nsegs + 1 entries (pre[nsegs] = total)
-	return al16(8 * (nb + 1)) + al16(8 * (nsegs + 1)) + 2 * al16(8 * nchains) + al16(nsegs + 1) +
+	return al16(8 * (nb + 1)) + al16(8 * (nsegs + 1)) + 2 * al16(8 * nchains) + al16(nsegs + 1) + al16(nchains) +
 	       al16(total_bytes + 16) +
 	       al16(xxh3_workspace_bytes_for(nchains ? nchains : 1, nwave, xxh3_long_blocks_bound(total_bytes)));
 }
@@ -224,6 +238,8 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	p += al16(8 * nchains);
 	uint8_t* segflag = p;
 	p += al16(nsegs + 1);
+	uint8_t* chflag = p;
+	p += al16(nchains);
 	uint8_t* staging = p;
 	p += al16(total_bytes + 16);
 	void* eng = p;
@@ -235,7 +251,7 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 		return -1;
 	}
 	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, nsegs, pre, total_bytes, base,
-	                                                                   seg_off, staging, segflag, ch_off, ch_len);
+	                                                                   seg_off, staging, segflag, ch_off, ch_len, chflag);
 	if (nsegs) {
 		const uint64_t g = (nsegs + 255) / 256;  // a wave per 64 segments
 		k_seg_gather<<<(unsigned)(g < 65536 ? g : 65536), 256, 0, s>>>(base, seg_off, seg_len, pre, segflag, nsegs,
@@ -251,7 +267,18 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	P.out = out;
 	P.ws_bytes = xxh3_workspace_bytes_for(nchains ? nchains : 1, (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock,
 	                                      xxh3_long_blocks_bound(total_bytes));
-	return launch_xxh3(P, num_cus, eng, s);
+	if (launch_xxh3(P, num_cus, eng, s)) return -1;
+	SegRowsP R{};
+	R.base = base;
+	R.seg_off = seg_off;
+	R.seg_len = seg_len;
+	R.starts = starts;
+	R.flag = chflag;
+	R.nchains = nchains;
+	R.seed = seed;
+	R.seeds = seeds;
+	R.out = out;
+	return launch_xxh3_segrows(R, num_cus, s);
 }
 
 }  // namespace fdbxxh

@@ -66,6 +66,22 @@ int launch_xxh3(const XxhParams& P, int num_cus, void* ws, hipStream_t stream);
 // Fixed-length (> 240 B, 16-byte aligned base and stride) pages over a device
 // list: buffer j = base + idx[j]*stride, j < *d_count; P.count bounds the grid.
 int launch_xxh3_pages_list(const XxhParams& P, int num_cus, hipStream_t stream);
+// Chains of segments hashed in place (xxh3_segrows.hip): one 16-lane row per
+// chain whose flag[c] is 2 (k_chain_ranges: two to kSegRowsMax segments,
+// 241 B to kSegRowsMaxLen bytes), the chain's segments read where they lie.
+constexpr uint32_t kSegRowsMax = 16;
+constexpr uint64_t kSegRowsMaxLen = 1ull << 20;
+struct SegRowsP {
+	const uint8_t* base;
+	const uint64_t* seg_off;
+	const uint64_t* seg_len;
+	const uint64_t* starts;
+	const uint8_t* flag;
+	uint64_t nchains, seed;
+	const uint64_t* seeds;
+	uint64_t* out;
+};
+int launch_xxh3_segrows(const SegRowsP& P, int num_cus, hipStream_t stream);
 // Chains of segments (xxh3_chain.hip): gather into a staging area, then varlen.
 uint64_t xxh3_chain_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes, uint64_t nwave);
 int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint64_t* seg_len, uint64_t nsegs,

@@ -320,6 +320,61 @@ def test_gpu_xxh3_chained_packet_buffers(cuda):
 
 
 @pytest.mark.gpu
+def test_gpu_xxh3_chained_in_place_rows(cuda):
+    """Chains of 2..16 segments and 241 B .. 1 MiB are hashed where their
+    segments lie (xxh3_segrows.hip), one 16-lane row per chain: segment ends
+    at every offset mod 16 and inside stripes, 1-byte segments, a segment
+    boundary inside the last stripe (len - 64), lengths at the 240 / 241,
+    1024 / 1025 and 1 MiB thresholds, 16 and 17 segments (the latter
+    gathered), uniform and per-chain seeds -- against the reference's own
+    flow/xxhash.c over each chain's concatenated bytes."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    rng = np.random.default_rng(2046)
+    h = O.splitmix64((48 << 20) // 8, 0x2046).view(np.uint8)
+    d = torch.from_numpy(h).to(cuda)
+    offs, lens, starts = [], [], [0]
+
+    def chain(parts):
+        for L in parts:
+            offs.append(int(rng.integers(0, h.size - max(L, 1) - 1)))
+            lens.append(int(L))
+        starts.append(len(offs))
+
+    for total in (241, 242, 255, 256, 257, 300, 1023, 1024, 1025, 1088, 2047, 2048, 2049, 4096, 16384, 65536,
+                  (1 << 20) - 1, 1 << 20, (1 << 20) + 1):
+        for ns in (2, 3, 16, 17):
+            if ns > total:
+                continue
+            cuts = np.sort(rng.choice(np.arange(1, total), ns - 1, replace=False))
+            chain(np.diff(np.concatenate([[0], cuts, [total]])))
+    for m in range(16):  # the boundary at every offset mod 16, inside the first block and inside the last stripe
+        chain([320 + m, 700])
+        chain([1000, 30 + m])
+        chain([1, 1, 1, 500 + m, 1])
+    for _ in range(400):  # PacketBuffer-like chains: a packet over 4 KiB buffers
+        L = int(rng.integers(241, 16385))
+        first = int(rng.integers(1, 4097))
+        parts = [min(first, L)]
+        while sum(parts) < L:
+            parts.append(min(4096, L - sum(parts)))
+        chain(parts)
+    cat = lambda c: b"".join(h[o:o + l].tobytes() for o, l in zip(offs[starts[c]:starts[c + 1]], lens[starts[c]:starts[c + 1]]))
+    t = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device=cuda)
+    nc = len(starts) - 1
+    got = X.batch_chained(d, t(offs), t(lens), t(starts)).cpu().numpy().view(np.uint64)
+    want = np.array([O.ref_xxh3_64(cat(c)) for c in range(nc)], dtype=np.uint64)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(c), len(cat(c)), int(starts[c + 1] - starts[c])) for c in bad[:8]]
+    seeds = rng.integers(0, 2**63, nc, dtype=np.int64)
+    got = X.batch_chained(d, t(offs), t(lens), t(starts), seeds=torch.from_numpy(seeds).to(cuda)).cpu().numpy().view(np.uint64)
+    want = np.array([O.ref_xxh3_64(cat(c), int(seeds[c])) for c in range(nc)], dtype=np.uint64)
+    assert np.array_equal(got, want)
+    got = X.batch_chained(d, t(offs), t(lens), t(starts), seed=0xFDBEEFDB).cpu().numpy().view(np.uint64)
+    assert all(int(got[c]) == O.ref_xxh3_64(cat(c), 0xFDBEEFDB) for c in range(0, nc, 5))
+
+
+@pytest.mark.gpu
 def test_gpu_xxh3_chained_underestimated_total(cuda):
     """A total_bytes below the real sum of the segment lengths (caller error):
     the digests are undefined but every read stays inside the workspace
