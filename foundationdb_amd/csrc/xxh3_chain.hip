@@ -186,18 +186,17 @@ __global__ __launch_bounds__(256) void k_seg_gather(const uint8_t* __restrict__ 
 // is hashed in place: its offset is taken relative to the staging area
 // (64-bit wrap-around: the kernels add it to the staging address), and its
 // segment is flagged so that the gather skips it.
-// A chain of 2 .. kSegRowsMax segments and 241 B .. kSegRowsMaxLen bytes is
-// hashed in place by the segment rows (chflag 2, its segments not gathered,
-// its varlen range empty: that digest is overwritten); shorter ones take the
-// closed forms from staging (a gather of at most 240 bytes), longer ones the
-// split route from staging.
+// With the segment rows on (rows_on), a chain of 2 .. kSegRowsMax segments
+// and 241 B .. kSegRowsMaxLen bytes is hashed in place by them (chflag 2, its
+// segments not gathered, its varlen range empty: that digest is overwritten);
+// every other multi-segment chain is hashed from staging.
 __global__ __launch_bounds__(256) void k_chain_ranges(const uint64_t* __restrict__ starts, uint64_t nchains,
                                                       uint64_t nsegs, const uint64_t* __restrict__ pre, uint64_t cap,
                                                       const uint8_t* __restrict__ base,
                                                       const uint64_t* __restrict__ seg_off,
                                                       const uint8_t* __restrict__ staging,
                                                       uint8_t* __restrict__ segflag, uint64_t* __restrict__ ch_off,
-                                                      uint64_t* __restrict__ ch_len, uint8_t* __restrict__ chflag) {
+                                                      uint64_t* __restrict__ ch_len, uint8_t* __restrict__ chflag, int rows_on) {
 	const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (c >= nchains) return;
 	uint64_t s0 = starts[c], s1 = starts[c + 1];
@@ -207,11 +206,26 @@ __global__ __launch_bounds__(256) void k_chain_ranges(const uint64_t* __restrict
 	uint64_t a = la < cap ? la : cap, b = lb < cap ? lb : cap;
 	const bool one = s1 == s0 + 1;
 	const uint64_t L = lb > la ? lb - la : 0;
-	const bool rows = !one && s1 > s0 && s1 - s0 <= kSegRowsMax && L > 240 && L <= kSegRowsMaxLen;
+	const bool rows = rows_on && !one && s1 > s0 && s1 - s0 <= kSegRowsMax && L > 240 && L <= kSegRowsMaxLen;
 	for (uint64_t j = s0; j < s1; ++j) segflag[j] = one || rows ? 1 : 0;
 	ch_off[c] = one ? reinterpret_cast<uint64_t>(base) + seg_off[s0] - reinterpret_cast<uint64_t>(staging) : a;
 	ch_len[c] = rows ? 0 : (b > a ? b - a : 0);
 	chflag[c] = rows ? 2 : 0;
+}
+
+// The segment rows read each byte once where the gather route reads it
+// three times, but measured slower on the bench's PacketBuffer-like chains
+// (latency-bound at 2 waves per SIMD), so they are
+// off unless FDBXXH_SEGROWS=1 or fdbxxh_set_segrows(1) (tests) turns them on.
+static int g_segrows = -1;
+static bool segrows_on() {
+	if (__atomic_load_n(&g_segrows, __ATOMIC_RELAXED) < 0) {
+		const char* e = getenv("FDBXXH_SEGROWS");
+		int expect = -1;
+		__atomic_compare_exchange_n(&g_segrows, &expect, e && atoi(e) == 1 ? 1 : 0, false, __ATOMIC_RELAXED,
+		                            __ATOMIC_RELAXED);
+	}
+	return __atomic_load_n(&g_segrows, __ATOMIC_RELAXED) == 1;
 }
 
 static uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
@@ -250,8 +264,10 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	} else if (hipMemsetAsync(pre, 0, 8, s) != hipSuccess) {
 		return -1;
 	}
+	const bool rows_on = segrows_on();
 	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, nsegs, pre, total_bytes, base,
-	                                                                   seg_off, staging, segflag, ch_off, ch_len, chflag);
+	                                                                   seg_off, staging, segflag, ch_off, ch_len, chflag,
+	                                                                   rows_on ? 1 : 0);
 	if (nsegs) {
 		const uint64_t g = (nsegs + 255) / 256;  // a wave per 64 segments
 		k_seg_gather<<<(unsigned)(g < 65536 ? g : 65536), 256, 0, s>>>(base, seg_off, seg_len, pre, segflag, nsegs,
@@ -268,6 +284,7 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	P.ws_bytes = xxh3_workspace_bytes_for(nchains ? nchains : 1, (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock,
 	                                      xxh3_long_blocks_bound(total_bytes));
 	if (launch_xxh3(P, num_cus, eng, s)) return -1;
+	if (!rows_on) return 0;
 	SegRowsP R{};
 	R.base = base;
 	R.seg_off = seg_off;
@@ -282,3 +299,11 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 }
 
 }  // namespace fdbxxh
+
+// Development / tests: hash qualifying multi-segment chains in place (1) or
+// all from staging (0) in later calls; returns the previous setting.
+extern "C" int fdbxxh_set_segrows(int on) {
+	const int prev = fdbxxh::segrows_on() ? 1 : 0;
+	__atomic_store_n(&fdbxxh::g_segrows, on ? 1 : 0, __ATOMIC_RELAXED);
+	return prev;
+}

@@ -320,9 +320,12 @@ def test_gpu_xxh3_chained_packet_buffers(cuda):
 
 
 @pytest.mark.gpu
-def test_gpu_xxh3_chained_in_place_rows(cuda):
-    """Chains of 2..16 segments and 241 B .. 1 MiB are hashed where their
-    segments lie (xxh3_segrows.hip), one 16-lane row per chain: segment ends
+@pytest.mark.parametrize("rows", [1, 0])
+def test_gpu_xxh3_chained_in_place_rows(cuda, rows):
+    """With the segment rows on (opt-in: fdbxxh_set_segrows),
+    chains of 2..16 segments and 241 B .. 1 MiB are hashed where their
+    segments lie (xxh3_segrows.hip), one 16-lane row per chain; off (the
+    default), the same chains through staging.  Segment ends
     at every offset mod 16 and inside stripes, 1-byte segments, a segment
     boundary inside the last stripe (len - 64), lengths at the 240 / 241,
     1024 / 1025 and 1 MiB thresholds, 16 and 17 segments (the latter
@@ -330,6 +333,17 @@ def test_gpu_xxh3_chained_in_place_rows(cuda):
     flow/xxhash.c over each chain's concatenated bytes."""
     import torch
     import foundationdb_amd.xxh3 as X
+    from foundationdb_amd import crc32c as F
+    L = F.lib()
+    prev = L.fdbxxh_set_segrows(rows)
+    try:
+        _chained_rows_case(cuda, X)
+    finally:
+        L.fdbxxh_set_segrows(prev)
+
+
+def _chained_rows_case(cuda, X):
+    import torch
     rng = np.random.default_rng(2046)
     h = O.splitmix64((48 << 20) // 8, 0x2046).view(np.uint8)
     d = torch.from_numpy(h).to(cuda)
