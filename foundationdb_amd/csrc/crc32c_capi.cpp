@@ -49,6 +49,8 @@ struct StreamState {
 	void* xmem = nullptr;
 	uint64_t xcount = 0;            // buffers it holds
 	uint32_t xepoch = 0;            // launches on the extent route (epoch tags, never 0)
+	// the prep-free block route's part accumulators (kNPAccBytes, zero between launches)
+	uint32_t* bacc = nullptr;
 };
 
 struct DeviceState {
@@ -227,6 +229,26 @@ bool stream_extent(DeviceState* st, hipStream_t s, uint64_t count, XState* xs) {
 	return true;
 }
 
+// The prep-free block route's accumulators of `s` (caller holds the stream's
+// lock): allocated and zeroed on the stream at first use, left zero by every
+// launch.  nullptr: none (the route keeps its prep).
+uint32_t* stream_blocks_acc(DeviceState* st, hipStream_t s) {
+	StreamState* ss = stream_state(st, s);
+	if (!ss->bacc) {
+		void* m = nullptr;
+		if (hipMalloc(&m, kNPAccBytes) != hipSuccess) {
+			(void)hipGetLastError();
+			return nullptr;
+		}
+		if (hipMemsetAsync(m, 0, kNPAccBytes, s) != hipSuccess) {
+			(void)hipFree(m);
+			return nullptr;
+		}
+		ss->bacc = static_cast<uint32_t*>(m);
+	}
+	return ss->bacc;
+}
+
 int check_launch(const char* what) {
 	hipError_t e = hipGetLastError();
 	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, what, e);
@@ -324,6 +346,7 @@ int release_stream(hipStream_t stream) {
 	if (ss->aux) (void)hipFree(ss->aux);
 	if (ss->hst_h) (void)hipHostFree(ss->hst_h);
 	if (ss->xmem) (void)hipFree(ss->xmem);
+	if (ss->bacc) (void)hipFree(ss->bacc);
 	if (e != hipSuccess) return fail(FDB_CRC32C_EHIP, "hipStreamSynchronize(release)", e);
 	return 0;
 }
@@ -335,7 +358,8 @@ uint64_t stream_bytes(hipStream_t stream) {
 	auto it = st->streams.find(stream);
 	if (it == st->streams.end()) return 0;
 	return it->second->ws_bytes + it->second->ctr_bytes +
-	       (it->second->xmem ? extent_state_bytes(it->second->xcount, kXGrabCap, st->num_cus) : 0);
+	       (it->second->xmem ? extent_state_bytes(it->second->xcount, kXGrabCap, st->num_cus) : 0) +
+	       (it->second->bacc ? kNPAccBytes : 0);
 }
 
 // used by the host pipeline (crc32c_pipeline.cpp)
@@ -458,7 +482,7 @@ uint64_t crc32c_gpu_varlen_workspace_bytes(uint64_t count) {
 static int batch_varlen_impl(const void* d_base, const uint64_t* d_offsets, const uint64_t* d_lengths, uint64_t count,
                              uint32_t seed, const uint32_t* d_seeds, uint32_t* d_out, void* d_workspace,
                              uint64_t workspace_bytes, void* stream, int route, uint64_t* hstat,
-                             const XState* xs = nullptr) {
+                             const XState* xs = nullptr, uint32_t* bacc = nullptr, uint32_t* pctr = nullptr) {
 	if (count == 0) return 0;
 	if (!d_out || !d_offsets || !d_lengths)
 		return fail(FDB_CRC32C_EINVAL, "crc32c_gpu_batch_varlen: null pointer");
@@ -472,7 +496,7 @@ static int batch_varlen_impl(const void* d_base, const uint64_t* d_offsets, cons
 #endif
 	launch_varlen(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, seed, d_seeds, d_out, st->tables,
 	              st->num_cus, d_workspace, reinterpret_cast<hipStream_t>(stream), route, hstat,
-	              hstat ? reinterpret_cast<uint32_t*>(hstat + kHstatErr) : nullptr, xs);
+	              hstat ? reinterpret_cast<uint32_t*>(hstat + kHstatErr) : nullptr, xs, bacc, pctr);
 #ifdef FDBCRC_DEBUG
 	(void)hipDeviceSynchronize();
 	debug_report("batch_varlen");
@@ -506,8 +530,16 @@ int crc32c_gpu_batch_varlen(const void* d_base, const uint64_t* d_offsets, const
 	XState xs;
 	const bool ext = route == kRouteExtent && stream_extent(st, reinterpret_cast<hipStream_t>(stream), count, &xs);
 	if (route == kRouteExtent && !ext) route = kRouteWindows;
+	// the block route alone over a small enough batch: no prep (k_bigblocks
+	// plans its own blocks), with the stream's accumulators and grab counters
+	uint32_t* bacc = nullptr;
+	uint32_t* pctr = nullptr;
+	if (route == kRouteBlocks && count <= kNPMax && !capturing(reinterpret_cast<hipStream_t>(stream))) {
+		bacc = stream_blocks_acc(st, reinterpret_cast<hipStream_t>(stream));
+		if (bacc && page_counters(reinterpret_cast<hipStream_t>(stream), st->num_cus, &pctr)) pctr = nullptr;
+	}
 	return batch_varlen_impl(d_base, d_offsets, d_lengths, count, seed, d_seeds, d_out, ws, have, stream, route, hstat,
-	                         ext ? &xs : nullptr);
+	                         ext ? &xs : nullptr, bacc, pctr);
 }
 
 // ---- grouped chains ------------------------------------------------------------

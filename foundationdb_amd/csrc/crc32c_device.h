@@ -191,7 +191,7 @@ uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
                   hipStream_t stream, int route = kRouteBoth, uint64_t* hstat = nullptr, uint32_t* err = nullptr,
-                  const XState* xs = nullptr);
+                  const XState* xs = nullptr, uint32_t* bacc = nullptr, uint32_t* pctr = nullptr);
 inline const uint64_t* varlen_refused_word(const void* ws) { return static_cast<const uint64_t*>(ws) + 6; }
 // Fixed stride, any length/alignment (same engine, same workspace size as varlen).
 int launch_fixed_general(const uint8_t* base, uint64_t stride, uint64_t length, uint64_t count, uint32_t seed,
@@ -202,7 +202,8 @@ uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave);
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                    const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat,
-                   uint32_t* err = nullptr, const XState* xs = nullptr);
+                   uint32_t* err = nullptr, const XState* xs = nullptr, uint32_t* bacc = nullptr,
+                   uint32_t* pctr = nullptr);
 // The extent route's streaming and finishing kernels (crc32c_extent.hip),
 // launched by launch_varlen7 for kRouteExtent after the packing check.
 int launch_extent(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
@@ -233,9 +234,25 @@ struct BigParams {
 	const uint64_t* hdr;
 	const BigEnt* ent;
 	uint32_t* out;
-	uint32_t* ctr;  // kPageCtrWords per workgroup, zeroed by prep
+	uint32_t* ctr;  // kPageCtrWords per workgroup, zeroed by prep (prep-free form: by the previous launch)
 	const DevTables* tabs;
+	// Prep-free form (k_bigblocks<U, true>: the block route alone, lists of at
+	// most kNPMax buffers, 8 per thread): the batch's own metadata, read by
+	// every workgroup
+	const uint8_t* base;
+	const uint64_t* offsets;
+	const uint64_t* lengths;
+	uint64_t nbuf;
+	uint32_t seed;
+	const uint32_t* seeds;
+	uint32_t* acc;   // [kNPMax] parts' XORs, [kNPMax] blocks done (zero between launches), u64[4] statistics
+	BigEnt* priv;    // route entries of workgroup w's blocks at q + 2w (its sentinel included)
+	uint64_t* hstat;
+	uint32_t* err;
 };
+constexpr uint64_t kNPMax = 8192;
+constexpr uint64_t kNPAccBytes = 8 * kNPMax + 32;  // P.acc
+int launch_bigblocks_np(const BigParams& P, int num_cus, hipStream_t stream);
 constexpr uint64_t kBigMax = 1ull << 40;  // spans routed are below this (block index from the end < 2^28)
 int launch_bigblocks(const BigParams& P, int num_cus, hipStream_t stream);
 int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out, hipStream_t stream);

@@ -169,6 +169,15 @@ __device__ __forceinline__ uint32_t vmul_tab(const uint32_t (*tab)[16], uint32_t
 #ifdef FDBCRC_BTIMES
 // development: per-wave start / end timestamps of k_pages4k and k_bigblocks (s_memrealtime, 100 MHz)
 __device__ uint64_t g_bt[16384][4];
+__device__ uint64_t g_bt2[16384][4];  // prep-free start-up: after the scan's barrier, the entries' barrier, the first loads
+#define FDBCRC_BT2(k) \
+	{ \
+		const uint64_t tk = __builtin_amdgcn_s_memrealtime(); \
+		const uint32_t wk = blockIdx.x * 16 + (threadIdx.x >> 6); \
+		if ((threadIdx.x & 63) == 0) __hip_atomic_store(&g_bt2[wk][k], tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+	}
+#else
+#define FDBCRC_BT2(k)
 #endif
 #ifndef FDBCRC_STRIDED
 #define FDBCRC_STRIDED 0
@@ -388,7 +397,253 @@ __device__ __forceinline__ void chunk_slot(uint32_t o, uint32_t& ln, uint32_t& r
 	ln = 32 * ((o >> 4) & 1) + 16 * ((o >> 5) & 1) + ((o >> 6) & 15);
 	ri = ((o >> 11) & 1) | (((o >> 10) & 1) << 1);
 }
-template <int U>
+// ---- prep-free form: each workgroup plans its own blocks ------------------
+// The kernel's arguments re-read at their use from the kernarg segment (an
+// opaque pointer: the compiler cannot keep the values in SGPRs across the
+// stream loop, where they spilled)
+typedef __attribute__((address_space(4))) const BigParams KBig;
+__device__ __forceinline__ KBig* big_kargs() {
+#if defined(__HIP_DEVICE_COMPILE__)
+	KBig* kp = (KBig*)__builtin_amdgcn_kernarg_segment_ptr();
+	asm volatile("" : "+s"(kp));
+	return kp;
+#else
+	return nullptr;
+#endif
+}
+// Route geometry of one buffer on the block route alone: every buffer of 16
+// bytes or more, in 4 KiB blocks aligned to its 16-byte-rounded end (a span
+// of 1 TiB or more refuses the batch); shorter ones are finished byte by byte.
+struct NPGeo {
+	uint32_t nb;  // blocks (0: shorter than 16 bytes)
+	bool refuse;
+};
+__device__ __forceinline__ NPGeo np_geo(uint64_t P0, uint64_t len) {
+	NPGeo g;
+	const uint64_t E = (P0 + len + 15) & ~uint64_t(15), A = P0 & ~uint64_t(15);
+	const uint64_t span = E - A;
+	g.refuse = len >= 16 && span >= kBigMax;
+	g.nb = len >= 16 && !g.refuse ? (uint32_t)((span + 4095) >> 12) : 0u;
+	return g;
+}
+__device__ __forceinline__ BigEnt np_entry(uint64_t P0, uint64_t len, uint32_t nb, uint32_t s, uint32_t idx,
+                                           uint32_t seed) {
+	const uint64_t E = (P0 + len + 15) & ~uint64_t(15), A = P0 & ~uint64_t(15);
+	const uint32_t lo = (uint32_t)(4096ull * nb - (E - A));
+	BigEnt e;
+	e.E = E;
+	e.s = s;
+	e.idx = idx;
+	e.lot = (lo >> 4) | ((uint32_t)(P0 & 15) << 8) | ((uint32_t)(E - (P0 + len)) << 12);
+	e.sd = ~seed;
+	return e;
+}
+struct NPStart {
+	uint32_t count, nbig;  // blocks, entries
+	uint32_t qa, qlim;     // this workgroup's first entry, and its sentinel (the entry after its last)
+	uint32_t smallm;       // this thread's buffers (bit j: buffer t*m + j) shorter than 16 bytes
+	uint32_t m;            // buffers per thread
+	bool refused;
+};
+// LDS words used before the table fill (fill_commit_1024 writes wave w's
+// share of round r, words [4096 r + 256 w, + 256), only after its own reads):
+// round 0, wave w's first words: the hand-over (first entry, sentinel); wave
+// 0's words 16..47: workgroup 0's statistics; round 1: the scan's wave sums;
+// rounds 2-3: the batch's block counts.
+// A workgroup barrier for LDS only: the waves' LDS writes done, global memory
+// operations left in flight (__syncthreads' fence waits for them too); the
+// memory clobber keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+constexpr uint32_t kNPRing = 0;         // [128][6] route entries by q mod 128 (the waves' first windows)
+constexpr uint32_t kNPScratch = 1024;   // the scan's wave sums
+constexpr uint32_t kNPStats = 1088;     // u64 [4 waves][4]: workgroup 0's route statistics
+constexpr uint32_t kNPHand = 1200;      // first entry, sentinel
+constexpr uint32_t kNPBlocks = 8192;    // [8192] blocks per buffer
+constexpr uint32_t kNPGeo = 16384;      // [8192][3] E (2 words), lo | k0 | t: entries without reloads
+// Every workgroup sums the whole batch's block counts (thread t: buffers
+// [8t, 8t + 8), their metadata loaded at once), writes the route entries of
+// the buffers its own grab range [g0, g1) covers -- plus a sentinel entry
+// holding the first block after them -- into its part of P.priv, and hands
+// its first entry to its waves.  All of this runs before the table fill is
+// written to LDS (the table loads are in flight meanwhile).
+template <uint32_t C>
+__device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
+	typedef __attribute__((address_space(1))) const uint64_t g_u64;
+	auto gl64 = [](const uint64_t* p) -> uint64_t { return *((g_u64*)reinterpret_cast<uintptr_t>(p)); };
+	NPStart R;
+	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+	const uint64_t n = P.nbuf;  // (<= kNPMax = 8192: at most eight buffers per thread)
+	const uint32_t m = (uint32_t)((n + 1023) >> 10);
+	const uint64_t i0 = (uint64_t)t * m;
+	uint32_t* const nbl = lds + kNPBlocks;                                // [n] blocks per buffer
+	uint64_t* const sB = reinterpret_cast<uint64_t*>(lds + kNPScratch);  // [16] wave block sums
+	uint32_t* const sN = lds + kNPScratch + 32;                           // [16] wave entry sums
+	uint32_t* const sR = lds + kNPScratch + 48;                           // [16] wave refusals
+	uint64_t B = 0;
+	uint32_t N = 0, smallm = 0;
+	bool refuse = false;
+	for (uint32_t j0 = 0; j0 < m; j0 += 8) {
+		uint64_t o[8], l[8];
+#pragma unroll
+		for (uint32_t u = 0; u < 8; ++u) {
+			const uint64_t ic = j0 + u < m && i0 + j0 + u < n ? i0 + j0 + u : 0;
+			o[u] = gl64(P.offsets + ic);
+			l[u] = gl64(P.lengths + ic);
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < 8; ++u) {
+			if (j0 + u < m && i0 + j0 + u < n) {
+				const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + o[u];
+				const NPGeo g = np_geo(P0, l[u]);
+				nbl[i0 + j0 + u] = g.nb;
+				const BigEnt e = np_entry(P0, l[u], g.nb, 0u, 0u, 0u);
+				uint32_t* const gq = lds + kNPGeo + 3 * (uint32_t)(i0 + j0 + u);
+				gq[0] = (uint32_t)e.E;
+				gq[1] = (uint32_t)(e.E >> 32);
+				gq[2] = e.lot;
+				B += g.nb;
+				N += g.nb ? 1u : 0u;
+				refuse |= g.refuse;
+				smallm |= (g.nb == 0 && !g.refuse ? 1u : 0u) << (j0 + u);
+			}
+		}
+	}
+	FDBCRC_BT2(0)
+	uint64_t Bi = B;
+	uint32_t Ni = N;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint64_t vb = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(Bi >> 32), d) << 32) |
+		                    (uint32_t)__shfl_up((int)(uint32_t)Bi, d);
+		const uint32_t vn = (uint32_t)__shfl_up((int)Ni, d);
+		if (lane >= (uint32_t)d) {
+			Bi += vb;
+			Ni += vn;
+		}
+	}
+	const bool wref = __ballot(refuse) != 0;
+	if (lane == 63) {
+		sB[wv] = Bi;
+		sN[wv] = Ni;
+		sR[wv] = wref ? 1u : 0u;
+	}
+	__syncthreads();
+	FDBCRC_BT2(1)
+	uint64_t Bex = Bi - B, Btot = 0;
+	uint32_t Nex = Ni - N, Ntot = 0;
+	bool ref = false;
+	const uint32_t nw = blockDim.x >> 6;
+	for (uint32_t k = 0; k < nw; ++k) {
+		const uint64_t b = sB[k];
+		const uint32_t c = sN[k];
+		if (k < wv) {
+			Bex += b;
+			Nex += c;
+		}
+		Btot += b;
+		Ntot += c;
+		ref |= sR[k] != 0;
+	}
+	// 32-bit block and entry numbers, as the planner's
+	R.refused = ref || Btot >= 0xFFFFFFFFull;
+	R.count = R.refused ? 0u : (uint32_t)Btot;
+	R.nbig = Ntot;
+	R.smallm = smallm;
+	R.m = m;
+	R.qa = R.qlim = 0;
+	const uint32_t ngrab = (uint32_t)(((uint64_t)R.count + C - 1) / C);
+	const uint32_t per = (ngrab + gridDim.x - 1) / gridDim.x;
+	const uint32_t g0 = blockIdx.x * per, g1 = g0 + per < ngrab ? g0 + per : ngrab;
+	const uint64_t blo = (uint64_t)g0 * C;
+	const uint64_t bhi = g1 * (uint64_t)C < R.count ? g1 * (uint64_t)C : R.count;  // this workgroup's blocks [blo, bhi)
+	BigEnt* const priv = P.priv + 2 * blockIdx.x;
+	// an entry: to the ring (the first windows) and to this workgroup's part of
+	// P.priv (window moves, when its range holds more entries than a window)
+	auto put = [&](uint32_t q, const BigEnt& e) {
+		priv[q] = e;
+		uint32_t* const r = lds + kNPRing + 6 * (q & 127u);
+		r[0] = (uint32_t)e.E;
+		r[1] = (uint32_t)(e.E >> 32);
+		r[2] = e.s;
+		r[3] = e.idx;
+		r[4] = e.lot;
+		r[5] = e.sd;
+	};
+	if (!R.refused && g0 < g1 && Bex < bhi && Bex + B > blo) {
+		uint64_t sb = Bex;
+		uint32_t q = Nex;
+		for (uint32_t j = 0; j < m; ++j) {
+			const uint64_t i = i0 + j;
+			if (i >= n || sb >= bhi) break;
+			const uint32_t nb = nbl[i];
+			if (!nb) continue;
+			if (sb + nb > blo) {
+				const uint32_t* const gq = lds + kNPGeo + 3 * (uint32_t)i;
+				BigEnt e;
+				e.E = ((uint64_t)gq[1] << 32) | gq[0];
+				e.s = (uint32_t)sb;
+				e.idx = (uint32_t)i;
+				e.lot = gq[2];
+				e.sd = ~(P.seeds ? P.seeds[i] : P.seed);
+				put(q, e);
+				if (sb <= blo) lds[kNPHand] = q;  // holds the workgroup's first block
+				if (bhi <= sb + nb) {  // holds its last block: the sentinel follows
+					BigEnt z;
+					z.E = 0;
+					z.s = (uint32_t)(sb + nb);
+					z.idx = ~0u;
+					z.lot = 0;
+					z.sd = 0;
+					put(q + 1, z);
+					lds[kNPHand + 1] = q + 1;
+				}
+			}
+			sb += nb;
+			++q;
+		}
+	}
+	// workgroup 0: the route statistics of the first 256 buffers (v7_route_stats'
+	// classes and packing), one buffer per thread, into wave 0's own fill words
+	if (blockIdx.x == 0 && P.hstat && t < 256) {
+		const uint64_t i = t;
+		const bool ok = i < n;
+		const uint64_t off = ok ? P.offsets[i] : 0, len = ok ? P.lengths[i] : 0;
+		const bool nx = i + 1 < n;
+		const uint64_t on = nx ? P.offsets[i + 1] : 0;
+		const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + off;
+		const uint64_t span = ok && len >= 16 ? ((P0 + len + 15) & ~uint64_t(15)) - (P0 & ~uint64_t(15)) : 0;
+		const uint64_t e = off + len, gap = on - e;
+		uint64_t c[4] = {span > 128 && span < 4096 ? len : 0, span >= 4096 && span < 16384 ? len : 0,
+		                 span >= 16384 ? len : 0,
+		                 (ok && nx && !(on >= e && gap < 4096 && gap <= (len > 256 ? len : 256))) ? 1u : 0u};
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			for (int o = 32; o > 0; o >>= 1)
+				c[k] += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(c[k] >> 32), o) << 32) |
+				        (uint32_t)__shfl_xor((int)(uint32_t)c[k], o);
+		uint64_t* const s64 = reinterpret_cast<uint64_t*>(lds + kNPStats);
+		if (lane == 0)
+#pragma unroll
+			for (int k = 0; k < 4; ++k) s64[4 * wv + k] = c[k];
+	}
+	// LDS only: the entries' global stores stay in flight (waited for below
+	// only when this workgroup's windows will move and read them back)
+	lds_barrier();
+	FDBCRC_BT2(2)
+	R.qa = rdfirst(lds[kNPHand]);
+	R.qlim = rdfirst(lds[kNPHand + 1]);
+	if (R.qlim - R.qa >= 64 && !R.refused && g0 < g1) __syncthreads();  // (its fence: the stores have landed)
+	// parked in device memory beside the accumulators: the host-mapped words
+	// are written at the kernel's end, off the start-up's path
+	if (blockIdx.x == 0 && t == 0 && P.hstat) {
+		const uint64_t* const s64 = reinterpret_cast<const uint64_t*>(lds + kNPStats);
+		uint64_t* const park = reinterpret_cast<uint64_t*>(P.acc + 2 * kNPMax);
+		for (int k = 0; k < 4; ++k) park[k] = s64[k] + s64[4 + k] + s64[8 + k] + s64[12 + k];
+	}
+	return R;
+}
+
+template <int U, bool NP>
 __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 #ifdef FDBCRC_BTIMES
 	const uint64_t bt0 = __builtin_amdgcn_s_memrealtime();
@@ -401,14 +656,26 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	// entry search and the window load (dependent round trips) proceed
 	FillRegs fill;
 	fill_issue_1024(fill, P.tabs);
-	// (32-bit block, entry and grab numbers: the planner refuses batches of
-	// 2^32 - 1 or more blocks)
-	const uint32_t count = (uint32_t)rdfirst64(gl64(P.hdr + 2));  // blocks
-	if (count == 0) return;
-	const uint32_t nbig = (uint32_t)rdfirst64(gl64(P.hdr + 3));   // entries
 	constexpr uint32_t C = 2 * U;   // blocks per grab
 	constexpr uint32_t F = 64 / C;  // grabs per store group
 	__shared__ uint32_t lds[kLdsBytesB / 4];
+	// (32-bit block, entry and grab numbers: the planner refuses batches of
+	// 2^32 - 1 or more blocks)
+	NPStart S;
+	uint32_t count, nbig;
+	if (NP) {
+		S = np_start<C>(P, lds);
+		if (S.refused) {
+			if (blockIdx.x == 0 && threadIdx.x == 0 && P.err) *P.err = 1u;
+			return;
+		}
+		count = S.count;
+		nbig = S.nbig;
+	} else {
+		count = (uint32_t)rdfirst64(gl64(P.hdr + 2));  // blocks
+		if (count == 0) return;
+		nbig = (uint32_t)rdfirst64(gl64(P.hdr + 3));   // entries
+	}
 	const DevTables* __restrict__ T = P.tabs;
 	const LaneCtx c = make_ctx();
 	const uint32_t lane = (uint32_t)c.lane;
@@ -428,9 +695,20 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	uint32_t wj = 0;
 	uint32_t ws = 0, wI = 0, wL = 0, wS = 0, wend = 0;  // first block (~0: none), output index, lo | k0 | t, ~seed
 	uint64_t wE = 0;                                   // 16-byte-rounded end
+	// (prep-free: this workgroup's own entries, read past the L1 -- a line
+	// cached there by an earlier launch would be stale)
 	auto ent = [&](uint32_t q) -> BigEnt {
-		const uint64_t* w = reinterpret_cast<const uint64_t*>(P.ent + q);
-		const uint64_t w0 = gl64(w), w1 = gl64(w + 1), w2 = gl64(w + 2);
+		const uint64_t* w = reinterpret_cast<const uint64_t*>(NP ? big_kargs()->priv + 2 * blockIdx.x + q : P.ent + q);
+		uint64_t w0, w1, w2;
+		if (NP) {
+			w0 = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			w1 = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			w2 = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		} else {
+			w0 = gl64(w);
+			w1 = gl64(w + 1);
+			w2 = gl64(w + 2);
+		}
 		BigEnt e;
 		e.E = w0;
 		e.s = (uint32_t)w1;
@@ -439,20 +717,34 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		e.sd = (uint32_t)(w2 >> 32);
 		return e;
 	};
-	auto ent_s = [&](uint32_t q) -> uint32_t { return gl32(&P.ent[q].s); };
+	auto ent_s = [&](uint32_t q) -> uint32_t {
+		if (NP)
+			return __hip_atomic_load(&big_kargs()->priv[2 * blockIdx.x + q].s, __ATOMIC_RELAXED,
+			                         __HIP_MEMORY_SCOPE_AGENT);
+		return gl32(&P.ent[q].s);
+	};
+	// prep-free: entries past this workgroup's sentinel are never read
+	const uint32_t qtop = NP ? S.qlim : nbig - 1;
 	auto load_window = [&](uint32_t j0) {
 		const uint32_t q = j0 + lane;
-		const uint32_t qc = q < nbig ? q : nbig - 1;  // clamped: every load is unconditional
+		const uint32_t qc = q <= qtop ? q : qtop;  // clamped: every load is unconditional
 		const BigEnt e = ent(qc);
 		const uint32_t s = e.s;
 		wE = e.E;
 		wI = e.idx;
 		wL = e.lot;
 		wS = e.sd;
-		const uint32_t qe = (uint64_t)j0 + 64 < nbig ? j0 + 64 : nbig - 1;
-		const uint32_t se = ent_s(qe);
-		ws = q < nbig ? s : (q == nbig ? count : ~0u);
-		wend = (uint64_t)j0 + 64 < nbig ? rdfirst(se) : count;
+		if (NP) {  // entries qa .. qlim (the sentinel's first block closes the last one)
+			const uint32_t qe = (uint64_t)j0 + 64 <= qtop ? j0 + 64 : qtop;
+			const uint32_t se = ent_s(qe);
+			ws = q <= qtop ? s : ~0u;
+			wend = (uint64_t)j0 + 64 <= qtop ? rdfirst(se) : count;
+		} else {
+			const uint32_t qe = (uint64_t)j0 + 64 < nbig ? j0 + 64 : nbig - 1;
+			const uint32_t se = ent_s(qe);
+			ws = q < nbig ? s : (q == nbig ? count : ~0u);
+			wend = (uint64_t)j0 + 64 < nbig ? rdfirst(se) : count;
+		}
 		wj = j0;
 	};
 	// the entry holding block b: the last q with es[q] <= b (64-ary narrowing)
@@ -492,7 +784,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	// grabs live -- they spilled 113 SGPRs.)  A block's fields are read with
 	// v_readlane where it is loaded and checksummed.
 	struct Meta {
-		uint32_t alo, ahi, kt, ek, sd, idx;
+		uint32_t alo, ahi, kt, ek, sd, idx, nbt;  // (nbt: the buffer's blocks, prep-free form)
 	};
 	auto rd = [](uint32_t v, uint32_t j) { return rdlane(v, (int)j); };
 	// lane j (< C): block b0 + j (past the batch's last block: a duplicate
@@ -526,6 +818,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		M.ek = m == 0 ? lot & 0xFFFu : 0u;
 		M.sd = m == 0 ? sdv : 0u;
 		M.idx = b0 + j <= last ? ixv : ~0u;
+		M.nbt = sn - se;
 	};
 	auto meta_of = [&](uint32_t g, Meta& M) {
 		const uint64_t bf = (uint64_t)g * C;
@@ -539,6 +832,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 			M.ek = lo16;
 			M.sd = 0;
 			M.idx = ~0u;
+			M.nbt = 0;
 			return;
 		}
 		const uint32_t b0 = (uint32_t)bf;
@@ -618,7 +912,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		for (uint32_t j = 0; j < U; ++j) crc[j] ^= spill[j];
 	};
 
-	uint32_t mine = 0, mkt = 0, midx = ~0u;  // lane f*C + j: block j of the group's f-th grab
+	uint32_t mine = 0, mkt = 0, midx = ~0u, mnbt = 0;  // lane f*C + j: block j of the group's f-th grab
 	auto store = [&]() {
 		const uint32_t k = mkt & 0xFFFFFFFu, t = mkt >> 28;
 		uint32_t w = vmul_tab(T->bpow[0][k & 255u], mine);
@@ -626,15 +920,42 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 		if (__ballot(k >= (1u << 16))) w = vmul_tab(T->bpow[2][(k >> 16) & 255u], w);
 		if (__ballot(k >= (1u << 24))) w = vmul_tab(T->bpow[3][k >> 24], w);
 		w = vmul_tab(T->inv_z[t], w);
-		// segmented inclusive XOR over runs of equal output index
+		// segmented inclusive XOR over runs of equal output index (and, prep-free,
+		// the run's block count)
+		uint32_t nrun = 1;
 #pragma unroll
 		for (int d = 1; d < 64; d <<= 1) {
 			const uint32_t y = (uint32_t)__shfl_up((int)w, d);
 			const uint32_t yi = (uint32_t)__shfl_up((int)midx, d);
-			if ((int)lane >= d && yi == midx) w ^= y;
+			const uint32_t yn = NP ? (uint32_t)__shfl_up((int)nrun, d) : 0u;
+			if ((int)lane >= d && yi == midx) {
+				w ^= y;
+				nrun += yn;
+			}
 		}
 		const uint32_t ni = (uint32_t)__shfl_down((int)midx, 1);
-		if (midx != ~0u && (lane == 63 || ni != midx)) atomicXor(P.out + midx, w);
+		if (midx != ~0u && (lane == 63 || ni != midx)) {
+			if (!NP) {
+				atomicXor(P.out + midx, w);
+			} else {
+				// The part's XOR, performed (its return awaited) before its block
+				// count is added: the part whose count completes the buffer reads
+				// every part's XOR back, writes ~acc to out[] and leaves both words
+				// zero for the next launch.  (No out[] initialisation ahead of the
+				// stream: that took a kernel of its own.)
+				uint32_t* const acc = big_kargs()->acc + midx;
+				uint32_t* const cnt = acc + kNPMax;
+				const uint32_t old = atomicXor(acc, w);
+				asm volatile("" ::"v"(old));
+				const uint32_t done = atomicAdd(cnt, nrun) + nrun;
+				if (done == mnbt) {
+					const uint32_t v = atomicExch(acc, 0u);
+					atomicExch(cnt, 0u);
+					big_kargs()->out[midx] = ~v;
+				}
+
+			}
+		}
 		midx = ~0u;
 	};
 
@@ -647,23 +968,52 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	// grab A static (g0 + wi), then one request per grab, issued at its start
 	// and read at its middle (k_pages4k)
 	uint32_t gA = clampg(g0 + wi);
-	// One entry search per workgroup (wave 0; every wave searching put 16x the
-	// scattered entry loads at the kernel's start), handed to each wave in an
-	// LDS word of its OWN table-fill share: wave w reads it before its
-	// fill_commit overwrites it, so no wave's fill races another's read.  (The
-	// barrier's fence waits for the table loads in flight: they return during
-	// the search anyway.)
-	if (wi == 0) {
-		const uint32_t q = find(g0 * C < count ? (uint32_t)(g0 * C) : last);
-		if (lane < wpb) lds[kS4Off / 4 + 256 * lane] = q;  // (thread 64w's first fill word)
+	// prep-free: a workgroup without grabs (or a batch without blocks) streams
+	// nothing -- its window would hold no entry of its own
+	const bool run = !NP || (count > 0 && g0 < g1);
+	if (!NP) {
+		// One entry search per workgroup (wave 0; every wave searching put 16x the
+		// scattered entry loads at the kernel's start), handed to each wave in an
+		// LDS word of its OWN table-fill share: wave w reads it before its
+		// fill_commit overwrites it, so no wave's fill races another's read.  (The
+		// barrier's fence waits for the table loads in flight: they return during
+		// the search anyway.)
+		if (wi == 0) {
+			const uint32_t q = find(g0 * C < count ? (uint32_t)(g0 * C) : last);
+			if (lane < wpb) lds[kS4Off / 4 + 256 * lane] = q;  // (thread 64w's first fill word)
+		}
+		__syncthreads();
+		load_window(rdfirst(lds[kS4Off / 4 + 256 * wi]));
+	} else if (run) {
+		if (S.qlim - S.qa < 64) {
+			// the whole range fits one window: from the LDS ring, and it never
+			// moves (no round trip)
+			const uint32_t q = S.qa + lane, qc = q <= S.qlim ? q : S.qlim;
+			const uint32_t* const r = lds + kNPRing + 6 * (qc & 127u);
+			wE = ((uint64_t)r[1] << 32) | r[0];
+			ws = q <= S.qlim ? r[2] : ~0u;
+			wI = r[3];
+			wL = r[4];
+			wS = r[5];
+			wend = count;
+			wj = S.qa;
+		} else {
+			load_window(S.qa);
+		}
+
 	}
-	__syncthreads();
-	load_window(rdfirst(lds[kS4Off / 4 + 256 * wi]));
 	Meta MA, MB;
-	meta_of(gA, MA);
 	Block u0[U], u1[U];
-	load_u(u0, MA, 0);  // in flight while the tables are written
+	if (run) {
+		meta_of(gA, MA);
+		load_u(u0, MA, 0);  // in flight while the tables are written
+	}
+	FDBCRC_BT2(3)
+	if (NP) lds_barrier();  // every wave has read the ring before any table word overwrites it
 	fill_commit_1024(fill, lds);
+#ifdef FDBCRC_BTIMES
+	const uint64_t bt1 = __builtin_amdgcn_s_memrealtime();
+#endif
 	uint32_t f = 0;
 	// one grab: X is its metadata; Y becomes the next grab's (its first unit
 	// is loaded here)
@@ -683,6 +1033,10 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 			const uint32_t ix = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)X.idx);
 			mkt = mine_grab ? kt : mkt;
 			midx = mine_grab ? ix : midx;
+			if (NP) {
+				const uint32_t nt = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)X.nbt);
+				mnbt = mine_grab ? nt : mnbt;
+			}
 		}
 		__builtin_amdgcn_sched_barrier(0);
 		const uint32_t gB = clampg(g0 + wpb + rdlane(req, 0));
@@ -701,19 +1055,50 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	};
 	// two grabs per iteration: the metadata registers swap roles instead of
 	// being copied
-	while (gA < ngrab) {
-		step(MA, MB);
-		if (gA >= ngrab) break;
-		step(MB, MA);
+	if (run) {
+		while (gA < ngrab) {
+			step(MA, MB);
+			if (gA >= ngrab) break;
+			step(MB, MA);
+		}
+		if (f) store();
 	}
-	if (f) store();
 #ifdef FDBCRC_BTIMES
-	if (lane == 0) {
+	const uint64_t bt2 = __builtin_amdgcn_s_memrealtime();
+#endif
+	if (NP) {
+		// buffers shorter than 16 bytes, byte by byte (the 1-byte table of the
+		// LDS image), spread over the workgroups by index
+		KBig* const K = big_kargs();
+		const uint64_t i0 = (uint64_t)threadIdx.x * S.m;
+		for (uint32_t msk = S.smallm; msk;) {
+			const uint32_t j = (uint32_t)__builtin_ctz(msk);
+			msk &= msk - 1;
+			const uint64_t i = i0 + j;
+			if (i % gridDim.x != blockIdx.x) continue;
+			const uint8_t* b = K->base + K->offsets[i];
+			const uint32_t len = (uint32_t)K->lengths[i];
+			uint32_t r = ~(K->seeds ? K->seeds[i] : K->seed);
+			for (uint32_t k = 0; k < len; ++k)
+				r = (r >> 8) ^ lds_rd(lds, (0x10000u | (((r ^ ld1(b + k)) & 255u) << 8) | col4) + 128);
+			K->out[i] = ~r;
+		}
+		// the stream's route statistics for its next batch (v7_route_stats)
+		uint64_t* const hs = K->hstat;
+		if (blockIdx.x == 0 && threadIdx.x == 0 && hs) {
+			const uint64_t* const park = reinterpret_cast<const uint64_t*>(K->acc + 2 * kNPMax);
+			for (int k = 0; k < 3; ++k) hs[k] = park[k];
+			hs[kHstatPacked] = park[3] ? 0 : 1;
+			if (hs[kHstatXfail] > 0 && hs[kHstatXfail] <= kXfailBackoff) --hs[kHstatXfail];
+		}
+	}
+#ifdef FDBCRC_BTIMES
+	if (lane == 0) {  // start, stream end, stream start, kernel end (after the prep-free tail)
 		const uint32_t w = blockIdx.x * wpb + wi;
 		g_bt[w][0] = bt0;
-		g_bt[w][1] = __builtin_amdgcn_s_memrealtime();
-		g_bt[w][2] = g1 - g0;
-		g_bt[w][3] = ngrab;
+		g_bt[w][1] = bt2;
+		g_bt[w][2] = bt1;
+		g_bt[w][3] = __builtin_amdgcn_s_memrealtime();
 	}
 #endif
 	// every request of every wave has returned: the counter goes back to zero
@@ -725,7 +1110,13 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 int launch_bigblocks(const BigParams& P, int num_cus, hipStream_t stream) {
 	// the block count lives on the device: one workgroup per CU, waves
 	// without a grab leave at once
-	k_bigblocks<FDBCRC_PU><<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+	k_bigblocks<FDBCRC_PU, false><<<(unsigned)num_cus, 1024, 0, stream>>>(P);
+	return 0;
+}
+
+int launch_bigblocks_np(const BigParams& P, int num_cus, hipStream_t stream) {
+	if (P.nbuf == 0 || P.nbuf > kNPMax || !P.offsets || !P.lengths || !P.acc || !P.priv || !P.ctr) return -1;
+	k_bigblocks<FDBCRC_PU, true><<<(unsigned)num_cus, 1024, 0, stream>>>(P);
 	return 0;
 }
 
@@ -817,5 +1208,8 @@ int launch_fill_seeds(uint64_t count, uint32_t seed, const uint32_t* seeds, uint
 #ifdef FDBCRC_BTIMES
 extern "C" int fdbcrc_debug_btimes(void* host, uint64_t nwave) {
 	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbcrc::g_bt), nwave * 32, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int fdbcrc_debug_btimes2(void* host, uint64_t nwave) {
+	return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fdbcrc::g_bt2), nwave * 32, 0, hipMemcpyDeviceToHost);
 }
 #endif

@@ -1288,7 +1288,7 @@ uint64_t varlen7_workspace_bytes(uint64_t count, uint64_t nwave) {
 int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t stride,
                    uint64_t length, uint64_t count, uint32_t seed, const uint32_t* seeds, uint32_t* out,
                    const DevTables* tabs, int num_cus, void* ws, hipStream_t stream, int route, uint64_t* hstat,
-                   uint32_t* err, const XState* xs) {
+                   uint32_t* err, const XState* xs, uint32_t* bacc, uint32_t* pctr) {
 	const uint64_t grid = (uint64_t)num_cus;
 	const uint64_t nwave = grid * kV7RangesPerBlock;  // one slot range per wave
 	const uint64_t ntile = (count + kTileW - 1) / kTileW;
@@ -1357,6 +1357,31 @@ int launch_varlen7(const uint8_t* base, const uint64_t* offsets, const uint64_t*
 		              1);
 		return 0;
 	}
+	// The block route alone over a list batch of at most kNPMax buffers, with
+	// the stream's part accumulators: no prep, one kernel (k_bigblocks<U, true>
+	// plans its own blocks).  FDBCRC_NP=0 (development) keeps the prep.
+	static const bool np_env = [] {
+		const char* e = getenv("FDBCRC_NP");
+		return !(e && atoi(e) == 0);
+	}();
+	if (np_env && route == kRouteBlocks && P.bigmin && bacc && pctr && offsets && lengths && count <= kNPMax &&
+	    (uint64_t)num_cus <= 1024) {
+		BigParams B{};
+		B.out = out;
+		B.ctr = pctr;
+		B.tabs = tabs;
+		B.base = base;
+		B.offsets = offsets;
+		B.lengths = lengths;
+		B.nbuf = count;
+		B.seed = seed;
+		B.seeds = seeds;
+		B.acc = bacc;
+		B.priv = reinterpret_cast<BigEnt*>(al16(reinterpret_cast<uint64_t>(P.gs)));  // (the window route's area)
+		B.hstat = hstat;
+		B.err = err;
+		return launch_bigblocks_np(B, num_cus, stream);
+	}
 	if (!P.selfsum) k_v7count<<<(unsigned)ntile, 256, 0, stream>>>(P);
 	if (P.scanned)
 		k_scan<<<1, 1024, 0, stream>>>(P.tsum, ntile, wave_tile, nwave, P.hdr, 4, 4, P.bigmin ? P.bsum : nullptr,
@@ -1382,9 +1407,10 @@ uint64_t varlen_workspace_bytes(uint64_t count, uint64_t nwave) { return varlen7
 
 int launch_varlen(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, uint64_t count, uint32_t seed,
                   const uint32_t* seeds, uint32_t* out, const DevTables* tabs, int num_cus, void* ws,
-                  hipStream_t stream, int route, uint64_t* hstat, uint32_t* err, const XState* xs) {
+                  hipStream_t stream, int route, uint64_t* hstat, uint32_t* err, const XState* xs, uint32_t* bacc,
+                  uint32_t* pctr) {
 	return launch_varlen7(base, offsets, lengths, 0, 0, count, seed, seeds, out, tabs, num_cus, ws, stream, route,
-	                      hstat, err, xs);
+	                      hstat, err, xs, bacc, pctr);
 }
 
 // Fixed stride, any length and alignment: the same engine with metadata

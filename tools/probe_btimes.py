@@ -1,5 +1,6 @@
-"""Development: per-wave timestamps of the CRC extent stream kernel k_bigblocks
-(library built with -DFDBCRC_BTIMES, FDBCRC_LIB=...) on a configs batch."""
+"""Development: per-wave timestamps of the block-route kernel k_bigblocks
+(library built with -DFDBCRC_BTIMES, FDBCRC_LIB=...) on a configs batch: start,
+stream start (tables in LDS), stream end, kernel end."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -27,13 +28,19 @@ lib.fdbcrc_debug_btimes(t.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint64(nw))
 t = t.astype(np.int64)
 t0 = t[:, 0].min()
 st, end = (t[:, 0] - t0) / 100, (t[:, 1] - t0) / 100
+s1, fin = (t[:, 2] - t0) / 100, (t[:, 3] - t0) / 100
 pc = lambda a: " ".join(f"{np.percentile(a, q):6.1f}" for q in (0, 10, 50, 90, 99, 100))
 print(f"{name}: percentiles 0/10/50/90/99/100 (us)")
-print(" start", pc(st)); print(" end  ", pc(end)); print(" grabs/wave", pc(t[:, 2].astype(float)))
+print(" start       ", pc(st)); print(" stream start", pc(s1)); print(" stream end  ", pc(end)); print(" kernel end  ", pc(fin))
 wg_end = end.reshape(ncu, 16).max(1)
 wg_first = end.reshape(ncu, 16).min(1)
 print(" WG end (last wave)", pc(wg_end)); print(" WG first wave done", pc(wg_first))
-print(" WG range", t[0, 2], "grabs", t[0, 3])
+if hasattr(lib, "fdbcrc_debug_btimes2") and os.environ.get("FDBCRC_NP", "1") != "0":
+    t2 = np.zeros((nw, 4), dtype=np.uint64)
+    lib.fdbcrc_debug_btimes2(t2.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint64(nw))
+    t2 = (t2.astype(np.int64) - t0) / 100
+    for k, nm in enumerate(["metadata in", "scan barrier", "entries barrier", "first loads issued"]):
+        print(f" {nm:18s}", pc(t2[:, k]))
 for x in range(8):
     m = (np.arange(ncu) % 8) == x
     print(f"  xcd {x}: WG end median {np.median(wg_end[m]):.1f}")
