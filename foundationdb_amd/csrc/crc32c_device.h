@@ -250,7 +250,7 @@ struct BigParams {
 	uint64_t* hstat;
 	uint32_t* err;
 };
-constexpr uint64_t kNPMax = 8192;
+constexpr uint64_t kNPMax = 6144;  // (k_bigblocks<U, true> keeps 5 words per buffer in LDS before its table fill)
 constexpr uint64_t kNPAccBytes = 8 * kNPMax + 32;  // P.acc
 int launch_bigblocks_np(const BigParams& P, int num_cus, hipStream_t stream);
 constexpr uint64_t kBigMax = 1ull << 40;  // spans routed are below this (block index from the end < 2^28)

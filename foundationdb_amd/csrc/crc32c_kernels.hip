@@ -458,8 +458,10 @@ constexpr uint32_t kNPRing = 0;         // [128][6] route entries by q mod 128 (
 constexpr uint32_t kNPScratch = 1024;   // the scan's wave sums
 constexpr uint32_t kNPStats = 1088;     // u64 [4 waves][4]: workgroup 0's route statistics
 constexpr uint32_t kNPHand = 1200;      // first entry, sentinel
-constexpr uint32_t kNPBlocks = 8192;    // [8192] blocks per buffer
-constexpr uint32_t kNPGeo = 16384;      // [8192][3] E (2 words), lo | k0 | t: entries without reloads
+constexpr uint32_t kNPBlocks = 2048;    // [kNPMax] blocks per buffer
+constexpr uint32_t kNPGeo = kNPBlocks + kNPMax;  // [kNPMax][3] E (2 words), lo | k0 | t: entries without reloads
+constexpr uint32_t kNPSeed = kNPGeo + 3 * kNPMax;  // [kNPMax] ~seed
+static_assert(kNPSeed + kNPMax <= kLdsBytesB / 4, "prep-free start-up: its LDS scratch fits the table image");
 // Every workgroup sums the whole batch's block counts (thread t: buffers
 // [8t, 8t + 8), their metadata loaded at once), writes the route entries of
 // the buffers its own grab range [g0, g1) covers -- plus a sentinel entry
@@ -467,12 +469,12 @@ constexpr uint32_t kNPGeo = 16384;      // [8192][3] E (2 words), lo | k0 | t: e
 // its first entry to its waves.  All of this runs before the table fill is
 // written to LDS (the table loads are in flight meanwhile).
 template <uint32_t C>
-__device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
+__device__ NPStart np_start(const BigParams& P, uint32_t* lds, uint32_t ngrid) {
 	typedef __attribute__((address_space(1))) const uint64_t g_u64;
 	auto gl64 = [](const uint64_t* p) -> uint64_t { return *((g_u64*)reinterpret_cast<uintptr_t>(p)); };
 	NPStart R;
 	const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-	const uint64_t n = P.nbuf;  // (<= kNPMax = 8192: at most eight buffers per thread)
+	const uint64_t n = P.nbuf;  // (<= kNPMax = 6144: at most six buffers per thread)
 	const uint32_t m = (uint32_t)((n + 1023) >> 10);
 	const uint64_t i0 = (uint64_t)t * m;
 	uint32_t* const nbl = lds + kNPBlocks;                                // [n] blocks per buffer
@@ -484,11 +486,15 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
 	bool refuse = false;
 	for (uint32_t j0 = 0; j0 < m; j0 += 8) {
 		uint64_t o[8], l[8];
+		uint32_t sd[8];
 #pragma unroll
 		for (uint32_t u = 0; u < 8; ++u) {
 			const uint64_t ic = j0 + u < m && i0 + j0 + u < n ? i0 + j0 + u : 0;
 			o[u] = gl64(P.offsets + ic);
 			l[u] = gl64(P.lengths + ic);
+			// (per-buffer seeds loaded here, with the metadata: a load in the
+			// entry loop below made its join wait for the entries' stores)
+			sd[u] = P.seeds ? P.seeds[ic] : P.seed;
 		}
 #pragma unroll
 		for (uint32_t u = 0; u < 8; ++u) {
@@ -501,6 +507,7 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
 				gq[0] = (uint32_t)e.E;
 				gq[1] = (uint32_t)(e.E >> 32);
 				gq[2] = e.lot;
+				lds[kNPSeed + (uint32_t)(i0 + j0 + u)] = ~sd[u];
 				B += g.nb;
 				N += g.nb ? 1u : 0u;
 				refuse |= g.refuse;
@@ -532,7 +539,7 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
 	uint64_t Bex = Bi - B, Btot = 0;
 	uint32_t Nex = Ni - N, Ntot = 0;
 	bool ref = false;
-	const uint32_t nw = blockDim.x >> 6;
+	constexpr uint32_t nw = 16;  // (1024-thread workgroups: blockDim read from memory costs a round trip here)
 	for (uint32_t k = 0; k < nw; ++k) {
 		const uint64_t b = sB[k];
 		const uint32_t c = sN[k];
@@ -552,7 +559,7 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
 	R.m = m;
 	R.qa = R.qlim = 0;
 	const uint32_t ngrab = (uint32_t)(((uint64_t)R.count + C - 1) / C);
-	const uint32_t per = (ngrab + gridDim.x - 1) / gridDim.x;
+	const uint32_t per = (ngrab + ngrid - 1) / ngrid;
 	const uint32_t g0 = blockIdx.x * per, g1 = g0 + per < ngrab ? g0 + per : ngrab;
 	const uint64_t blo = (uint64_t)g0 * C;
 	const uint64_t bhi = g1 * (uint64_t)C < R.count ? g1 * (uint64_t)C : R.count;  // this workgroup's blocks [blo, bhi)
@@ -584,7 +591,7 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
 				e.s = (uint32_t)sb;
 				e.idx = (uint32_t)i;
 				e.lot = gq[2];
-				e.sd = ~(P.seeds ? P.seeds[i] : P.seed);
+				e.sd = lds[kNPSeed + (uint32_t)i];
 				put(q, e);
 				if (sb <= blo) lds[kNPHand] = q;  // holds the workgroup's first block
 				if (bhi <= sb + nb) {  // holds its last block: the sentinel follows
@@ -632,7 +639,10 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds) {
 	FDBCRC_BT2(2)
 	R.qa = rdfirst(lds[kNPHand]);
 	R.qlim = rdfirst(lds[kNPHand + 1]);
-	if (R.qlim - R.qa >= 64 && !R.refused && g0 < g1) __syncthreads();  // (its fence: the stores have landed)
+	if (R.qlim - R.qa >= 64 && !R.refused && g0 < g1) {  // (uniform)
+		__builtin_amdgcn_s_waitcnt(0);
+		__syncthreads();
+	}
 	// parked in device memory beside the accumulators: the host-mapped words
 	// are written at the kernel's end, off the start-up's path
 	if (blockIdx.x == 0 && t == 0 && P.hstat) {
@@ -654,6 +664,10 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	auto gl64 = [](const uint64_t* p) -> uint64_t { return *((g_u64*)reinterpret_cast<uintptr_t>(p)); };
 	// the LDS table loads go out first: they return while the header, the
 	// entry search and the window load (dependent round trips) proceed
+	// the grid size is a hidden kernel argument: read now, with the others (a
+	// scalar load where it is first used put a round trip into the planning)
+	const uint32_t ngrid = gridDim.x;
+	asm volatile("" ::"s"(ngrid));
 	FillRegs fill;
 	fill_issue_1024(fill, P.tabs);
 	constexpr uint32_t C = 2 * U;   // blocks per grab
@@ -664,7 +678,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	NPStart S;
 	uint32_t count, nbig;
 	if (NP) {
-		S = np_start<C>(P, lds);
+		S = np_start<C>(P, lds, ngrid);
 		if (S.refused) {
 			if (blockIdx.x == 0 && threadIdx.x == 0 && P.err) *P.err = 1u;
 			return;
@@ -682,10 +696,10 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 	const uint32_t col4 = (lane & 31) * 4;
 	const uint32_t c4 = col4 | 0x10000u;
 	const uint32_t c_lane = (kS4LaneOff + (lane >> 5) * 0x4000) | col4;
-	const uint32_t wpb = blockDim.x >> 6;
+	constexpr uint32_t wpb = 16;  // waves per workgroup (launched with 1024 threads)
 	const uint32_t wi = rdfirst(threadIdx.x >> 6);
 	const uint32_t ngrab = (uint32_t)(((uint64_t)count + C - 1) / C);
-	const uint32_t per = (ngrab + gridDim.x - 1) / gridDim.x;
+	const uint32_t per = (ngrab + ngrid - 1) / ngrid;
 	const uint32_t g0 = blockIdx.x * per;
 	const uint32_t g1 = g0 + per < ngrab ? g0 + per : ngrab;
 	uint32_t* const my_ctr = P.ctr + kPageCtrWords * blockIdx.x;
@@ -1075,7 +1089,7 @@ __global__ __launch_bounds__(1024) void k_bigblocks(BigParams P) {
 			const uint32_t j = (uint32_t)__builtin_ctz(msk);
 			msk &= msk - 1;
 			const uint64_t i = i0 + j;
-			if (i % gridDim.x != blockIdx.x) continue;
+			if (i % ngrid != blockIdx.x) continue;
 			const uint8_t* b = K->base + K->offsets[i];
 			const uint32_t len = (uint32_t)K->lengths[i];
 			uint32_t r = ~(K->seeds ? K->seeds[i] : K->seed);
