@@ -12,8 +12,16 @@ big = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
 F.fill_splitmix64(big, 0x5EED)
 out = torch.empty(n, dtype=torch.uint32, device=dev)
 out64 = torch.empty(n, dtype=torch.uint64, device=dev)
-VARLEN = ("chunks", "zipf", "v4096", "v1024", "xchunks", "xzipf")
-if mode in VARLEN:
+VARLEN = ("chunks", "zipf", "v4096", "v1024", "xchunks", "xzipf", "scattered")
+if mode == "scattered":  # the zipf-scattered bench line: the same packets, shuffled non-ascending offsets
+    import numpy as np
+    import bench_shapes as S
+    lens, offs_np, extent = S.shape("zipf-scattered")
+    assert extent <= big.numel()
+    offs = torch.from_numpy(offs_np.astype(np.int64)).to(dev)
+    lt = torch.from_numpy(lens.astype(np.int64)).to(dev)
+    vout = torch.empty(lens.size, dtype=torch.uint32, device=dev)
+elif mode in VARLEN:
     import numpy as np
     import bench_workloads as W
     lens = {"chunks": W.chunk_lengths, "zipf": W.zipf_lengths, "xchunks": W.chunk_lengths, "xzipf": W.zipf_lengths, "v4096": lambda: np.full(1 << 18, 4096),

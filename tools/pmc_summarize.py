@@ -103,6 +103,7 @@ PRESETS = {
     "chunks": ("chunks", "chunks", VARLEN_KERNELS, _varlen("chunk_lengths"), None),
     "xchunks": ("xchunks", "xxh3-chunks", XXH3_VARLEN_KERNELS, _varlen("chunk_lengths", 24), None),
     "xzipf": ("xzipf", "xxh3-zipf", XXH3_VARLEN_KERNELS, _varlen("zipf_lengths", 24), None),
+    "scattered": ("scattered", "zipf-scattered", VARLEN_KERNELS, _varlen("zipf_lengths"), None),
 }
 
 if __name__ == "__main__":

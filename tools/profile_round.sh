@@ -7,7 +7,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-ROUND=${ROUND:-round5}
+ROUND=${ROUND:-round6}
 R=gpurun_out/$ROUND
 P=gpurun_out/pmc
 mkdir -p $R $P
@@ -18,7 +18,7 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-me
 tail -1 $R/pytest_gpu.txt
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $R/smoke.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $R/bench_pages4k.json 2> $R/bench_pages4k.err || exit 1
-for w in pages8k zipf chunks chunks-host pages4k-host xxh3-pages4k xxh3-zipf xxh3-chunks xxh3-chained sqlite-verify sqlite-verify-host diskqueue-verify sqlite-seal diskqueue-seal packets-verify; do
+for w in pages8k zipf zipf-scattered chunks chunks-host pages4k-host xxh3-pages4k xxh3-zipf xxh3-chunks xxh3-chained sqlite-verify sqlite-verify-host diskqueue-verify sqlite-seal diskqueue-seal packets-verify redwood-verify redwood-seal; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --cpu-seconds 5 > $R/bench_$w.json 2> $R/bench_$w.err || { tail -3 $R/bench_$w.err; exit 1; }
 done
 echo benches done
@@ -31,11 +31,11 @@ for f in $R/bench_*.json; do echo "$f $(cut -c1-200 $f)"; done
 exit 0
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_pages4k -o pages4k -- python bench.py --cpu-seconds 0 > $R/prof_pages4k.log 2>&1 || exit 1
-for w in pages8k zipf chunks xxh3-pages4k xxh3-zipf xxh3-chunks xxh3-chained sqlite-verify diskqueue-verify sqlite-seal diskqueue-seal packets-verify; do
+for w in pages8k zipf zipf-scattered chunks xxh3-pages4k xxh3-zipf xxh3-chunks xxh3-chained sqlite-verify diskqueue-verify sqlite-seal diskqueue-seal packets-verify redwood-verify redwood-seal; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_$w -o $w -- python bench.py --workload $w --steps 20 --cpu-seconds 0 --no-verify > $R/prof_$w.log 2>&1 || exit 1
 done
 echo rocprof done
-for MODE in pages4k pages8k xxh3 zipf chunks xchunks xzipf; do
+for MODE in pages4k pages8k xxh3 zipf chunks xchunks xzipf scattered; do
   for spec in "fetch FETCH_SIZE" "write WRITE_SIZE" "sq GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD"; do
     set -- $spec; name=$1; shift
     timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $P/$MODE -o ${name}_$MODE -- python tools/pmc_probe.py $MODE > $P/$MODE.log 2>&1 || exit 1
