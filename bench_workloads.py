@@ -217,7 +217,8 @@ class VarLen:
         csum = np.cumsum(self.h_lengths)
         k = int(np.searchsorted(csum, 256 << 20)) + 1
         k = min(k, self.h_lengths.size)
-        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        # (the bytes up to the furthest of them: a scattered layout's offsets are not ascending)
+        end = int((self.h_offsets[:k] + self.h_lengths[:k]).max())
         buf = O.splitmix64((end + 7) // 8, STATE).view(np.uint8)
         return CpuSample(f"first {k} buffers ({int(csum[k - 1]) >> 20} MiB) of the same list", int(csum[k - 1]), buf,
                          offsets=self.h_offsets[:k].copy(), lengths=self.h_lengths[:k].copy(), seed=self.seed)
@@ -272,7 +273,7 @@ class HostChunks:
         from oracle import oracle as O
         csum = np.cumsum(self.h_lengths)
         k = min(int(np.searchsorted(csum, 256 << 20)) + 1, self.h_lengths.size)
-        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        end = int((self.h_offsets[:k] + self.h_lengths[:k]).max())
         buf = self.buf.numpy()[:end]
         return CpuSample(f"first {k} buffers ({int(csum[k - 1]) >> 20} MiB) of the same list", int(csum[k - 1]), buf,
                          offsets=self.h_offsets[:k].copy(), lengths=self.h_lengths[:k].copy(), seed=self.seed)
@@ -824,7 +825,7 @@ class Xxh3Zipf(VarLen):
     def cpu_sample(self):
         from oracle import oracle as O
         k = 120000
-        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        end = int((self.h_offsets[:k] + self.h_lengths[:k]).max())
         host = self.buf[:end].cpu().numpy()
         offs, lens = self.h_offsets[:k], self.h_lengths[:k]
         return CpuSample(f"first {k} packets ({int(lens.sum()) >> 20} MiB), reference flow/xxhash.c XXH3_64bits",
@@ -853,7 +854,7 @@ class Xxh3Chunks(Xxh3Zipf):
         from oracle import oracle as O
         csum = np.cumsum(self.h_lengths)
         k = min(int(np.searchsorted(csum, 256 << 20)) + 1, self.h_lengths.size)
-        end = int(self.h_offsets[k - 1] + self.h_lengths[k - 1])
+        end = int((self.h_offsets[:k] + self.h_lengths[:k]).max())
         host = self.buf[:end].cpu().numpy()
         offs, lens = self.h_offsets[:k], self.h_lengths[:k]
         return CpuSample(f"first {k} chunks ({int(lens.sum()) >> 20} MiB), reference flow/xxhash.c XXH3_64bits",
