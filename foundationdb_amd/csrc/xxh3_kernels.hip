@@ -549,8 +549,18 @@ __global__ __launch_bounds__(256) void k_xxh3_rows(XxhParams P) {
 					D.v[i][0] = x[0];
 					D.v[i][1] = x[1];
 				} else {
+#ifndef FDBXXH_ROWS_X2
+					// one unaligned dwordx4 (gfx950: full rate at a 4- or 8-byte
+					// aligned address, tools/membench3.hip), not two dwordx2
+					typedef uint64_t u64x2r __attribute__((ext_vector_type(2), aligned(4)));
+					typedef __attribute__((address_space(1))) const u64x2r g_u64x2r;
+					const u64x2r x = __builtin_nontemporal_load((g_u64x2r*)a);
+					D.v[i][0] = x[0];
+					D.v[i][1] = x[1];
+#else
 					D.v[i][0] = __builtin_nontemporal_load((g_u64*)a);
 					D.v[i][1] = __builtin_nontemporal_load((g_u64*)(a + 8));
+#endif
 				}
 			}
 		}
