@@ -459,9 +459,8 @@ constexpr uint32_t kNPScratch = 1024;   // the scan's wave sums
 constexpr uint32_t kNPStats = 1088;     // u64 [4 waves][4]: workgroup 0's route statistics
 constexpr uint32_t kNPHand = 1200;      // first entry, sentinel
 constexpr uint32_t kNPBlocks = 2048;    // [kNPMax] blocks per buffer
-constexpr uint32_t kNPGeo = kNPBlocks + kNPMax;  // [kNPMax][3] E (2 words), lo | k0 | t: entries without reloads
-constexpr uint32_t kNPSeed = kNPGeo + 3 * kNPMax;  // [kNPMax] ~seed
-static_assert(kNPSeed + kNPMax <= kLdsBytesB / 4, "prep-free start-up: its LDS scratch fits the table image");
+constexpr uint32_t kNPGeo = kNPBlocks + kNPMax;  // [kNPMax][4] E (2 words), lo | k0 | t, ~seed: one 16-byte read
+static_assert(kNPGeo + 4 * kNPMax <= kLdsBytesB / 4, "prep-free start-up: its LDS scratch fits the table image");
 // Every workgroup sums the whole batch's block counts (thread t: buffers
 // [8t, 8t + 8), their metadata loaded at once), writes the route entries of
 // the buffers its own grab range [g0, g1) covers -- plus a sentinel entry
@@ -502,12 +501,9 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds, uint32_t ngrid) {
 				const uint64_t P0 = reinterpret_cast<uint64_t>(P.base) + o[u];
 				const NPGeo g = np_geo(P0, l[u]);
 				nbl[i0 + j0 + u] = g.nb;
-				const BigEnt e = np_entry(P0, l[u], g.nb, 0u, 0u, 0u);
-				uint32_t* const gq = lds + kNPGeo + 3 * (uint32_t)(i0 + j0 + u);
-				gq[0] = (uint32_t)e.E;
-				gq[1] = (uint32_t)(e.E >> 32);
-				gq[2] = e.lot;
-				lds[kNPSeed + (uint32_t)(i0 + j0 + u)] = ~sd[u];
+				const BigEnt e = np_entry(P0, l[u], g.nb, 0u, 0u, sd[u]);
+				*reinterpret_cast<u32x4*>(lds + kNPGeo + 4 * (uint32_t)(i0 + j0 + u)) =
+				    u32x4{(uint32_t)e.E, (uint32_t)(e.E >> 32), e.lot, e.sd};
 				B += g.nb;
 				N += g.nb ? 1u : 0u;
 				refuse |= g.refuse;
@@ -536,21 +532,27 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds, uint32_t ngrid) {
 	}
 	__syncthreads();
 	FDBCRC_BT2(1)
-	uint64_t Bex = Bi - B, Btot = 0;
-	uint32_t Nex = Ni - N, Ntot = 0;
-	bool ref = false;
+	// the 16 wave sums, lane-parallel: lanes 0..15 of every wave read them
+	// once and scan them (serial reads took 0.8 us)
 	constexpr uint32_t nw = 16;  // (1024-thread workgroups: blockDim read from memory costs a round trip here)
-	for (uint32_t k = 0; k < nw; ++k) {
-		const uint64_t b = sB[k];
-		const uint32_t c = sN[k];
-		if (k < wv) {
-			Bex += b;
-			Nex += c;
+	const uint32_t kl = lane & 15;
+	uint64_t sb16 = sB[kl];
+	uint32_t sn16 = sN[kl];
+	const bool ref = __ballot(sR[kl] != 0) != 0;
+#pragma unroll
+	for (int d = 1; d < 16; d <<= 1) {
+		const uint64_t vb = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(sb16 >> 32), d, 16) << 32) |
+		                    (uint32_t)__shfl_up((int)(uint32_t)sb16, d, 16);
+		const uint32_t vn = (uint32_t)__shfl_up((int)sn16, d, 16);
+		if (kl >= (uint32_t)d) {
+			sb16 += vb;
+			sn16 += vn;
 		}
-		Btot += b;
-		Ntot += c;
-		ref |= sR[k] != 0;
 	}
+	const uint64_t Btot = rdlane64(sb16, 15);
+	const uint32_t Ntot = rdlane(sn16, 15);
+	const uint64_t Bex = Bi - B + (wv ? rdlane64(sb16, (int)wv - 1) : 0);
+	const uint32_t Nex = Ni - N + (wv ? rdlane(sn16, (int)wv - 1) : 0u);
 	// 32-bit block and entry numbers, as the planner's
 	R.refused = ref || Btot >= 0xFFFFFFFFull;
 	R.count = R.refused ? 0u : (uint32_t)Btot;
@@ -585,13 +587,13 @@ __device__ NPStart np_start(const BigParams& P, uint32_t* lds, uint32_t ngrid) {
 			const uint32_t nb = nbl[i];
 			if (!nb) continue;
 			if (sb + nb > blo) {
-				const uint32_t* const gq = lds + kNPGeo + 3 * (uint32_t)i;
+				const u32x4 gq = *reinterpret_cast<const u32x4*>(lds + kNPGeo + 4 * (uint32_t)i);
 				BigEnt e;
 				e.E = ((uint64_t)gq[1] << 32) | gq[0];
 				e.s = (uint32_t)sb;
 				e.idx = (uint32_t)i;
 				e.lot = gq[2];
-				e.sd = lds[kNPSeed + (uint32_t)i];
+				e.sd = gq[3];
 				put(q, e);
 				if (sb <= blo) lds[kNPHand] = q;  // holds the workgroup's first block
 				if (bhi <= sb + nb) {  // holds its last block: the sentinel follows
