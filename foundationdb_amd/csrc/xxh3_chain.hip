@@ -18,6 +18,13 @@
 //                                           of two or more, to their staging
 //                                           offsets
 //   launch_xxh3                             the varlen engine over the ranges
+//   launch_xxh3_lchain                      chains of 2..8 segments and at most
+//                                           16 KiB (k_chain_ranges lists them
+//                                           per XCD), one wave each, staged in
+//                                           LDS: no staging area, each byte read
+//                                           from HBM once (k_xxh3_lchain in
+//                                           xxh3_kernels.hip), over the varlen
+//                                           pass's empty digests
 //   launch_xxh3_segrows                     the flagged chains where their
 //                                           segments lie (xxh3_segrows.hip),
 //                                           over the varlen pass's empty digests
@@ -41,8 +48,9 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s_w) {
 }
 
 __global__ __launch_bounds__(kScanT) void k_seg_bsum(const uint64_t* __restrict__ len, uint64_t n,
-                                                     uint64_t* __restrict__ bsum) {
+                                                     uint64_t* __restrict__ bsum, uint64_t* __restrict__ lcount) {
 	__shared__ uint64_t s_w[kScanT / 64];
+	if (blockIdx.x == 0 && threadIdx.x < 8) lcount[16 * threadIdx.x] = 0;  // (k_chain_ranges appends after this launch)
 	uint64_t v = 0;
 	for (unsigned k = 0; k < kScanPer; ++k) {
 		const uint64_t i = (uint64_t)blockIdx.x * kScanSpan + k * kScanT + threadIdx.x;
@@ -196,21 +204,52 @@ __global__ __launch_bounds__(256) void k_chain_ranges(const uint64_t* __restrict
                                                       const uint64_t* __restrict__ seg_off,
                                                       const uint8_t* __restrict__ staging,
                                                       uint8_t* __restrict__ segflag, uint64_t* __restrict__ ch_off,
-                                                      uint64_t* __restrict__ ch_len, uint8_t* __restrict__ chflag, int rows_on) {
+                                                      uint64_t* __restrict__ ch_len, uint8_t* __restrict__ chflag, int rows_on,
+                                                      int lc_on, uint64_t* __restrict__ list, uint64_t* __restrict__ counts,
+                                                      uint64_t lcap) {
 	const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (c >= nchains) return;
-	uint64_t s0 = starts[c], s1 = starts[c + 1];
+	const bool in = c < nchains;
+	const uint64_t cc = in ? c : 0;
+	uint64_t s0 = starts[cc], s1 = starts[cc + 1];
 	s0 = s0 < nsegs ? s0 : nsegs;
 	s1 = s1 < nsegs ? s1 : nsegs;
 	const uint64_t la = pre[s0], lb = pre[s1];  // (unclamped: the chain's true length)
 	uint64_t a = la < cap ? la : cap, b = lb < cap ? lb : cap;
 	const bool one = s1 == s0 + 1;
 	const uint64_t L = lb > la ? lb - la : 0;
-	const bool rows = rows_on && !one && s1 > s0 && s1 - s0 <= kSegRowsMax && L > 240 && L <= kSegRowsMaxLen;
-	for (uint64_t j = s0; j < s1; ++j) segflag[j] = one || rows ? 1 : 0;
+	// the LDS route (k_xxh3_lchain): 2 .. kLChainSegs segments, at most kLChainMax bytes
+	const bool lc = in && lc_on && s1 >= s0 + 2 && s1 - s0 <= kLChainSegs && L <= kLChainMax;
+	const bool rows = !lc && rows_on && !one && s1 > s0 && s1 - s0 <= kSegRowsMax && L > 240 && L <= kSegRowsMaxLen;
+	// appended to the list of this workgroup's XCD (workgroup b runs on XCD
+	// b % 8), one atomic per workgroup on that XCD's counter: one counter for
+	// the batch, one atomic per wave, serialised the appends (81 us on the
+	// bench's 406 k chains)
+	{
+		__shared__ uint32_t s_n[4];
+		__shared__ uint64_t s_at;
+		const uint64_t m = __ballot(lc);
+		const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+		if (lane == 0) s_n[wv] = (uint32_t)__builtin_popcountll(m);
+		__syncthreads();
+		const uint32_t x = blockIdx.x & 7;
+		if (threadIdx.x == 0) {
+			const uint32_t tot = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+			s_at = tot ? atomicAdd((unsigned long long*)(counts + 16 * x), (unsigned long long)tot) : 0;
+		}
+		__syncthreads();
+		if (lc) {
+			uint64_t k = s_at + (uint64_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+			for (uint32_t u = 0; u < wv; ++u) k += s_n[u];
+			uint64_t* const lx = list + 2 * lcap * x;
+			lx[2 * k] = c;
+			lx[2 * k + 1] = s0 | ((s1 - s0) << 56);
+		}
+	}
+	if (!in) return;
+	for (uint64_t j = s0; j < s1; ++j) segflag[j] = one || rows || lc ? 1 : 0;
 	ch_off[c] = one ? reinterpret_cast<uint64_t>(base) + seg_off[s0] - reinterpret_cast<uint64_t>(staging) : a;
-	ch_len[c] = rows ? 0 : (b > a ? b - a : 0);
-	chflag[c] = rows ? 2 : 0;
+	ch_len[c] = rows || lc ? 0 : (b > a ? b - a : 0);
+	chflag[c] = lc ? 3 : rows ? 2 : 0;
 }
 
 // The segment rows read each byte once where the gather route reads it
@@ -228,12 +267,27 @@ static bool segrows_on() {
 	return __atomic_load_n(&g_segrows, __ATOMIC_RELAXED) == 1;
 }
 
+// The LDS route for short chains (k_xxh3_lchain) is on unless FDBXXH_LCHAIN=0
+// or fdbxxh_set_lchain(0) (tests: both routes against the reference).
+static int g_lchain = -1;
+static bool lchain_on() {
+	if (__atomic_load_n(&g_lchain, __ATOMIC_RELAXED) < 0) {
+		const char* e = getenv("FDBXXH_LCHAIN");
+		int expect = -1;
+		__atomic_compare_exchange_n(&g_lchain, &expect, e && atoi(e) == 0 ? 0 : 1, false, __ATOMIC_RELAXED,
+		                            __ATOMIC_RELAXED);
+	}
+	return __atomic_load_n(&g_lchain, __ATOMIC_RELAXED) == 1;
+}
+
 static uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
+// entries per XCD list: the chains of every eighth 256-chain workgroup
+static uint64_t lchain_cap(uint64_t nchains) { return 256 * (((nchains + 255) / 256 + 7) / 8); }
 
 uint64_t xxh3_chain_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes, uint64_t nwave) {
 	const uint64_t nb = nsegs / kScanSpan + 1;  // the scan covers nsegs + 1 entries (pre[nsegs] = total)
 	return al16(8 * (nb + 1)) + al16(8 * (nsegs + 1)) + 2 * al16(8 * nchains) + al16(nsegs + 1) + al16(nchains) +
-	       al16(total_bytes + 16) +
+	       8 * 128 + 8 * 16 * lchain_cap(nchains) + al16(total_bytes + 16) +
 	       al16(xxh3_workspace_bytes_for(nchains ? nchains : 1, nwave, xxh3_long_blocks_bound(total_bytes)));
 }
 
@@ -254,20 +308,27 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	p += al16(nsegs + 1);
 	uint8_t* chflag = p;
 	p += al16(nchains);
+	// the LDS route's lists: per XCD a count (its own 128-byte line) and entries
+	const uint64_t lcap = lchain_cap(nchains);
+	uint64_t* counts = reinterpret_cast<uint64_t*>(p);
+	p += 8 * 128;
+	uint64_t* list = reinterpret_cast<uint64_t*>(p);
+	p += 8 * 16 * lcap;
 	uint8_t* staging = p;
 	p += al16(total_bytes + 16);
 	void* eng = p;
 	if (nsegs) {
-		k_seg_bsum<<<(unsigned)nb, kScanT, 0, s>>>(seg_len, nsegs, bsum);
+		k_seg_bsum<<<(unsigned)nb, kScanT, 0, s>>>(seg_len, nsegs, bsum, counts);
 		k_seg_bscan<<<1, kScanT, 0, s>>>(bsum, nb);
 		k_seg_scan<<<(unsigned)nb, kScanT, 0, s>>>(seg_len, nsegs, bsum, pre);
 	} else if (hipMemsetAsync(pre, 0, 8, s) != hipSuccess) {
 		return -1;
 	}
 	const bool rows_on = segrows_on();
+	const bool lc_on = nsegs != 0 && lchain_on();  // (nsegs == 0: no chain of two segments)
 	k_chain_ranges<<<(unsigned)((nchains + 255) / 256), 256, 0, s>>>(starts, nchains, nsegs, pre, total_bytes, base,
 	                                                                   seg_off, staging, segflag, ch_off, ch_len, chflag,
-	                                                                   rows_on ? 1 : 0);
+	                                                                   rows_on ? 1 : 0, lc_on ? 1 : 0, list, counts, lcap);
 	if (nsegs) {
 		const uint64_t g = (nsegs + 255) / 256;  // a wave per 64 segments
 		k_seg_gather<<<(unsigned)(g < 65536 ? g : 65536), 256, 0, s>>>(base, seg_off, seg_len, pre, segflag, nsegs,
@@ -284,6 +345,19 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 	P.ws_bytes = xxh3_workspace_bytes_for(nchains ? nchains : 1, (uint64_t)num_cus * xxh3_blocks_per_cu() * kWavesPerBlock,
 	                                      xxh3_long_blocks_bound(total_bytes));
 	if (launch_xxh3(P, num_cus, eng, s)) return -1;
+	if (lc_on) {  // over the varlen pass's empty digests of the listed chains
+		LChainP C{};
+		C.base = base;
+		C.seg_off = seg_off;
+		C.seg_len = seg_len;
+		C.list = list;
+		C.counts = counts;
+		C.lcap = lcap;
+		C.seed = seed;
+		C.seeds = seeds;
+		C.out = out;
+		if (launch_xxh3_lchain(C, num_cus, s)) return -1;
+	}
 	if (!rows_on) return 0;
 	SegRowsP R{};
 	R.base = base;
@@ -299,6 +373,14 @@ int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint
 }
 
 }  // namespace fdbxxh
+
+// Tests / A-B: the LDS route for short chains on (1, the default) or off (0)
+// in later calls; returns the previous setting.
+extern "C" int fdbxxh_set_lchain(int on) {
+	const int prev = fdbxxh::lchain_on() ? 1 : 0;
+	__atomic_store_n(&fdbxxh::g_lchain, on ? 1 : 0, __ATOMIC_RELAXED);
+	return prev;
+}
 
 // Development / tests: hash qualifying multi-segment chains in place (1) or
 // all from staging (0) in later calls; returns the previous setting.

@@ -82,6 +82,26 @@ struct SegRowsP {
 	uint64_t* out;
 };
 int launch_xxh3_segrows(const SegRowsP& P, int num_cus, hipStream_t stream);
+// Short chains staged in LDS (k_xxh3_lchain): a chain of 2..kLChainSegs
+// segments and at most kLChainMax bytes, one wave each, listed by
+// k_chain_ranges as {chain, first segment | segments << 56} in one list per
+// XCD (a workgroup appends to its own XCD's).
+#ifndef FDBXXH_LCMAX
+#define FDBXXH_LCMAX 16384
+#endif
+constexpr uint32_t kLChainMax = FDBXXH_LCMAX, kLChainSegs = 8;
+struct LChainP {
+	const uint8_t* base;
+	const uint64_t* seg_off;
+	const uint64_t* seg_len;
+	const uint64_t* list;    // [8][lcap][2]: per XCD, counts[16 x] entries
+	const uint64_t* counts;  // [8 x 16]
+	uint64_t lcap;
+	uint64_t seed;
+	const uint64_t* seeds;
+	uint64_t* out;
+};
+int launch_xxh3_lchain(const LChainP& P, int num_cus, hipStream_t stream);
 // Chains of segments (xxh3_chain.hip): gather into a staging area, then varlen.
 uint64_t xxh3_chain_workspace_bytes(uint64_t nsegs, uint64_t nchains, uint64_t total_bytes, uint64_t nwave);
 int launch_xxh3_chained(const uint8_t* base, const uint64_t* seg_off, const uint64_t* seg_len, uint64_t nsegs,

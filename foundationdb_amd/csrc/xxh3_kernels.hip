@@ -1938,6 +1938,278 @@ int launch_xxh3_pages_list(const XxhParams& P0, int num_cus, hipStream_t stream)
 	return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Short chains staged in LDS (round 6; xxh3_chain.hip's third route).  A chain
+// of 2..kLChainSegs segments and at most kLChainMax bytes -- a packet over two
+// or three PacketBuffers, FlowTransport.cpp:2025-2068 -- is hashed by one wave
+// from LDS: its segments are read once, coalesced (16-byte loads at each
+// segment's own alignment, 16-byte aligned LDS writes; the bytes of the chunks
+// a segment boundary cuts one by one), and the one-wave long form (the block
+// step of k_xxh3: lane = stripe x accumulator pair) or the short forms run
+// over the LDS copy -- no staging area in HBM, so each byte crosses HBM once
+// instead of three times (gather read + write, hash read).  Per wave the
+// chains go through a three-stage pipeline: chain t+2's list entry (scalar
+// loads), chain t+1's segment metadata and data loads in flight while chain t
+// is hashed.
+// ---------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t* L, uint32_t o) {
+	const uint32_t a = o >> 2;
+	return __builtin_amdgcn_alignbyte(L[a + 1], L[a], o & 3u);
+}
+__device__ __forceinline__ uint64_t lds_u64(const uint32_t* L, uint32_t o) {
+	const uint32_t a = o >> 2, w0 = L[a], w1 = L[a + 1], w2 = L[a + 2];
+	return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, o & 3u) << 32) | __builtin_amdgcn_alignbyte(w1, w0, o & 3u);
+}
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+__device__ __forceinline__ uint32_t lds_u8(const uint32_t* L, uint32_t o) { return (L[o >> 2] >> (8 * (o & 3u))) & 255u; }
+__device__ __forceinline__ uint64_t mix16_lds(const uint32_t* L, uint32_t o, int soff, uint64_t seed) {
+	return mulfold(lds_u64(L, o) ^ (ksec(soff) + seed), lds_u64(L, o + 8) ^ (ksec(soff + 8) - seed));
+}
+// xxh3_short over an LDS copy (xxhash.h:2734-2951)
+__device__ uint64_t xxh3_short_lds(const uint32_t* L, uint32_t len, uint64_t seed) {
+	if (len <= 16) {
+		if (len > 8) {
+			const uint64_t f1 = (ksec(24) ^ ksec(32)) + seed, f2 = (ksec(40) ^ ksec(48)) - seed;
+			const uint64_t lo = lds_u64(L, 0) ^ f1, hi = lds_u64(L, len - 8) ^ f2;
+			return xxh3_aval(len + __builtin_bswap64(lo) + hi + mulfold(lo, hi));
+		}
+		if (len >= 4) {
+			const uint64_t s2 = seed ^ ((uint64_t)__builtin_bswap32((uint32_t)seed) << 32);
+			const uint32_t i1 = lds_u32(L, 0), i2 = lds_u32(L, len - 4);
+			const uint64_t flip = (ksec(8) ^ ksec(16)) - s2;
+			return rrmxmx(((uint64_t)i2 + ((uint64_t)i1 << 32)) ^ flip, len);
+		}
+		if (len) {
+			const uint32_t c1 = lds_u8(L, 0), c2 = lds_u8(L, len >> 1), c3 = lds_u8(L, len - 1);
+			const uint32_t comb = (c1 << 16) | (c2 << 24) | c3 | (len << 8);
+			return xxh64_aval((uint64_t)comb ^ ((uint64_t)(ksec32(0) ^ ksec32(4)) + seed));
+		}
+		return xxh64_aval(seed ^ (ksec(56) ^ ksec(64)));
+	}
+	uint64_t acc = (uint64_t)len * P64_1;
+	if (len <= 128) {
+		const int pairs = (int)((len - 1) >> 5);
+		for (int i = pairs; i >= 1; --i) {
+			acc += mix16_lds(L, 16 * i, 32 * i, seed);
+			acc += mix16_lds(L, len - 16 * (i + 1), 32 * i + 16, seed);
+		}
+		acc += mix16_lds(L, 0, 0, seed);
+		acc += mix16_lds(L, len - 16, 16, seed);
+		return xxh3_aval(acc);
+	}
+	const int rounds = (int)len / 16;
+	for (int i = 0; i < 8; ++i) acc += mix16_lds(L, 16 * i, 16 * i, seed);
+	acc = xxh3_aval(acc);
+	for (int i = 8; i < rounds; ++i) acc += mix16_lds(L, 16 * i, 16 * (i - 8) + 3, seed);
+	acc += mix16_lds(L, len - 16, 136 - 17, seed);
+	return xxh3_aval(acc);
+}
+}  // namespace
+
+constexpr uint32_t kLcSlots = kLChainMax / 1024;  // 16-byte chunks per lane
+__global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
+	__shared__ __attribute__((aligned(16))) uint32_t lbuf[4][kLChainMax / 4 + 16];
+	const int lane = threadIdx.x & 63;
+	const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	uint32_t* const L = lbuf[wv];
+	typedef __attribute__((address_space(4))) const uint64_t k_u64;
+	k_u64* const lst = (k_u64*)P.list;  // written by k_chain_ranges (an earlier launch): scalar loads
+	// this XCD's list (workgroup b runs on XCD b % 8; k_chain_ranges appended
+	// to the list of its own), strided over the XCD's waves
+	const uint32_t x = blockIdx.x & 7;
+	const uint64_t nx = ((k_u64*)P.counts)[16 * x];
+	const uint64_t wx = (uint64_t)(blockIdx.x >> 3) * 4 + wv, nwx = (uint64_t)(gridDim.x >> 3) * 4;
+	if (wx >= nx) return;
+	k_u64* const lx = lst + 2 * P.lcap * x;
+	const uint64_t dummy = reinterpret_cast<uint64_t>(P.list);  // 16 readable bytes
+	const uint64_t base = reinterpret_cast<uint64_t>(P.base);
+
+	// chain t's list entry: chain index, first segment, segment count
+	uint64_t ec1 = 0, es1 = 0;
+	uint32_t en1 = 0;
+	// The wave's next 64 list entries (and seeds) wait in its lanes: a list
+	// entry read at its use held up the metadata loads behind it every chain.
+	const uint64_t* const lg = P.list + 2 * P.lcap * x;
+	uint64_t ea = 0, eb = 0, esd = 0;
+	uint32_t et = 0;  // the next entry's ordinal (entry wx + et * nwx)
+	auto entry = [&](uint64_t i, uint64_t& c, uint64_t& s0, uint32_t& ns, uint64_t& sdv) {
+		(void)i;
+		if ((et & 63u) == 0) {
+			const uint64_t j = wx + (uint64_t)(et + (uint32_t)lane) * nwx;
+			const uint64_t jc = j < nx ? j : wx;
+			ea = lg[2 * jc];
+			eb = lg[2 * jc + 1];
+			esd = P.seeds ? P.seeds[ea] : P.seed;
+		}
+		const uint64_t a = rdlane64(ea, (int)(et & 63u)), b = rdlane64(eb, (int)(et & 63u));
+		sdv = rdlane64(esd, (int)(et & 63u));
+		++et;
+		c = a;
+		s0 = b & ((1ull << 56) - 1);
+		ns = (uint32_t)(b >> 56);
+	};
+	// segment metadata in lanes 0 .. ns-1
+	uint64_t moff = 0, mlen = 0;
+	auto meta_issue = [&](uint64_t s0, uint32_t ns) {
+		const uint64_t j = s0 + ((uint32_t)lane < ns ? (uint32_t)lane : 0u);
+		moff = P.seg_off[j];
+		mlen = P.seg_len[j];
+	};
+	// the geometry derived from the metadata (uniform)
+	uint32_t gns = 0, gL = 0;
+	uint32_t gcs[kLChainSegs], gend[kLChainSegs];
+	uint64_t gd[kLChainSegs];
+	auto geometry = [&](uint32_t ns) {
+		uint32_t len = (uint32_t)lane < ns ? (uint32_t)mlen : 0u;  // (a chain of this route is under 2^14 bytes)
+		uint32_t inc = len;
+#pragma unroll
+		for (int d = 1; d < (int)kLChainSegs; d <<= 1) {
+			const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - d) << 2, (int)inc);
+			inc += lane >= d ? y : 0u;
+		}
+		const uint32_t cs = inc - len;
+		const uint64_t dd = moff - cs;
+		gns = ns;
+		gL = rdlane(inc, (int)kLChainSegs - 1);
+#pragma unroll
+		for (uint32_t j = 0; j < kLChainSegs; ++j) {
+			gcs[j] = rdlane(cs, (int)j);
+			gend[j] = rdlane(inc, (int)j);
+			gd[j] = rdlane64(dd, (int)j);
+		}
+	};
+	// data loads: 16-byte chunk q = lane + 64 r of the chain (full chunks), and
+	// the bytes of the chunks a boundary cuts (items lane, lane + 64: boundary
+	// p = item / 16 -- segment p's end --, byte item % 16 of its chunk)
+	typedef __attribute__((address_space(1))) const u64x2u g_u64x2u_;
+	u64x2u R[kLcSlots];
+	uint32_t full = 0;  // bit r: slot r is a full chunk
+	uint32_t bv[2], bo[2];
+	bool bon[2];
+	auto data_issue = [&]() {
+		const uint32_t nr = (gL + 1023) >> 10;
+		full = 0;
+#pragma unroll
+		for (uint32_t r = 0; r < kLcSlots; ++r) {
+			if (r < nr) {
+				const uint32_t q16 = 16u * ((uint32_t)lane + 64u * r);
+				uint64_t d = gd[0];
+				uint32_t e = gend[0];
+#pragma unroll
+				for (uint32_t j = 1; j < kLChainSegs; ++j) {
+					const bool m = j < gns && gcs[j] <= q16;
+					d = m ? gd[j] : d;
+					e = m ? gend[j] : e;
+				}
+				const bool f = q16 + 16u <= e;  // (e <= gL)
+				full |= f ? 1u << r : 0u;
+#ifdef FDBXXH_LC_NOLOAD
+				R[r] = u64x2u{d, (uint64_t)f};  // timing experiment: no data loads (wrong results)
+#else
+				R[r] = __builtin_nontemporal_load((g_u64x2u_*)(f ? base + d + q16 : dummy));
+#endif
+			}
+		}
+#pragma unroll
+		for (int v = 0; v < 2; ++v) {
+			const uint32_t it = (uint32_t)lane + 64u * v, p = it >> 4;
+			uint32_t bp = gend[0];
+#pragma unroll
+			for (uint32_t j = 1; j < kLChainSegs; ++j) bp = p == j ? gend[j] : bp;
+			const uint32_t e = (bp & ~15u) + (it & 15u);
+			uint64_t d = gd[0];
+#pragma unroll
+			for (uint32_t j = 1; j < kLChainSegs; ++j) d = (j < gns && gcs[j] <= e) ? gd[j] : d;
+			const bool on = p < gns && (bp & 15u) != 0 && e < gL;
+			bon[v] = on;
+			bo[v] = e;
+			typedef __attribute__((address_space(1))) const uint8_t g_u8_;
+			bv[v] = *((g_u8_*)(on ? base + d + e : dummy));
+		}
+	};
+	auto data_commit = [&]() {
+		const uint32_t nr = (gL + 1023) >> 10;
+#pragma unroll
+		for (uint32_t r = 0; r < kLcSlots; ++r)
+			if (r < nr && (full >> r & 1u)) {
+				typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
+				*reinterpret_cast<u64x2a*>(L + 4u * ((uint32_t)lane + 64u * r)) = u64x2a{R[r][0], R[r][1]};
+			}
+#pragma unroll
+		for (int v = 0; v < 2; ++v)
+			if (bon[v]) reinterpret_cast<uint8_t*>(L)[bo[v]] = (uint8_t)bv[v];
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	};
+
+	// prologue: the first chain's geometry and data in flight, the next one's metadata
+	uint64_t c0, s00;
+	uint32_t n0;
+	uint64_t sd0 = 0, esd1 = 0;
+	entry(wx, c0, s00, n0, sd0);
+	meta_issue(s00, n0);
+	geometry(n0);
+	data_issue();
+	uint64_t i1 = wx + nwx;
+	if (i1 < nx) {
+		entry(i1, ec1, es1, en1, esd1);
+		meta_issue(es1, en1);
+	}
+	for (uint64_t i = wx; i < nx; i += nwx) {
+		const uint32_t len = gL;
+		const uint64_t c = c0;
+		const uint64_t sd = sd0;
+		data_commit();  // this chain in LDS
+		// the next chain: its data in flight while this one is hashed; the one after: its metadata
+		if (i1 < nx) {
+			c0 = ec1;
+			sd0 = esd1;
+			geometry(en1);
+			data_issue();
+			i1 += nwx;
+			if (i1 < nx) {
+				entry(i1, ec1, es1, en1, esd1);
+				meta_issue(es1, en1);
+			}
+		}
+		uint64_t h;
+#ifdef FDBXXH_LC_NOHASH
+		if (len != 0x7fffffff) {  // timing experiment: no hash (wrong results)
+			h = L[lane];
+		} else
+#endif
+		if (len <= 240) {
+			h = xxh3_short_lds(L, len, sd);
+		} else {
+			const Keys K = make_keys(lane, sd);
+			Acc A = acc_init(lane);
+			const uint32_t nfull = (len - 1) >> 10, ns = ((len - 1) - (nfull << 10)) >> 6;
+			for (uint32_t b = 0; b < nfull; ++b) {
+				typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
+				const u64x2a v = *reinterpret_cast<const u64x2a*>(L + 256u * b + 4u * (uint32_t)lane);
+				block_step(A, v[0], v[1], K.k0, K.k1, true);
+				scramble(A, K);
+			}
+			const bool last = lane >= 60;
+			const uint32_t o = last ? len - 64u + 16u * (uint32_t)(lane - 60) : (nfull << 10) + 16u * (uint32_t)lane;
+			const uint64_t v0 = lds_u64(L, o), v1 = lds_u64(L, o + 8);
+			block_step(A, v0, v1, last ? K.l0 : K.k0, last ? K.l1 : K.k1, last || (uint32_t)lane < 4 * ns);
+			h = merge(A, K, len, lane);
+		}
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();  // (every lane's LDS reads before the next chain's writes)
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		if (lane == 0) P.out[c] = h;
+	}
+}
+
+int launch_xxh3_lchain(const LChainP& P, int num_cus, hipStream_t stream) {
+	k_xxh3_lchain<<<(unsigned)(8 * ((2 * num_cus + 7) / 8)), 256, 0, stream>>>(P);  // (a multiple of 8: the XCD lists)
+	return 0;
+}
+
 }  // namespace fdbxxh
 
 #ifdef FDBXXH_TIMES

@@ -389,6 +389,72 @@ def _chained_rows_case(cuda, X):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lc", [1, 0])
+def test_gpu_xxh3_chained_lds_route(cuda, lc):
+    """Short chains staged in LDS (k_xxh3_lchain, round 6: 2..8 segments, at
+    most 16 KiB) and, with the route off, the same chains through staging:
+    every short-form threshold (0, 1-3, 4-8, 9-16, 17-128, 129-240) and the
+    long form's (241, 1024/1025, a last stripe cut by a boundary, 16383 /
+    16384 / 16385 bytes, the last gathered), zero-length and 1-byte segments,
+    boundaries at every offset mod 16 and several inside one 16-byte chunk,
+    8 and 9 segments, segments at any alignment up to the buffer's last byte,
+    uniform and per-chain seeds -- against the reference's own flow/xxhash.c
+    over each chain's concatenated bytes."""
+    import torch
+    import foundationdb_amd.xxh3 as X
+    from foundationdb_amd import crc32c as F
+    Lb = F.lib()
+    prev = Lb.fdbxxh_set_lchain(lc)
+    try:
+        rng = np.random.default_rng(2047)
+        h = O.splitmix64((8 << 20) // 8, 0x2047).view(np.uint8)
+        d = torch.from_numpy(h).to(cuda)
+        offs, lens, starts = [], [], [0]
+
+        def chain(parts, at_end=False):
+            for L in parts:
+                o = h.size - int(L) if at_end else int(rng.integers(0, h.size - max(int(L), 1)))
+                offs.append(o)
+                lens.append(int(L))
+            starts.append(len(offs))
+
+        for total in (0, 1, 2, 3, 4, 7, 8, 9, 15, 16, 17, 31, 32, 33, 127, 128, 129, 200, 239, 240, 241, 255, 256,
+                      1023, 1024, 1025, 1088, 1090, 2047, 2048, 4095, 4096, 4097, 8000, 16383, 16384, 16385):
+            for ns in (2, 3, 5, 8, 9):
+                cuts = np.sort(rng.integers(0, total + 1, ns - 1))
+                chain(np.diff(np.concatenate([[0], cuts, [total]])))
+        for m in range(16):  # boundaries at every offset mod 16; three inside one chunk; inside the last stripe
+            chain([320 + m, 700])
+            chain([16 * 40 + m, 1, 2, 3000])
+            chain([1000, 30 + m])
+            chain([2, 0, 0, 1, 700 + m, 1])
+        chain([5, 300], at_end=True)  # segments ending at the buffer's last byte
+        chain([4096 - 7, 4096, 4096, 4000], at_end=True)
+        for _ in range(300):  # PacketBuffer-like chains
+            L = int(rng.integers(1, 16385))
+            first = int(rng.integers(1, 4097))
+            parts = [min(first, L)]
+            while sum(parts) < L:
+                parts.append(min(4096, L - sum(parts)))
+            chain(parts)
+        cat = lambda c: b"".join(h[o:o + l].tobytes() for o, l in zip(offs[starts[c]:starts[c + 1]], lens[starts[c]:starts[c + 1]]))
+        t = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device=cuda)
+        nc = len(starts) - 1
+        got = X.batch_chained(d, t(offs), t(lens), t(starts)).cpu().numpy().view(np.uint64)
+        want = np.array([O.ref_xxh3_64(cat(c)) for c in range(nc)], dtype=np.uint64)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(int(c), len(cat(c)), int(starts[c + 1] - starts[c])) for c in bad[:8]]
+        seeds = rng.integers(0, 2**63, nc, dtype=np.int64)
+        got = X.batch_chained(d, t(offs), t(lens), t(starts), seeds=torch.from_numpy(seeds).to(cuda)).cpu().numpy().view(np.uint64)
+        want = np.array([O.ref_xxh3_64(cat(c), int(seeds[c])) for c in range(nc)], dtype=np.uint64)
+        assert np.array_equal(got, want)
+        got = X.batch_chained(d, t(offs), t(lens), t(starts), seed=0xFDBEEFDB).cpu().numpy().view(np.uint64)
+        assert all(int(got[c]) == O.ref_xxh3_64(cat(c), 0xFDBEEFDB) for c in range(nc))
+    finally:
+        Lb.fdbxxh_set_lchain(prev)
+
+
+@pytest.mark.gpu
 def test_gpu_xxh3_chained_underestimated_total(cuda):
     """A total_bytes below the real sum of the segment lengths (caller error):
     the digests are undefined but every read stays inside the workspace
