@@ -1963,46 +1963,73 @@ __device__ __forceinline__ uint64_t lds_u64(const uint32_t* L, uint32_t o) {
 }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
 __device__ __forceinline__ uint32_t lds_u8(const uint32_t* L, uint32_t o) { return (L[o >> 2] >> (8 * (o & 3u))) & 255u; }
-__device__ __forceinline__ uint64_t mix16_lds(const uint32_t* L, uint32_t o, int soff, uint64_t seed) {
-	return mulfold(lds_u64(L, o) ^ (ksec(soff) + seed), lds_u64(L, o + 8) ^ (ksec(soff + 8) - seed));
+// The secret from an LDS copy (ks: the default secret's 24 words): kSec in
+// constant memory is a global load, and one issued behind a chain's data loads
+// waited for all of them (in-order vmcnt) before the hash could start.
+__device__ __forceinline__ uint64_t ksec_l(const uint64_t* ks, int off) {
+	const int j = off >> 3, r = off & 7;
+	return r ? (ks[j] >> (8 * r)) | (ks[j + 1] << (64 - 8 * r)) : ks[j];
+}
+__device__ __forceinline__ uint64_t sec_word_l(const uint64_t* ks, int j, uint64_t seed) {
+	const uint64_t w = ks[j];
+	return (j & 1) ? w - seed : w + seed;
+}
+__device__ __forceinline__ uint64_t sec_at_l(const uint64_t* ks, int j, int r, uint64_t seed) {
+	return (sec_word_l(ks, j, seed) >> (8 * r)) | (sec_word_l(ks, j + 1, seed) << (64 - 8 * r));
+}
+__device__ __forceinline__ Keys make_keys_l(const uint64_t* ks, int lane, uint64_t seed) {  // make_keys
+	const int s = lane >> 2, k = lane & 3;
+	Keys K;
+	K.k0 = sec_word_l(ks, s + 2 * k, seed);
+	K.k1 = sec_word_l(ks, s + 2 * k + 1, seed);
+	K.l0 = sec_at_l(ks, 15 + 2 * k, 1, seed);
+	K.l1 = sec_at_l(ks, 16 + 2 * k, 1, seed);
+	K.c0 = sec_word_l(ks, 16 + 2 * k, seed);
+	K.c1 = sec_word_l(ks, 17 + 2 * k, seed);
+	K.g0 = sec_at_l(ks, 1 + 2 * k, 3, seed);
+	K.g1 = sec_at_l(ks, 2 + 2 * k, 3, seed);
+	return K;
+}
+__device__ __forceinline__ uint64_t mix16_lds(const uint64_t* ks, const uint32_t* L, uint32_t o, int soff, uint64_t seed) {
+	return mulfold(lds_u64(L, o) ^ (ksec_l(ks, soff) + seed), lds_u64(L, o + 8) ^ (ksec_l(ks, soff + 8) - seed));
 }
 // xxh3_short over an LDS copy (xxhash.h:2734-2951)
-__device__ uint64_t xxh3_short_lds(const uint32_t* L, uint32_t len, uint64_t seed) {
+__device__ uint64_t xxh3_short_lds(const uint64_t* ks, const uint32_t* L, uint32_t len, uint64_t seed) {
 	if (len <= 16) {
 		if (len > 8) {
-			const uint64_t f1 = (ksec(24) ^ ksec(32)) + seed, f2 = (ksec(40) ^ ksec(48)) - seed;
+			const uint64_t f1 = (ksec_l(ks, 24) ^ ksec_l(ks, 32)) + seed, f2 = (ksec_l(ks, 40) ^ ksec_l(ks, 48)) - seed;
 			const uint64_t lo = lds_u64(L, 0) ^ f1, hi = lds_u64(L, len - 8) ^ f2;
 			return xxh3_aval(len + __builtin_bswap64(lo) + hi + mulfold(lo, hi));
 		}
 		if (len >= 4) {
 			const uint64_t s2 = seed ^ ((uint64_t)__builtin_bswap32((uint32_t)seed) << 32);
 			const uint32_t i1 = lds_u32(L, 0), i2 = lds_u32(L, len - 4);
-			const uint64_t flip = (ksec(8) ^ ksec(16)) - s2;
+			const uint64_t flip = (ksec_l(ks, 8) ^ ksec_l(ks, 16)) - s2;
 			return rrmxmx(((uint64_t)i2 + ((uint64_t)i1 << 32)) ^ flip, len);
 		}
 		if (len) {
 			const uint32_t c1 = lds_u8(L, 0), c2 = lds_u8(L, len >> 1), c3 = lds_u8(L, len - 1);
 			const uint32_t comb = (c1 << 16) | (c2 << 24) | c3 | (len << 8);
-			return xxh64_aval((uint64_t)comb ^ ((uint64_t)(ksec32(0) ^ ksec32(4)) + seed));
+			return xxh64_aval((uint64_t)comb ^ ((uint64_t)((uint32_t)(ksec_l(ks, 0) ^ (ksec_l(ks, 4)))) + seed));
 		}
-		return xxh64_aval(seed ^ (ksec(56) ^ ksec(64)));
+		return xxh64_aval(seed ^ (ksec_l(ks, 56) ^ ksec_l(ks, 64)));
 	}
 	uint64_t acc = (uint64_t)len * P64_1;
 	if (len <= 128) {
 		const int pairs = (int)((len - 1) >> 5);
 		for (int i = pairs; i >= 1; --i) {
-			acc += mix16_lds(L, 16 * i, 32 * i, seed);
-			acc += mix16_lds(L, len - 16 * (i + 1), 32 * i + 16, seed);
+			acc += mix16_lds(ks, L, 16 * i, 32 * i, seed);
+			acc += mix16_lds(ks, L, len - 16 * (i + 1), 32 * i + 16, seed);
 		}
-		acc += mix16_lds(L, 0, 0, seed);
-		acc += mix16_lds(L, len - 16, 16, seed);
+		acc += mix16_lds(ks, L, 0, 0, seed);
+		acc += mix16_lds(ks, L, len - 16, 16, seed);
 		return xxh3_aval(acc);
 	}
 	const int rounds = (int)len / 16;
-	for (int i = 0; i < 8; ++i) acc += mix16_lds(L, 16 * i, 16 * i, seed);
+	for (int i = 0; i < 8; ++i) acc += mix16_lds(ks, L, 16 * i, 16 * i, seed);
 	acc = xxh3_aval(acc);
-	for (int i = 8; i < rounds; ++i) acc += mix16_lds(L, 16 * i, 16 * (i - 8) + 3, seed);
-	acc += mix16_lds(L, len - 16, 136 - 17, seed);
+	for (int i = 8; i < rounds; ++i) acc += mix16_lds(ks, L, 16 * i, 16 * (i - 8) + 3, seed);
+	acc += mix16_lds(ks, L, len - 16, 136 - 17, seed);
 	return xxh3_aval(acc);
 }
 }  // namespace
@@ -2010,6 +2037,9 @@ __device__ uint64_t xxh3_short_lds(const uint32_t* L, uint32_t len, uint64_t see
 constexpr uint32_t kLcSlots = kLChainMax / 1024;  // 16-byte chunks per lane
 __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 	__shared__ __attribute__((aligned(16))) uint32_t lbuf[4][kLChainMax / 4 + 16];
+	__shared__ uint64_t ks[25];
+	if (threadIdx.x < 25) ks[threadIdx.x] = threadIdx.x < 24 ? kSec[threadIdx.x] : 0;
+	__syncthreads();
 	const int lane = threadIdx.x & 63;
 	const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	uint32_t* const L = lbuf[wv];
@@ -2028,33 +2058,20 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 	// chain t's list entry: chain index, first segment, segment count
 	uint64_t ec1 = 0, es1 = 0;
 	uint32_t en1 = 0;
-	// The wave's next 64 list entries (and seeds) wait in its lanes: a list
-	// entry read at its use held up the metadata loads behind it every chain.
-	const uint64_t* const lg = P.list + 2 * P.lcap * x;
-	uint64_t ea = 0, eb = 0, esd = 0;
-	uint32_t et = 0;  // the next entry's ordinal (entry wx + et * nwx)
 	auto entry = [&](uint64_t i, uint64_t& c, uint64_t& s0, uint32_t& ns, uint64_t& sdv) {
-		(void)i;
-		if ((et & 63u) == 0) {
-			const uint64_t j = wx + (uint64_t)(et + (uint32_t)lane) * nwx;
-			const uint64_t jc = j < nx ? j : wx;
-			ea = lg[2 * jc];
-			eb = lg[2 * jc + 1];
-			esd = P.seeds ? P.seeds[ea] : P.seed;
-		}
-		const uint64_t a = rdlane64(ea, (int)(et & 63u)), b = rdlane64(eb, (int)(et & 63u));
-		sdv = rdlane64(esd, (int)(et & 63u));
-		++et;
+		const uint64_t a = lx[2 * i], b = lx[2 * i + 1];
 		c = a;
 		s0 = b & ((1ull << 56) - 1);
 		ns = (uint32_t)(b >> 56);
+		sdv = P.seeds ? *(k_u64*)(P.seeds + a) : P.seed;
 	};
 	// segment metadata in lanes 0 .. ns-1
-	uint64_t moff = 0, mlen = 0;
+	uint64_t moff = 0;
+	uint32_t mlen = 0;
 	auto meta_issue = [&](uint64_t s0, uint32_t ns) {
 		const uint64_t j = s0 + ((uint32_t)lane < ns ? (uint32_t)lane : 0u);
 		moff = P.seg_off[j];
-		mlen = P.seg_len[j];
+		mlen = reinterpret_cast<const uint32_t*>(P.seg_len)[2 * j];  // (the low word: a chain here is under 2^14 bytes; a dead high word's load held up the register's next use)
 	};
 	// the geometry derived from the metadata (uniform)
 	uint32_t gns = 0, gL = 0;
@@ -2122,10 +2139,11 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 #pragma unroll
 			for (uint32_t j = 1; j < kLChainSegs; ++j) d = (j < gns && gcs[j] <= e) ? gd[j] : d;
 			const bool on = p < gns && (bp & 15u) != 0 && e < gL;
+			const uint64_t a = on ? base + d + e : dummy;
 			bon[v] = on;
-			bo[v] = e;
-			typedef __attribute__((address_space(1))) const uint8_t g_u8_;
-			bv[v] = *((g_u8_*)(on ? base + d + e : dummy));
+			bo[v] = e | ((uint32_t)a & 3u) << 16;  // (the byte's place in its dword, extracted at the commit)
+			typedef __attribute__((address_space(1))) const uint32_t g_u32_;
+			bv[v] = *((g_u32_*)(a & ~3ull));  // (a dword holding a wanted byte never crosses a page)
 		}
 	};
 	auto data_commit = [&]() {
@@ -2138,7 +2156,7 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 			}
 #pragma unroll
 		for (int v = 0; v < 2; ++v)
-			if (bon[v]) reinterpret_cast<uint8_t*>(L)[bo[v]] = (uint8_t)bv[v];
+			if (bon[v]) reinterpret_cast<uint8_t*>(L)[bo[v] & 0xFFFFu] = (uint8_t)(bv[v] >> (8 * (bo[v] >> 16)));
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 		__builtin_amdgcn_wave_barrier();
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2181,9 +2199,9 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 		} else
 #endif
 		if (len <= 240) {
-			h = xxh3_short_lds(L, len, sd);
+			h = xxh3_short_lds(ks, L, len, sd);
 		} else {
-			const Keys K = make_keys(lane, sd);
+			const Keys K = make_keys_l(ks, lane, sd);
 			Acc A = acc_init(lane);
 			const uint32_t nfull = (len - 1) >> 10, ns = ((len - 1) - (nfull << 10)) >> 6;
 			for (uint32_t b = 0; b < nfull; ++b) {
