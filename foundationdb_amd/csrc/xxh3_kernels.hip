@@ -2038,6 +2038,9 @@ constexpr uint32_t kLcSlots = kLChainMax / 1024;  // 16-byte chunks per lane
 __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 	__shared__ __attribute__((aligned(16))) uint32_t lbuf[4][kLChainMax / 4 + 16];
 	__shared__ uint64_t ks[25];
+	__shared__ uint32_t tcs[4][kLChainSegs], tend[4][kLChainSegs];  // per wave: the chain's segment table
+	__shared__ uint64_t td[4][kLChainSegs];
+	__shared__ uint8_t tmap[4][kLChainMax / 16];                    // ... and its chunk -> segment map
 	if (threadIdx.x < 25) ks[threadIdx.x] = threadIdx.x < 24 ? kSec[threadIdx.x] : 0;
 	__syncthreads();
 	const int lane = threadIdx.x & 63;
@@ -2073,12 +2076,14 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 		moff = P.seg_off[j];
 		mlen = reinterpret_cast<const uint32_t*>(P.seg_len)[2 * j];  // (the low word: a chain here is under 2^14 bytes; a dead high word's load held up the register's next use)
 	};
-	// the geometry derived from the metadata (uniform)
+	// The geometry derived from the metadata, as LDS tables of the wave: per
+	// segment its chain offset, end and source displacement (address - chain
+	// offset), and per 16-byte chunk of the chain the segment holding its first
+	// byte (a chunk -> segment map: a chunk's segment is two LDS reads, where a
+	// search over the segments held in SGPRs cost ~90 instructions per chunk).
 	uint32_t gns = 0, gL = 0;
-	uint32_t gcs[kLChainSegs], gend[kLChainSegs];
-	uint64_t gd[kLChainSegs];
 	auto geometry = [&](uint32_t ns) {
-		uint32_t len = (uint32_t)lane < ns ? (uint32_t)mlen : 0u;  // (a chain of this route is under 2^14 bytes)
+		uint32_t len = (uint32_t)lane < ns ? mlen : 0u;  // (a chain of this route is under 2^14 bytes)
 		uint32_t inc = len;
 #pragma unroll
 		for (int d = 1; d < (int)kLChainSegs; d <<= 1) {
@@ -2086,15 +2091,21 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 			inc += lane >= d ? y : 0u;
 		}
 		const uint32_t cs = inc - len;
-		const uint64_t dd = moff - cs;
 		gns = ns;
 		gL = rdlane(inc, (int)kLChainSegs - 1);
-#pragma unroll
-		for (uint32_t j = 0; j < kLChainSegs; ++j) {
-			gcs[j] = rdlane(cs, (int)j);
-			gend[j] = rdlane(inc, (int)j);
-			gd[j] = rdlane64(dd, (int)j);
+		if ((uint32_t)lane < kLChainSegs) {
+			tcs[wv][lane] = cs;
+			tend[wv][lane] = inc;
+			td[wv][lane] = moff - cs;
 		}
+		// map[q] = j for the chunks whose first byte lies in segment j (ascending j)
+		for (uint32_t j = 0; j < ns; ++j) {
+			const uint32_t a = rdlane(cs, (int)j), b = rdlane(inc, (int)j);
+			for (uint32_t q = ((a + 15) >> 4) + (uint32_t)lane; q < ((b + 15) >> 4); q += 64) tmap[wv][q] = (uint8_t)j;
+		}
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 	};
 	// data loads: 16-byte chunk q = lane + 64 r of the chain (full chunks), and
 	// the bytes of the chunks a boundary cuts (items lane, lane + 64: boundary
@@ -2107,39 +2118,36 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 	auto data_issue = [&]() {
 		const uint32_t nr = (gL + 1023) >> 10;
 		full = 0;
+		uint32_t sj[kLcSlots];
+#pragma unroll
+		for (uint32_t r = 0; r < kLcSlots; ++r)
+			if (r < nr) sj[r] = tmap[wv][(uint32_t)lane + 64u * r];
 #pragma unroll
 		for (uint32_t r = 0; r < kLcSlots; ++r) {
 			if (r < nr) {
 				const uint32_t q16 = 16u * ((uint32_t)lane + 64u * r);
-				uint64_t d = gd[0];
-				uint32_t e = gend[0];
-#pragma unroll
-				for (uint32_t j = 1; j < kLChainSegs; ++j) {
-					const bool m = j < gns && gcs[j] <= q16;
-					d = m ? gd[j] : d;
-					e = m ? gend[j] : e;
-				}
-				const bool f = q16 + 16u <= e;  // (e <= gL)
+				const uint32_t j = q16 < gL ? sj[r] : 0u;
+				const uint64_t d = td[wv][j];
+				const uint32_t e = tend[wv][j];
+				const bool f = q16 < gL && q16 + 16u <= e;  // (e <= gL)
 				full |= f ? 1u << r : 0u;
-#ifdef FDBXXH_LC_NOLOAD
-				R[r] = u64x2u{d, (uint64_t)f};  // timing experiment: no data loads (wrong results)
-#else
 				R[r] = __builtin_nontemporal_load((g_u64x2u_*)(f ? base + d + q16 : dummy));
-#endif
 			}
 		}
 #pragma unroll
 		for (int v = 0; v < 2; ++v) {
 			const uint32_t it = (uint32_t)lane + 64u * v, p = it >> 4;
-			uint32_t bp = gend[0];
-#pragma unroll
-			for (uint32_t j = 1; j < kLChainSegs; ++j) bp = p == j ? gend[j] : bp;
+			const uint32_t bp = tend[wv][p & (kLChainSegs - 1)];
 			const uint32_t e = (bp & ~15u) + (it & 15u);
-			uint64_t d = gd[0];
-#pragma unroll
-			for (uint32_t j = 1; j < kLChainSegs; ++j) d = (j < gns && gcs[j] <= e) ? gd[j] : d;
 			const bool on = p < gns && (bp & 15u) != 0 && e < gL;
-			const uint64_t a = on ? base + d + e : dummy;
+			// the segment holding byte e: the one holding its chunk's first byte, or a later one
+			uint32_t j = on ? tmap[wv][e >> 4] : 0u;
+			for (;;) {
+				const bool step = on && j + 1 < gns && tcs[wv][(j + 1) & (kLChainSegs - 1)] <= e;
+				if (__ballot(step) == 0) break;
+				j += step ? 1u : 0u;
+			}
+			const uint64_t a = on ? base + td[wv][j] + e : dummy;
 			bon[v] = on;
 			bo[v] = e | ((uint32_t)a & 3u) << 16;  // (the byte's place in its dword, extracted at the commit)
 			typedef __attribute__((address_space(1))) const uint32_t g_u32_;
