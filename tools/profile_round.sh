@@ -35,6 +35,7 @@ for w in pages8k zipf zipf-scattered chunks xxh3-pages4k xxh3-zipf xxh3-chunks x
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_$w -o $w -- python bench.py --workload $w --steps 20 --cpu-seconds 0 --no-verify > $R/prof_$w.log 2>&1 || exit 1
 done
 echo rocprof done
+[ "${PMC:-1}" = 1 ] || exit 0  # (PMC=0: kernel traces only)
 for MODE in pages4k pages8k xxh3 zipf chunks xchunks xzipf scattered; do
   for spec in "fetch FETCH_SIZE" "write WRITE_SIZE" "sq GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD"; do
     set -- $spec; name=$1; shift
