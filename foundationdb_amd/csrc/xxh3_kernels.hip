@@ -2061,13 +2061,23 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 	// chain t's list entry: chain index, first segment, segment count
 	uint64_t ec1 = 0, es1 = 0;
 	uint32_t en1 = 0;
-	auto entry = [&](uint64_t i, uint64_t& c, uint64_t& s0, uint32_t& ns, uint64_t& sdv) {
-		const uint64_t a = lx[2 * i], b = lx[2 * i + 1];
+	// List entries and seeds by vector loads (every lane the same address),
+	// issued a chain ahead of their use and ahead of the data loads of the
+	// chain in flight, so that reading them waits for nothing: a scalar load
+	// is waited for at the next LDS wait (lgkmcnt counts both), one read at
+	// its use held up the metadata loads behind it every chain.
+	typedef uint64_t u64x2e __attribute__((ext_vector_type(2)));
+	typedef __attribute__((address_space(1))) const u64x2e g_u64x2e;
+	const uint64_t lgx = reinterpret_cast<uint64_t>(P.list + 2 * P.lcap * x);  // (16-byte aligned entries)
+	u64x2e eraw = u64x2e{0, 0};
+	auto entry_load = [&](uint64_t i) { eraw = *(g_u64x2e*)(lgx + 16 * i); };
+	auto entry_take = [&](uint64_t& c, uint64_t& s0, uint32_t& ns) {
+		const uint64_t a = rdfirst64v(eraw[0]), b = rdfirst64v(eraw[1]);
 		c = a;
 		s0 = b & ((1ull << 56) - 1);
 		ns = (uint32_t)(b >> 56);
-		sdv = P.seeds ? *(k_u64*)(P.seeds + a) : P.seed;
 	};
+	auto seed_load = [&](uint64_t c) -> uint64_t { return P.seeds ? P.seeds[c] : P.seed; };
 	// segment metadata in lanes 0 .. ns-1
 	uint64_t moff = 0;
 	uint32_t mlen = 0;
@@ -2170,35 +2180,43 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 	};
 
-	// prologue: the first chain's geometry and data in flight, the next one's metadata
+	// prologue: the first chain's geometry and data in flight, the second one's
+	// entry, seed and metadata, the third one's entry
 	uint64_t c0, s00;
 	uint32_t n0;
-	uint64_t sd0 = 0, esd1 = 0;
-	entry(wx, c0, s00, n0, sd0);
+	entry_load(wx);
+	entry_take(c0, s00, n0);
+	uint64_t sdr0 = seed_load(c0), sdr1 = 0;  // (vector: read a chain later)
 	meta_issue(s00, n0);
 	geometry(n0);
-	data_issue();
 	uint64_t i1 = wx + nwx;
 	if (i1 < nx) {
-		entry(i1, ec1, es1, en1, esd1);
+		entry_load(i1);
+		entry_take(ec1, es1, en1);
+		sdr1 = seed_load(ec1);
 		meta_issue(es1, en1);
+		if (i1 + nwx < nx) entry_load(i1 + nwx);
 	}
+	data_issue();
 	for (uint64_t i = wx; i < nx; i += nwx) {
 		const uint32_t len = gL;
 		const uint64_t c = c0;
-		const uint64_t sd = sd0;
-		data_commit();  // this chain in LDS
-		// the next chain: its data in flight while this one is hashed; the one after: its metadata
+		data_commit();  // this chain in LDS (its data were the last loads issued)
+		const uint64_t sd = rdfirst64v(sdr0);  // (issued before that data)
+		// the next chain: its geometry, then its data in flight while this one is
+		// hashed; the one after: its seed and metadata, then the entry after that
 		if (i1 < nx) {
 			c0 = ec1;
-			sd0 = esd1;
+			sdr0 = sdr1;
 			geometry(en1);
-			data_issue();
 			i1 += nwx;
 			if (i1 < nx) {
-				entry(i1, ec1, es1, en1, esd1);
+				entry_take(ec1, es1, en1);
+				sdr1 = seed_load(ec1);
 				meta_issue(es1, en1);
+				if (i1 + nwx < nx) entry_load(i1 + nwx);
 			}
+			data_issue();
 		}
 		uint64_t h;
 #ifdef FDBXXH_LC_NOHASH
