@@ -2040,7 +2040,6 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 	__shared__ uint64_t ks[25];
 	__shared__ uint32_t tcs[4][kLChainSegs], tend[4][kLChainSegs];  // per wave: the chain's segment table
 	__shared__ uint64_t td[4][kLChainSegs];
-	__shared__ uint8_t tmap[4][kLChainMax / 16];                    // ... and its chunk -> segment map
 	if (threadIdx.x < 25) ks[threadIdx.x] = threadIdx.x < 24 ? kSec[threadIdx.x] : 0;
 	__syncthreads();
 	const int lane = threadIdx.x & 63;
@@ -2086,12 +2085,20 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 		moff = P.seg_off[j];
 		mlen = reinterpret_cast<const uint32_t*>(P.seg_len)[2 * j];  // (the low word: a chain here is under 2^14 bytes; a dead high word's load held up the register's next use)
 	};
-	// The geometry derived from the metadata, as LDS tables of the wave: per
-	// segment its chain offset, end and source displacement (address - chain
-	// offset), and per 16-byte chunk of the chain the segment holding its first
-	// byte (a chunk -> segment map: a chunk's segment is two LDS reads, where a
-	// search over the segments held in SGPRs cost ~90 instructions per chunk).
+	// The geometry derived from the metadata: per segment its chain offset, end
+	// and source displacement (address - chain offset) as LDS tables of the
+	// wave, read by segment index -- a position's segment is a count over the
+	// segment starts held in SGPRs (selecting each field over the segments in
+	// SGPRs cost ~90 instructions per chunk, a chunk -> segment map in LDS its
+	// byte writes).
 	uint32_t gns = 0, gL = 0;
+	uint32_t gst[kLChainSegs];  // [1 ..]: segment starts (past the chain: ~0)
+	auto seg_of = [&](uint32_t pos) {
+		uint32_t j = 0;
+#pragma unroll
+		for (uint32_t k = 1; k < kLChainSegs; ++k) j += gst[k] <= pos ? 1u : 0u;
+		return j;
+	};
 	auto geometry = [&](uint32_t ns) {
 		uint32_t len = (uint32_t)lane < ns ? mlen : 0u;  // (a chain of this route is under 2^14 bytes)
 		uint32_t inc = len;
@@ -2108,11 +2115,11 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 			tend[wv][lane] = inc;
 			td[wv][lane] = moff - cs;
 		}
-		// map[q] = j for the chunks whose first byte lies in segment j (ascending j)
-		for (uint32_t j = 0; j < ns; ++j) {
-			const uint32_t a = rdlane(cs, (int)j), b = rdlane(inc, (int)j);
-			for (uint32_t q = ((a + 15) >> 4) + (uint32_t)lane; q < ((b + 15) >> 4); q += 64) tmap[wv][q] = (uint8_t)j;
-		}
+		// the segment starts (but the first) in SGPRs: a position's segment is
+		// the count of starts at or below it (a chunk map in LDS cost its byte
+		// writes: 70 us of the bench's step)
+#pragma unroll
+		for (uint32_t j = 1; j < kLChainSegs; ++j) gst[j] = j < ns ? rdlane(cs, (int)j) : 0xFFFFFFFFu;
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 		__builtin_amdgcn_wave_barrier();
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2128,15 +2135,11 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 	auto data_issue = [&]() {
 		const uint32_t nr = (gL + 1023) >> 10;
 		full = 0;
-		uint32_t sj[kLcSlots];
-#pragma unroll
-		for (uint32_t r = 0; r < kLcSlots; ++r)
-			if (r < nr) sj[r] = tmap[wv][(uint32_t)lane + 64u * r];
 #pragma unroll
 		for (uint32_t r = 0; r < kLcSlots; ++r) {
 			if (r < nr) {
 				const uint32_t q16 = 16u * ((uint32_t)lane + 64u * r);
-				const uint32_t j = q16 < gL ? sj[r] : 0u;
+				const uint32_t j = seg_of(q16);
 				const uint64_t d = td[wv][j];
 				const uint32_t e = tend[wv][j];
 				const bool f = q16 < gL && q16 + 16u <= e;  // (e <= gL)
@@ -2146,17 +2149,15 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 		}
 #pragma unroll
 		for (int v = 0; v < 2; ++v) {
+#ifdef FDBXXH_LC_NOBYTES
+			bon[v] = false;  // timing experiment: no cut bytes (wrong results)
+			continue;
+#endif
 			const uint32_t it = (uint32_t)lane + 64u * v, p = it >> 4;
 			const uint32_t bp = tend[wv][p & (kLChainSegs - 1)];
 			const uint32_t e = (bp & ~15u) + (it & 15u);
 			const bool on = p < gns && (bp & 15u) != 0 && e < gL;
-			// the segment holding byte e: the one holding its chunk's first byte, or a later one
-			uint32_t j = on ? tmap[wv][e >> 4] : 0u;
-			for (;;) {
-				const bool step = on && j + 1 < gns && tcs[wv][(j + 1) & (kLChainSegs - 1)] <= e;
-				if (__ballot(step) == 0) break;
-				j += step ? 1u : 0u;
-			}
+			const uint32_t j = seg_of(e);  // (e < gL: a segment of the chain)
 			const uint64_t a = on ? base + td[wv][j] + e : dummy;
 			bon[v] = on;
 			bo[v] = e | ((uint32_t)a & 3u) << 16;  // (the byte's place in its dword, extracted at the commit)
@@ -2168,7 +2169,11 @@ __global__ __launch_bounds__(256) void k_xxh3_lchain(LChainP P) {
 		const uint32_t nr = (gL + 1023) >> 10;
 #pragma unroll
 		for (uint32_t r = 0; r < kLcSlots; ++r)
+#ifdef FDBXXH_LC_NOCOMMIT
+			if (r == 99) {  // timing experiment: no stage writes (wrong results)
+#else
 			if (r < nr && (full >> r & 1u)) {
+#endif
 				typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
 				*reinterpret_cast<u64x2a*>(L + 4u * ((uint32_t)lane + 64u * r)) = u64x2a{R[r][0], R[r][1]};
 			}
