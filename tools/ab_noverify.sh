@@ -1,7 +1,7 @@
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab
-for L in "" nomap nobytes nocommit; do
+for L in "" ${LIBS:-}; do
   lib=""; [ -n "$L" ] && lib=$PWD/foundationdb_amd/lib/libfdb_crc32c_$L.so
   d=gpurun_out/ab/nv-${L:-prod}
   FDBCRC_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o k -- python bench.py --workload xxh3-chained --steps 20 --cpu-seconds 0 --no-verify > $d.json 2> $d.err || { tail -3 $d.err; exit 1; }
